@@ -1,0 +1,809 @@
+// C++ host runtime behind the C ABI (include/ctok.h): tokenizer.json loader, table compiler,
+// per-device workspace and the stream-ordered encode pipeline.
+//
+// Reference counterparts (Complexity-ML/complexity-tokenizer v0.3.3):
+//   loader            src/huggingface/mod.rs:32-116 (schema), :159-166 (from_file), :247-334
+//   merge table       src/bpe.rs:52-79 (BpeTokenizer::new)
+//   normaliser choice src/huggingface/parsing.rs:10-90 (NFC default at :89)
+//   pre-tokenizer     src/huggingface/parsing.rs:92-190; src/pretokenizers.rs:71-126, :298-302
+//   vocab getters     src/vocab.rs:34-100, src/huggingface/mod.rs:856-866
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <functional>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <sstream>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/ctok.h"
+#include "ctok_internal.h"
+#include "gen/unicode_data.h"
+#include "json.hpp"
+
+using namespace ctok_dev;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+struct CtokError {
+  int code;
+  std::string msg;
+};
+
+[[noreturn]] void throw_err(int code, const std::string& msg) { throw CtokError{code, msg}; }
+
+#define HIPTRY(x)                                                                                   \
+  do {                                                                                              \
+    hipError_t e_ = (x);                                                                            \
+    if (e_ != hipSuccess) throw_err(CTOK_E_DEVICE, std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+// ----------------------------------------------------------------------------- byte map
+// GPT-2 bytes_to_unicode (src/pretokenizers.rs:130-153): byte -> code point
+std::vector<uint32_t> byte_map() {
+  std::vector<int> bs;
+  for (int b = '!'; b <= '~'; b++) bs.push_back(b);
+  for (int b = 0xA1; b <= 0xAC; b++) bs.push_back(b);
+  for (int b = 0xAE; b <= 0xFF; b++) bs.push_back(b);
+  std::vector<uint32_t> cs(bs.begin(), bs.end());
+  uint32_t n = 0;
+  std::vector<bool> in(256, false);
+  for (int b : bs) in[b] = true;
+  for (int b = 0; b < 256; b++)
+    if (!in[b]) { bs.push_back(b); cs.push_back(256 + n++); }
+  std::vector<uint32_t> m(256);
+  for (size_t i = 0; i < 256; i++) m[bs[i]] = cs[i];
+  return m;
+}
+
+std::string utf8(uint32_t cp) {
+  std::string o;
+  if (cp < 0x80) o += (char)cp;
+  else if (cp < 0x800) { o += (char)(0xC0 | (cp >> 6)); o += (char)(0x80 | (cp & 0x3F)); }
+  else if (cp < 0x10000) { o += (char)(0xE0 | (cp >> 12)); o += (char)(0x80 | ((cp >> 6) & 0x3F)); o += (char)(0x80 | (cp & 0x3F)); }
+  else { o += (char)(0xF0 | (cp >> 18)); o += (char)(0x80 | ((cp >> 12) & 0x3F)); o += (char)(0x80 | ((cp >> 6) & 0x3F)); o += (char)(0x80 | (cp & 0x3F)); }
+  return o;
+}
+
+bool decode_utf8(const std::string& s, std::vector<uint32_t>& out) {
+  out.clear();
+  for (size_t i = 0; i < s.size();) {
+    uint8_t b = (uint8_t)s[i];
+    int len = b < 0x80 ? 1 : (b >> 5) == 6 ? 2 : (b >> 4) == 14 ? 3 : (b >> 3) == 30 ? 4 : 0;
+    if (!len || i + len > s.size()) return false;
+    uint32_t cp = len == 1 ? b : len == 2 ? (b & 0x1Fu) : len == 3 ? (b & 0x0Fu) : (b & 0x07u);
+    for (int k = 1; k < len; k++) cp = (cp << 6) | ((uint8_t)s[i + k] & 0x3Fu);
+    out.push_back(cp);
+    i += len;
+  }
+  return true;
+}
+
+int host_cls(uint32_t cp) {
+  if (cp >= 0x110000) return 3;
+  uint32_t w = ct_cls_stage2[ct_cls_stage1[cp >> 8] * 64 + ((cp & 255) >> 2)];
+  return (w >> ((cp & 3) * 2)) & 3;
+}
+
+// Can the raw byte string `pat` occur inside one GPT2_PATTERN piece?  Pieces are: a run of
+// White_Space; an optional leading U+0020 plus a run of one class among {L, N, other}; or a
+// contraction 's 't 're 've 'm 'll 'd.  Conservative: true unless provably impossible.
+bool can_occur_in_piece(const std::string& pat) {
+  if (pat.empty()) return true;
+  static const char* con[] = {"'s", "'t", "'re", "'ve", "'m", "'ll", "'d"};
+  for (const char* c : con)
+    if (std::string(c).find(pat) != std::string::npos) return true;
+  size_t i = 0;
+  bool lead_partial = false;
+  while (i < pat.size() && ((uint8_t)pat[i] & 0xC0) == 0x80) { i++; lead_partial = true; }
+  std::vector<int> cls;
+  std::vector<uint32_t> cps;
+  while (i < pat.size()) {
+    uint8_t b = (uint8_t)pat[i];
+    int len = b < 0x80 ? 1 : (b >> 5) == 6 ? 2 : (b >> 4) == 14 ? 3 : 4;
+    if (i + len > pat.size()) break;  // trailing partial code point: class unknown
+    uint32_t cp = len == 1 ? b : len == 2 ? (b & 0x1Fu) : len == 3 ? (b & 0x0Fu) : (b & 0x07u);
+    for (int k = 1; k < len; k++) cp = (cp << 6) | ((uint8_t)pat[i + k] & 0x3Fu);
+    cps.push_back(cp);
+    cls.push_back(host_cls(cp));
+    i += len;
+  }
+  if (cls.empty()) return true;
+  bool all_ws = std::all_of(cls.begin(), cls.end(), [](int c) { return c == 0; });
+  if (all_ws) return true;
+  size_t k = 0;
+  if (!lead_partial && cps[0] == ' ') k = 1;
+  int want = -1;
+  for (; k < cls.size(); k++) {
+    if (cls[k] == 0) return false;
+    if (want < 0) want = cls[k];
+    else if (cls[k] != want) return false;
+  }
+  return true;
+}
+
+// ----------------------------------------------------------------------------- device state
+
+template <typename T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t cap = 0;  // elements
+  void ensure(size_t n) {
+    if (n <= cap && p) return;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    size_t want = std::max<size_t>(n + n / 4, 1024);
+    HIPTRY(hipMalloc((void**)&p, want * sizeof(T)));
+    cap = want;
+  }
+  ~DevBuf() { if (p) (void)hipFree(p); }
+};
+
+struct DeviceState {
+  int device = -1;
+  std::mutex mu;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev[8] = {};
+  // tables
+  DevBuf<uint64_t> merge_tab;
+  DevBuf<uint32_t> rank_newid;
+  DevBuf<int32_t> byte2id;
+  DevBuf<uint8_t> cls_s1, cls_s2, nfc_s1, alnum, at_bytes, at_flags;
+  DevBuf<uint16_t> nfc_s2, decomp_off;
+  DevBuf<uint32_t> decomp_cp, decomp_data, comp_val, at_off, at_id;
+  DevBuf<uint64_t> comp_key;
+  Tables t{};
+  // workspace
+  DevBuf<uint32_t> docbits, pbits, tile_cnt, word_prefix, pstart, pcnt, scratch, doc_piece, long_list, counters, lw;
+  DevBuf<uint64_t> scan_tmp;
+  DevBuf<uint32_t> doc_flag, ncp;
+  DevBuf<uint64_t> norm_off;
+  DevBuf<uint8_t> norm_text;
+  // host-API staging
+  DevBuf<uint8_t> in_text;
+  DevBuf<uint64_t> in_off, out_off;
+  DevBuf<uint32_t> out_ids;
+  ~DeviceState() {
+    if (device >= 0) {
+      (void)hipSetDevice(device);
+      for (auto& e : ev) if (e) (void)hipEventDestroy(e);
+      if (stream) (void)hipStreamDestroy(stream);
+    }
+  }
+};
+
+}  // namespace
+
+// ----------------------------------------------------------------------------- tokenizer
+
+struct ctok {
+  // host-side model (immutable after load)
+  std::unordered_map<std::string, uint32_t> vocab;          // model.vocab
+  std::unordered_map<uint32_t, std::string> id_to_token;    // Vocab::id_to_token
+  std::vector<std::pair<std::string, uint32_t>> special;    // special added tokens
+  bool nfc = true;
+  bool add_prefix_space = false;
+  // compiled tables
+  std::vector<uint64_t> merge_tab;
+  uint32_t merge_mask = 0;
+  std::vector<uint32_t> rank_newid;
+  int32_t byte2id[256];
+  std::string at_bytes;
+  std::vector<uint32_t> at_off{0}, at_id;
+  std::vector<uint8_t> at_flags;
+  bool proper = true;
+  // per device
+  std::mutex dev_mu;
+  std::map<int, std::unique_ptr<DeviceState>> devs;
+};
+
+namespace {
+
+bool get_bool_field(const ctj::Value& o, const char* k, bool dflt, const char* ctx) {
+  const ctj::Value* v = o.get(k);
+  if (!v) return dflt;
+  if (v->kind != ctj::Value::Bool) throw_err(CTOK_E_PARSE, std::string("invalid type for `") + k + "` in " + ctx + ", expected a boolean");
+  return v->b;
+}
+
+// parse_normalizer (src/huggingface/parsing.rs:10-90): 1 = NFC, 0 = none
+int parse_normalizer(const ctj::Value* v) {
+  if (v && v->kind == ctj::Value::Object) {
+    const ctj::Value* t = v->get("type");
+    if (t) {
+      std::string ty = t->kind == ctj::Value::String ? t->s : "";
+      if (ty == "NFC") return 1;
+      if (ty == "Sequence") {
+        const ctj::Value* ns = v->get("normalizers");
+        if (!ns || ns->kind != ctj::Value::Array) return 0;
+        int any = 0;
+        for (const auto& n : ns->arr) any |= parse_normalizer(&n);  // NFC is idempotent
+        return any;
+      }
+      static const char* unsup[] = {"NFD", "NFKC", "NFKD", "Lowercase", "Strip", "StripAccents", "Replace",
+                                    "Prepend", "BertNormalizer", "Precompiled"};
+      for (const char* u : unsup)
+        if (ty == u) throw_err(CTOK_E_UNSUPPORTED, "normalizer `" + ty + "` is outside the encode hot path (only NFC / none)");
+      return 0;
+    }
+  }
+  return 1;  // null, absent, or an object without "type": NFC (parsing.rs:89)
+}
+
+bool rust_regex_compiles(const std::string& p) {
+  for (const char* bad : {"(?=", "(?!", "(?<=", "(?<!", "(?>"})
+    if (p.find(bad) != std::string::npos) return false;
+  for (size_t i = 0; i + 1 < p.size(); i++)
+    if (p[i] == '\\' && p[i + 1] >= '1' && p[i + 1] <= '9') return false;
+  return true;
+}
+
+// flattens parse_pre_tokenizer (src/huggingface/parsing.rs:92-190) into the supported chain:
+// no-op Splits (patterns the Rust regex crate rejects, src/pretokenizers.rs:298-302) around
+// exactly one ByteLevel.  kinds: 'B' ByteLevel, 'S' no-op split
+void parse_pre_tokenizer(const ctj::Value* v, std::vector<std::pair<char, bool>>& chain, int depth) {
+  if (!(v && v->kind == ctj::Value::Object && v->get("type"))) {
+    if (depth == 0) { chain.push_back({'B', false}); return; }  // default ByteLevel(false)
+    throw_err(CTOK_E_UNSUPPORTED, "pre_tokenizer entry without a type");
+  }
+  const ctj::Value* t = v->get("type");
+  std::string ty = t->kind == ctj::Value::String ? t->s : "";
+  if (ty == "ByteLevel") {
+    const ctj::Value* a = v->get("add_prefix_space");
+    chain.push_back({'B', a && a->kind == ctj::Value::Bool ? a->b : false});
+  } else if (ty == "Split") {
+    std::string pat;
+    const ctj::Value* p = v->get("pattern");
+    if (p && p->kind == ctj::Value::Object) {
+      const ctj::Value* r = p->get("Regex");
+      if (r && r->kind == ctj::Value::String) pat = r->s;
+    }
+    if (rust_regex_compiles(pat))
+      throw_err(CTOK_E_UNSUPPORTED, "Split pre-tokenizer with a pattern the Rust regex crate compiles is outside the encode hot path");
+    chain.push_back({'S', false});
+  } else if (ty == "Sequence" && depth == 0) {
+    const ctj::Value* ps = v->get("pretokenizers");
+    if (!ps || ps->kind != ctj::Value::Array || ps->arr.empty())
+      throw_err(CTOK_E_UNSUPPORTED, "empty pre_tokenizer Sequence (no byte-level split)");
+    for (const auto& e : ps->arr) parse_pre_tokenizer(&e, chain, depth + 1);
+  } else {
+    throw_err(CTOK_E_UNSUPPORTED, "pre_tokenizer `" + ty + "` is outside the encode hot path (ByteLevel only)");
+  }
+}
+
+uint32_t mhash_host(uint32_t a, uint32_t b) {
+  uint32_t h = a * 0x9E3779B1u ^ (b + 0x7F4A7C15u) * 0x85EBCA77u;
+  return h ^ (h >> 15);
+}
+
+void load(ctok* t, const char* buf, size_t len) {
+  ctj::Value root;
+  try {
+    root = ctj::parse(buf, len);
+  } catch (const ctj::ParseError& e) {
+    throw_err(CTOK_E_PARSE, e.what());
+  }
+  if (root.kind != ctj::Value::Object) throw_err(CTOK_E_PARSE, "invalid type: expected struct TokenizerJson");
+  const ctj::Value* model = root.get("model");
+  if (!model) throw_err(CTOK_E_PARSE, "missing field `model`");
+  if (model->kind != ctj::Value::Object) throw_err(CTOK_E_PARSE, "invalid type for `model`, expected struct ModelJson");
+  const ctj::Value* vocab = model->get("vocab");
+  if (!vocab) throw_err(CTOK_E_PARSE, "missing field `vocab`");
+  if (vocab->kind != ctj::Value::Object) throw_err(CTOK_E_PARSE, "invalid type for `vocab`, expected a map");
+  t->vocab.reserve(vocab->obj.size() * 2);
+  for (const auto& m : vocab->obj) {
+    if (!m.second.is_u32()) throw_err(CTOK_E_PARSE, "invalid value for vocab entry `" + m.first + "`, expected u32");
+    t->vocab[m.first] = (uint32_t)m.second.u;  // HashMap insert: a later duplicate key wins
+  }
+  for (const auto& kv : t->vocab) t->id_to_token[kv.second] = kv.first;
+
+  // merges: deserialize_merges (mod.rs:56-101) then split(' ') == 2 parts (mod.rs:252-264)
+  std::vector<std::pair<std::string, std::string>> merges;
+  if (const ctj::Value* mv = model->get("merges")) {
+    if (mv->kind != ctj::Value::Array) throw_err(CTOK_E_PARSE, "invalid type for `merges`, expected a sequence of strings or arrays of two strings");
+    merges.reserve(mv->arr.size());
+    for (const auto& it : mv->arr) {
+      std::string s;
+      if (it.kind == ctj::Value::String) s = it.s;
+      else if (it.kind == ctj::Value::Array && it.arr.size() == 2 && it.arr[0].kind == ctj::Value::String &&
+               it.arr[1].kind == ctj::Value::String) s = it.arr[0].s + " " + it.arr[1].s;
+      else continue;
+      size_t sp = s.find(' ');
+      if (sp == std::string::npos || s.find(' ', sp + 1) != std::string::npos) continue;
+      merges.emplace_back(s.substr(0, sp), s.substr(sp + 1));
+    }
+  }
+  // BpeTokenizer::new (src/bpe.rs:52-79)
+  std::unordered_map<uint64_t, uint32_t> ranks;  // (a<<32|b) -> rank, last duplicate wins
+  ranks.reserve(merges.size() * 2);
+  std::vector<uint32_t> valid_new;
+  for (size_t r = 0; r < merges.size(); r++) {
+    auto ia = t->vocab.find(merges[r].first);
+    auto ib = t->vocab.find(merges[r].second);
+    if (ia == t->vocab.end() || ib == t->vocab.end()) continue;
+    auto in = t->vocab.find(merges[r].first + merges[r].second);
+    if (in == t->vocab.end()) continue;
+    ranks[((uint64_t)ia->second << 32) | ib->second] = (uint32_t)r;
+    valid_new.push_back(in->second);
+  }
+  if (merges.size() >= (size_t)kNoRank - 2) throw_err(CTOK_E_UNSUPPORTED, "more than 4M merges");
+  t->rank_newid = valid_new;
+  size_t cap = 1024;
+  while (cap < ranks.size() * 2 + 16) cap <<= 1;
+  t->merge_tab.assign(cap, kEmpty);
+  t->merge_mask = (uint32_t)(cap - 1);
+  for (const auto& kv : ranks) {
+    uint32_t a = (uint32_t)(kv.first >> 32), b = (uint32_t)kv.first;
+    if (a > kMaxId || b > kMaxId) throw_err(CTOK_E_UNSUPPORTED, "token ids above 2^21-2 are not supported by the device merge table");
+    uint64_t e = ((uint64_t)kv.second << 42) | ((uint64_t)a << kIdBits) | b;
+    uint32_t h = mhash_host(a, b) & t->merge_mask;
+    while (t->merge_tab[h] != kEmpty) h = (h + 1) & t->merge_mask;
+    t->merge_tab[h] = e;
+  }
+  for (uint32_t id : valid_new)
+    if (id > kMaxId) throw_err(CTOK_E_UNSUPPORTED, "token ids above 2^21-2 are not supported by the device merge table");
+  // rank monotonicity ("proper"): every merge consuming z ranks after every merge producing z
+  {
+    std::unordered_map<uint32_t, uint32_t> maxprod, mincons;
+    for (const auto& kv : ranks) {
+      uint32_t r = kv.second;
+      if (r >= valid_new.size()) continue;  // panics on lookup anyway
+      uint32_t z = valid_new[r];
+      auto it = maxprod.find(z);
+      if (it == maxprod.end() || it->second < r) maxprod[z] = r;
+      for (uint32_t c : {(uint32_t)(kv.first >> 32), (uint32_t)kv.first}) {
+        auto jt = mincons.find(c);
+        if (jt == mincons.end() || jt->second > r) mincons[c] = r;
+      }
+    }
+    t->proper = true;
+    for (const auto& kv : maxprod) {
+      auto jt = mincons.find(kv.first);
+      if (jt != mincons.end() && jt->second <= kv.second) { t->proper = false; break; }
+    }
+  }
+
+  // byte-level initial ids: vocab[bytes_to_unicode[b]] (src/bpe.rs:94-97), -1 = dropped
+  std::vector<uint32_t> bm = byte_map();
+  for (int b = 0; b < 256; b++) {
+    auto it = t->vocab.find(utf8(bm[b]));
+    t->byte2id[b] = it == t->vocab.end() ? -1 : (int32_t)it->second;
+  }
+
+  // added tokens (mod.rs:103-116 schema, :274-305 maps)
+  std::vector<std::pair<std::string, std::pair<uint32_t, uint8_t>>> added;  // content -> (id, flags)
+  if (const ctj::Value* at = root.get("added_tokens")) {
+    if (at->kind != ctj::Value::Array) throw_err(CTOK_E_PARSE, "invalid type for `added_tokens`, expected a sequence");
+    for (const auto& a : at->arr) {
+      if (a.kind != ctj::Value::Object) throw_err(CTOK_E_PARSE, "invalid type: expected struct AddedToken");
+      const ctj::Value* id = a.get("id");
+      const ctj::Value* content = a.get("content");
+      const ctj::Value* special = a.get("special");
+      if (!id) throw_err(CTOK_E_PARSE, "missing field `id`");
+      if (!content) throw_err(CTOK_E_PARSE, "missing field `content`");
+      if (!special) throw_err(CTOK_E_PARSE, "missing field `special`");
+      if (!id->is_u32()) throw_err(CTOK_E_PARSE, "invalid type for added token `id`, expected u32");
+      if (content->kind != ctj::Value::String) throw_err(CTOK_E_PARSE, "invalid type for added token `content`, expected a string");
+      if (special->kind != ctj::Value::Bool) throw_err(CTOK_E_PARSE, "invalid type for added token `special`, expected a boolean");
+      uint8_t flags = (get_bool_field(a, "single_word", false, "AddedToken") ? 1 : 0) |
+                      (get_bool_field(a, "lstrip", false, "AddedToken") ? 2 : 0) |
+                      (get_bool_field(a, "rstrip", false, "AddedToken") ? 4 : 0);
+      (void)get_bool_field(a, "normalized", false, "AddedToken");
+      bool replaced = false;
+      for (auto& e : added)
+        if (e.first == content->s) { e.second = {(uint32_t)id->u, flags}; replaced = true; }
+      if (!replaced) added.push_back({content->s, {(uint32_t)id->u, flags}});
+      if (special->b) {
+        bool rep = false;
+        for (auto& e : t->special)
+          if (e.first == content->s) { e.second = (uint32_t)id->u; rep = true; }
+        if (!rep) t->special.push_back({content->s, (uint32_t)id->u});
+      }
+    }
+  }
+  // added tokens that can match inside a byte-mapped word, as raw-byte patterns
+  std::unordered_map<uint32_t, int> inv;  // mapped code point -> byte
+  for (int b = 0; b < 256; b++) inv[bm[b]] = b;
+  for (const auto& e : added) {
+    if (e.first.empty()) throw_err(CTOK_E_UNSUPPORTED, "added token with empty content: the reference's word loop never terminates (src/huggingface/mod.rs:569-610)");
+    std::vector<uint32_t> cps;
+    if (!decode_utf8(e.first, cps)) continue;
+    std::string raw;
+    bool ok = true;
+    for (uint32_t c : cps) {
+      auto it = inv.find(c);
+      if (it == inv.end()) { ok = false; break; }
+      raw += (char)it->second;
+    }
+    if (!ok || !can_occur_in_piece(raw)) continue;  // provably never matches inside a piece
+    t->at_bytes += raw;
+    t->at_off.push_back((uint32_t)t->at_bytes.size());
+    t->at_id.push_back(e.second.first);
+    t->at_flags.push_back(e.second.second);
+  }
+
+  t->nfc = parse_normalizer(root.get("normalizer")) != 0;
+  std::vector<std::pair<char, bool>> chain;
+  parse_pre_tokenizer(root.get("pre_tokenizer"), chain, 0);
+  int nbl = 0;
+  for (auto& c : chain)
+    if (c.first == 'B') { nbl++; t->add_prefix_space = c.second; }
+  if (nbl != 1) throw_err(CTOK_E_UNSUPPORTED, "pre_tokenizer must contain exactly one ByteLevel");
+}
+
+template <typename T>
+void upload(DevBuf<T>& b, const T* src, size_t n, hipStream_t s) {
+  b.ensure(n ? n : 1);
+  if (n) HIPTRY(hipMemcpyAsync(b.p, src, n * sizeof(T), hipMemcpyHostToDevice, s));
+}
+
+DeviceState* device_state(ctok* t, int device) {
+  std::lock_guard<std::mutex> lk(t->dev_mu);
+  auto it = t->devs.find(device);
+  if (it != t->devs.end()) return it->second.get();
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) throw_err(CTOK_E_DEVICE, "no HIP device visible (the encode path has no CPU fallback)");
+  if (device < 0 || device >= n) throw_err(CTOK_E_ARG, "device ordinal out of range");
+  HIPTRY(hipSetDevice(device));
+  auto ds = std::make_unique<DeviceState>();
+  ds->device = device;
+  HIPTRY(hipStreamCreateWithFlags(&ds->stream, hipStreamNonBlocking));
+  for (auto& e : ds->ev) HIPTRY(hipEventCreate(&e));
+  hipStream_t s = ds->stream;
+  upload(ds->merge_tab, t->merge_tab.data(), t->merge_tab.size(), s);
+  upload(ds->rank_newid, t->rank_newid.data(), t->rank_newid.size(), s);
+  upload(ds->byte2id, t->byte2id, 256, s);
+  upload(ds->cls_s1, ct_cls_stage1, sizeof(ct_cls_stage1), s);
+  upload(ds->cls_s2, ct_cls_stage2, sizeof(ct_cls_stage2), s);
+  upload(ds->nfc_s1, ct_nfc_stage1, sizeof(ct_nfc_stage1), s);
+  upload(ds->nfc_s2, ct_nfc_stage2, sizeof(ct_nfc_stage2) / 2, s);
+  upload(ds->decomp_cp, ct_decomp_cp, CT_DECOMP_N, s);
+  upload(ds->decomp_off, ct_decomp_off, CT_DECOMP_N + 1, s);
+  upload(ds->decomp_data, ct_decomp_data, CT_DECOMP_DATA_N, s);
+  upload(ds->comp_key, (const uint64_t*)ct_comp_key, CT_COMP_N, s);
+  upload(ds->comp_val, ct_comp_val, CT_COMP_N, s);
+  upload(ds->alnum, ct_bytemap_alnum, 256, s);
+  upload(ds->at_bytes, (const uint8_t*)t->at_bytes.data(), t->at_bytes.size(), s);
+  upload(ds->at_off, t->at_off.data(), t->at_off.size(), s);
+  upload(ds->at_id, t->at_id.data(), t->at_id.size(), s);
+  upload(ds->at_flags, t->at_flags.data(), t->at_flags.size(), s);
+  HIPTRY(hipStreamSynchronize(s));
+  Tables& tb = ds->t;
+  tb.merge_tab = ds->merge_tab.p;
+  tb.merge_mask = t->merge_mask;
+  tb.rank_newid = ds->rank_newid.p;
+  tb.n_ranks = (uint32_t)t->rank_newid.size();
+  tb.byte2id = ds->byte2id.p;
+  tb.cls_s1 = ds->cls_s1.p;
+  tb.cls_s2 = ds->cls_s2.p;
+  tb.nfc_s1 = ds->nfc_s1.p;
+  tb.nfc_s2 = ds->nfc_s2.p;
+  tb.decomp_cp = ds->decomp_cp.p;
+  tb.decomp_off = ds->decomp_off.p;
+  tb.decomp_data = ds->decomp_data.p;
+  tb.n_decomp = CT_DECOMP_N;
+  tb.comp_key = ds->comp_key.p;
+  tb.comp_val = ds->comp_val.p;
+  tb.n_comp = CT_COMP_N;
+  tb.bytemap_alnum = ds->alnum.p;
+  tb.at_bytes = ds->at_bytes.p;
+  tb.at_off = ds->at_off.p;
+  tb.at_id = ds->at_id.p;
+  tb.at_flags = ds->at_flags.p;
+  tb.n_at = (uint32_t)t->at_id.size();
+  tb.proper = (t->proper && !getenv("CTOK_FORCE_IMPROPER")) ? 1 : 0;
+  tb.dbg = getenv("CTOK_DBG_MODE") ? (uint32_t)atoi(getenv("CTOK_DBG_MODE")) : 0;
+  DeviceState* r = ds.get();
+  t->devs[device] = std::move(ds);
+  return r;
+}
+
+bool debug_sync() {
+  static int v = -1;
+  if (v < 0) v = getenv("CTOK_DEBUG_SYNC") ? 1 : 0;
+  return v == 1;
+}
+
+#define STEP(name, x)                                                                    \
+  do {                                                                                   \
+    HIPTRY(x);                                                                           \
+    if (debug_sync()) {                                                                  \
+      fprintf(stderr, "[ctok] %s launched\n", name);                                     \
+      HIPTRY(hipStreamSynchronize(s));                                                   \
+      fprintf(stderr, "[ctok] %s done\n", name);                                         \
+    }                                                                                    \
+  } while (0)
+
+double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// The pipeline on device-resident buffers.  Returns the token count.
+uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const uint64_t* d_off, uint64_t n_docs,
+                       uint64_t n_bytes, uint32_t* d_ids, uint64_t ids_cap, uint64_t* d_tok_off, hipStream_t s,
+                       bool timing, ctok_stats* st) {
+  if (n_bytes >= 0xF0000000ull) throw_err(CTOK_E_ARG, "a single call is limited to < 3.75 GiB of text; split the batch");
+  if (n_docs >= 0xF0000000ull) throw_err(CTOK_E_ARG, "too many documents in one call");
+  const Tables& tb = ds->t;
+  if (timing) HIPTRY(hipEventRecord(ds->ev[0], s));
+
+  ds->counters.ensure(8);
+  HIPTRY(hipMemsetAsync(ds->counters.p, 0, 8 * 4, s));
+  const uint8_t* text = d_text;
+  const uint64_t* off = d_off;
+  uint64_t B = n_bytes;
+  uint64_t nfc_docs = 0;
+  bool norm = t->add_prefix_space;
+  if (t->nfc && n_bytes) {
+    ds->doc_flag.ensure(n_docs + 1);
+    HIPTRY(hipMemsetAsync(ds->doc_flag.p, 0, (n_docs + 1) * 4, s));
+    STEP("nfc_check", launch_nfc_check(d_text, n_bytes, d_off, (uint32_t)n_docs, tb, ds->doc_flag.p, ds->counters.p + 3, s));
+    uint32_t cnt = 0;
+    HIPTRY(hipMemcpyAsync(&cnt, ds->counters.p + 3, 4, hipMemcpyDeviceToHost, s));
+    HIPTRY(hipStreamSynchronize(s));
+    nfc_docs = cnt;
+    if (cnt) norm = true;
+  }
+  if (norm) {
+    ds->doc_flag.ensure(n_docs + 1);
+    if (!t->nfc) HIPTRY(hipMemsetAsync(ds->doc_flag.p, 0, (n_docs + 1) * 4, s));
+    ds->ncp.ensure(n_docs + 1);
+    ds->norm_off.ensure(n_docs + 2);
+    ds->lw.ensure(4 * n_bytes + 64);
+    STEP("norm0", launch_norm(d_text, d_off, (uint32_t)n_docs, ds->doc_flag.p, t->add_prefix_space, t->nfc && nfc_docs, tb,
+                       ds->lw.p, ds->ncp.p, ds->norm_off.p, nullptr, 0, s));
+    ds->scan_tmp.ensure(scan_tmp_elems(n_docs + 1) + 64);
+    HIPTRY(scan_u64(ds->norm_off.p, n_docs, ds->scan_tmp.p, ds->scan_tmp.cap, s));
+    uint64_t nb = 0;
+    HIPTRY(hipMemcpyAsync(&nb, ds->norm_off.p + n_docs, 8, hipMemcpyDeviceToHost, s));
+    HIPTRY(hipStreamSynchronize(s));
+    if (nb >= 0xF0000000ull) throw_err(CTOK_E_ARG, "normalised batch exceeds 3.75 GiB; split the batch");
+    ds->norm_text.ensure(nb + 16);
+    STEP("norm1", launch_norm(d_text, d_off, (uint32_t)n_docs, ds->doc_flag.p, t->add_prefix_space, t->nfc && nfc_docs, tb,
+                       ds->lw.p, ds->ncp.p, ds->norm_off.p, ds->norm_text.p, 1, s));
+    text = ds->norm_text.p;
+    off = ds->norm_off.p;
+    B = nb;
+  }
+  if (B > 0 && ((uintptr_t)text & 15)) throw_err(CTOK_E_ARG, "device text buffer must be 16-byte aligned");
+
+  Work w{};
+  w.text = text;
+  w.n_bytes = (uint32_t)B;
+  w.doc_off = off;
+  w.n_docs = (uint32_t)n_docs;
+  w.n_words = (uint32_t)((B + 31) / 32);
+  w.n_tiles = (uint32_t)((B + kTile - 1) / kTile);
+  ds->docbits.ensure(w.n_words + 8);
+  ds->pbits.ensure(w.n_words + 8);
+  ds->tile_cnt.ensure(w.n_tiles + 2);
+  ds->word_prefix.ensure(w.n_words + 8);
+  ds->pstart.ensure(B + 2);
+  ds->pcnt.ensure(B + 2);
+  ds->scratch.ensure(B + 2);
+  ds->doc_piece.ensure(n_docs + 2);
+  ds->long_list.ensure(B / kShortMax + 2);
+  ds->lw.ensure(4 * B + 64);
+  ds->scan_tmp.ensure(scan_tmp_elems(std::max<uint64_t>(B + 1, n_docs + 1)) + 64);
+  w.docbits = ds->docbits.p;
+  w.pbits = ds->pbits.p;
+  w.tile_cnt = ds->tile_cnt.p;
+  w.word_prefix = ds->word_prefix.p;
+  w.pstart = ds->pstart.p;
+  w.pcnt = ds->pcnt.p;
+  w.scratch = ds->scratch.p;
+  w.doc_piece = ds->doc_piece.p;
+  w.long_list = ds->long_list.p;
+  w.counters = ds->counters.p;
+  w.lw = ds->lw.p;
+  w.scan_tmp = (uint32_t*)ds->scan_tmp.p;
+  w.scan_tmp_cap = ds->scan_tmp.cap * 2;
+
+  STEP("docstart", launch_docstart(w, s));
+  STEP("segment", launch_segment(w, tb, s));
+  STEP("pieces", launch_pieces(w, s));
+  if (timing) HIPTRY(hipEventRecord(ds->ev[1], s));
+  STEP("bpe", launch_bpe(w, tb, s));
+  if (timing) HIPTRY(hipEventRecord(ds->ev[2], s));
+  STEP("bpe_long", launch_bpe_long(w, tb, s));
+  if (timing) HIPTRY(hipEventRecord(ds->ev[3], s));
+  STEP("emit", launch_emit(w, d_ids, ids_cap, d_tok_off, s));
+  if (timing) HIPTRY(hipEventRecord(ds->ev[4], s));
+  uint64_t ntok = 0;
+  uint32_t cnt[4] = {0, 0, 0, 0};
+  HIPTRY(hipMemcpyAsync(&ntok, d_tok_off + n_docs, 8, hipMemcpyDeviceToHost, s));
+  HIPTRY(hipMemcpyAsync(cnt, ds->counters.p, 16, hipMemcpyDeviceToHost, s));
+  uint32_t P = 0;
+  HIPTRY(hipMemcpyAsync(&P, ds->tile_cnt.p + w.n_tiles, 4, hipMemcpyDeviceToHost, s));
+  HIPTRY(hipStreamSynchronize(s));
+  if (cnt[2] & kErrPanic)
+    throw_err(CTOK_E_PANIC, "index out of bounds: a merge rank points past the list of valid merges (reference src/bpe.rs:141 panics)");
+  if (ntok > ids_cap) throw_err(CTOK_E_CAPACITY, "ids_cap too small: tok_off[n_docs] holds the number of ids needed");
+  if (st) {
+    st->bytes_in = n_bytes;
+    st->bytes_norm = B;
+    st->docs = n_docs;
+    st->pieces = w.n_tiles ? P : 0;
+    st->long_pieces = cnt[0];
+    st->tokens = ntok;
+    st->nfc_docs = nfc_docs;
+    if (timing) {
+      float a = 0, b = 0, c = 0, d = 0;
+      HIPTRY(hipEventElapsedTime(&a, ds->ev[0], ds->ev[1]));
+      HIPTRY(hipEventElapsedTime(&b, ds->ev[1], ds->ev[3]));
+      HIPTRY(hipEventElapsedTime(&c, ds->ev[3], ds->ev[4]));
+      HIPTRY(hipEventElapsedTime(&d, ds->ev[0], ds->ev[4]));
+      st->ms_pretok = a;
+      st->ms_bpe = b;
+      st->ms_emit = c;
+      st->ms_device = d;
+    }
+  }
+  return ntok;
+}
+
+}  // namespace
+
+// ----------------------------------------------------------------------------- C ABI
+
+namespace {
+int run(const std::function<void()>& f) {
+  try {
+    f();
+    g_err.clear();
+    return CTOK_OK;
+  } catch (const CtokError& e) {
+    return fail(e.code, e.msg);
+  } catch (const std::bad_alloc&) {
+    return fail(CTOK_E_DEVICE, "out of host memory");
+  } catch (const std::exception& e) {
+    return fail(CTOK_E_ARG, e.what());
+  }
+}
+}  // namespace
+
+extern "C" {
+
+const char* ctok_last_error(void) { return g_err.c_str(); }
+const char* ctok_version(void) { return "0.3.3+mi355x.1"; }
+
+int ctok_create_from_buffer(const char* json, size_t len, ctok** out) {
+  if (!out || (!json && len)) return fail(CTOK_E_ARG, "null argument");
+  *out = nullptr;
+  return run([&] {
+    std::unique_ptr<ctok> t(new ctok());
+    load(t.get(), json, len);
+    *out = t.release();
+  });
+}
+
+int ctok_create_from_file(const char* path, ctok** out) {
+  if (!path || !out) return fail(CTOK_E_ARG, "null argument");
+  *out = nullptr;
+  std::ifstream f(path, std::ios::binary);
+  if (!f) return fail(CTOK_E_IO, std::string("No such file or directory (os error 2): ") + path);
+  std::stringstream ss;
+  ss << f.rdbuf();
+  if (f.bad()) return fail(CTOK_E_IO, std::string("read error: ") + path);
+  std::string s = ss.str();
+  return ctok_create_from_buffer(s.data(), s.size(), out);
+}
+
+void ctok_destroy(ctok* t) { delete t; }
+
+uint64_t ctok_vocab_size(const ctok* t) { return t ? t->vocab.size() : 0; }
+
+int ctok_token_to_id(const ctok* t, const char* tok, size_t len, uint32_t* id) {
+  if (!t || (!tok && len) || !id) return fail(CTOK_E_ARG, "null argument");
+  auto it = t->vocab.find(std::string(tok, len));
+  if (it == t->vocab.end()) return CTOK_E_NOTFOUND;
+  *id = it->second;
+  return CTOK_OK;
+}
+
+int ctok_id_to_token(const ctok* t, uint32_t id, char* buf, size_t cap, size_t* len) {
+  if (!t || !len) return fail(CTOK_E_ARG, "null argument");
+  auto it = t->id_to_token.find(id);
+  if (it == t->id_to_token.end()) return CTOK_E_NOTFOUND;
+  *len = it->second.size();
+  if (buf && cap) memcpy(buf, it->second.data(), std::min(cap, it->second.size()));
+  return CTOK_OK;
+}
+
+uint64_t ctok_num_special_tokens(const ctok* t) { return t ? t->special.size() : 0; }
+
+int ctok_special_token(const ctok* t, uint64_t i, char* buf, size_t cap, size_t* len, uint32_t* id) {
+  if (!t || !len || !id) return fail(CTOK_E_ARG, "null argument");
+  if (i >= t->special.size()) return fail(CTOK_E_ARG, "index out of range");
+  const auto& e = t->special[i];
+  *len = e.first.size();
+  *id = e.second;
+  if (buf && cap) memcpy(buf, e.first.data(), std::min(cap, e.first.size()));
+  return CTOK_OK;
+}
+
+uint64_t ctok_ids_bound(const ctok*, uint64_t n_bytes, uint64_t n_docs) { return 3 * n_bytes + n_docs + 16; }
+
+int ctok_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int ctok_encode_batch_device(const ctok* tc, const uint8_t* d_utf8, const uint64_t* d_doc_off, uint64_t n_docs,
+                             uint64_t n_bytes, uint32_t* d_ids, uint64_t ids_cap, uint64_t* d_tok_off,
+                             uint64_t* n_tokens_out, const ctok_exec* exec, ctok_stats* stats) {
+  if (!tc || !d_doc_off || !d_tok_off || (n_bytes && (!d_utf8 || !d_ids))) return fail(CTOK_E_ARG, "null argument");
+  ctok* t = const_cast<ctok*>(tc);
+  return run([&] {
+    double t0 = now_ms();
+    int dev = exec ? exec->device : 0;
+    DeviceState* ds = device_state(t, dev);
+    std::lock_guard<std::mutex> lk(ds->mu);
+    HIPTRY(hipSetDevice(dev));
+    hipStream_t s = exec && exec->stream ? (hipStream_t)exec->stream : ds->stream;
+    bool timing = exec && (exec->flags & CTOK_F_TIMING);
+    uint64_t n = encode_device(t, ds, d_utf8, d_doc_off, n_docs, n_bytes, d_ids, ids_cap, d_tok_off, s, timing, stats);
+    if (n_tokens_out) *n_tokens_out = n;
+    if (stats) stats->ms_total = now_ms() - t0;
+  });
+}
+
+int ctok_encode_batch(const ctok* tc, const uint8_t* utf8_in, const uint64_t* doc_off, uint64_t n_docs, uint32_t* ids,
+                      uint64_t ids_cap, uint64_t* tok_off, const ctok_exec* exec, ctok_stats* stats) {
+  if (!tc || !doc_off || !tok_off) return fail(CTOK_E_ARG, "null argument");
+  ctok* t = const_cast<ctok*>(tc);
+  return run([&] {
+    double t0 = now_ms();
+    if (doc_off[0] != 0) throw_err(CTOK_E_ARG, "doc_off[0] must be 0");
+    for (uint64_t d = 0; d < n_docs; d++)
+      if (doc_off[d + 1] < doc_off[d]) throw_err(CTOK_E_ARG, "doc_off must be non-decreasing");
+    const uint64_t B = doc_off[n_docs];
+    if (B && !utf8_in) throw_err(CTOK_E_ARG, "null text");
+    int dev = exec ? exec->device : 0;
+    DeviceState* ds = device_state(t, dev);
+    std::lock_guard<std::mutex> lk(ds->mu);
+    HIPTRY(hipSetDevice(dev));
+    hipStream_t s = exec && exec->stream ? (hipStream_t)exec->stream : ds->stream;
+    bool timing = exec && (exec->flags & CTOK_F_TIMING);
+    double h0 = now_ms();
+    ds->in_text.ensure(B + 16);
+    ds->in_off.ensure(n_docs + 1);
+    ds->out_off.ensure(n_docs + 1);
+    const uint64_t cap_dev = ctok_ids_bound(t, B, n_docs);
+    ds->out_ids.ensure(cap_dev);
+    if (B) HIPTRY(hipMemcpyAsync(ds->in_text.p, utf8_in, B, hipMemcpyHostToDevice, s));
+    HIPTRY(hipMemcpyAsync(ds->in_off.p, doc_off, (n_docs + 1) * 8, hipMemcpyHostToDevice, s));
+    HIPTRY(hipStreamSynchronize(s));
+    double h1 = now_ms();
+    uint64_t n = encode_device(t, ds, ds->in_text.p, ds->in_off.p, n_docs, B, ds->out_ids.p, ds->out_ids.cap,
+                               ds->out_off.p, s, timing, stats);
+    double d0 = now_ms();
+    HIPTRY(hipMemcpyAsync(tok_off, ds->out_off.p, (n_docs + 1) * 8, hipMemcpyDeviceToHost, s));
+    if (n <= ids_cap && n) HIPTRY(hipMemcpyAsync(ids, ds->out_ids.p, n * 4, hipMemcpyDeviceToHost, s));
+    HIPTRY(hipStreamSynchronize(s));
+    if (n > ids_cap) throw_err(CTOK_E_CAPACITY, "ids_cap too small: tok_off[n_docs] holds the number of ids needed");
+    if (stats) {
+      stats->ms_h2d = h1 - h0;
+      stats->ms_d2h = now_ms() - d0;
+      stats->ms_total = now_ms() - t0;
+    }
+  });
+}
+
+}  // extern "C"

@@ -1,0 +1,1034 @@
+// HIP kernels (gfx950 / CDNA4) for the batch ByteLevel-BPE encode path.
+//
+// Reference path (Complexity-ML/complexity-tokenizer v0.3.3):
+//   HuggingFaceTokenizer::encode_batch   src/huggingface/mod.rs:694-696
+//   -> encode                            src/huggingface/mod.rs:551-613
+//      NFC                               src/normalizers.rs:47
+//      byte_level_pretokenize            src/pretokenizers.rs:158-185 (GPT2_PATTERN :11-15)
+//      added-token split                 src/huggingface/mod.rs:566-675
+//      BpeTokenizer::encode              src/bpe.rs:88-153
+//
+// Data layout in HBM (all offsets u32: one call covers < 4 GiB of text):
+//   text[B] u8, doc_off[D+1] u64 (input) ->
+//   docbits / pbits: 1 bit per byte (doc start / piece start) ->
+//   pstart[P+1] u32 (piece start byte), word_prefix[B/32] u32 (pieces before each bitmap word) ->
+//   scratch[B] u32: the ids of piece p at scratch[pstart[p] ...] (ids <= bytes per piece) ->
+//   pcnt[P+1] u32 scanned in place to the token offset of each piece ->
+//   ids[T] u32 + tok_off[D+1] u64 (output).
+//
+// The regex of GPT2_PATTERN is evaluated as a per-code-point "piece starts here" predicate
+// over classes {White_Space, L, N, other} (derivation in DESIGN.md 3.2): one wavefront-parallel
+// pass, no backtracking, coalesced 16-byte loads.
+#include <hip/hip_runtime.h>
+
+#include "ctok_internal.h"
+
+namespace ctok_dev {
+
+#define HIPCHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) return e_; } while (0)
+
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+constexpr uint32_t kDead = 0xFFFFFFFFu;
+constexpr uint32_t kSel = kNoRank - 1;  // marks a merge site during a parallel round
+
+// ------------------------------------------------------------------------------------------
+// small device helpers
+
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, 64));
+  return v;
+}
+
+__device__ __forceinline__ uint64_t lanemask_lt() {
+  const uint32_t lane = threadIdx.x & 63;
+  return lane ? (~0ull >> (64 - lane)) : 0ull;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_incl_scan(T v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    T u = __shfl_up(v, o, 64);
+    if (lane >= o) v += u;
+  }
+  return v;
+}
+
+// block-wide exclusive scan; nthreads = blockDim.x (multiple of 64, <= 1024)
+template <typename T>
+__device__ T block_excl_scan(T v, T* smem /*[17]*/, T* total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  T inc = wave_incl_scan(v);
+  if (lane == 63) smem[wid] = inc;
+  __syncthreads();
+  if (wid == 0) {
+    T s = lane < nw ? smem[lane] : T(0);
+    T si = wave_incl_scan(s);
+    if (lane < nw) smem[lane] = si - s;
+    if (lane == nw - 1) smem[16] = si;
+  }
+  __syncthreads();
+  T r = inc - v + smem[wid];
+  if (total) *total = smem[16];
+  __syncthreads();
+  return r;
+}
+
+__device__ __forceinline__ int u8len(uint8_t b) {
+  return b < 0x80 ? 1 : (b >> 5) == 6 ? 2 : (b >> 4) == 14 ? 3 : 4;
+}
+
+__device__ __forceinline__ int cls_ascii(uint32_t c) {
+  // 0 White_Space, 1 letter, 2 number, 3 other
+  if (c == 32 || (c >= 9 && c <= 13)) return 0;
+  if ((c | 32) >= 'a' && (c | 32) <= 'z') return 1;
+  if (c >= '0' && c <= '9') return 2;
+  return 3;
+}
+
+__device__ __forceinline__ int cls_of(uint32_t cp, const Tables& t) {
+  if (cp < 0x80) return cls_ascii(cp);
+  if (cp >= 0x110000) return 3;
+  const uint32_t blk = t.cls_s1[cp >> 8];
+  const uint32_t w = t.cls_s2[blk * 64 + ((cp & 255) >> 2)];
+  return (w >> ((cp & 3) * 2)) & 3;
+}
+
+__device__ __forceinline__ uint32_t mhash(uint32_t a, uint32_t b) {
+  uint32_t h = a * 0x9E3779B1u ^ (b + 0x7F4A7C15u) * 0x85EBCA77u;
+  return h ^ (h >> 15);
+}
+
+// rank of pair (a, b) or kNoRank.  Sets the panic bit when the reference would index
+// BpeTokenizer.merges out of range (src/bpe.rs:141).
+__device__ __forceinline__ uint32_t rank_of(const Tables& t, uint32_t a, uint32_t b, uint32_t* err) {
+  const uint64_t key = ((uint64_t)a << kIdBits) | b;
+  uint32_t h = mhash(a, b) & t.merge_mask;
+  for (;;) {
+    const uint64_t e = t.merge_tab[h];
+    if ((e & kKeyMask) == key) {
+      const uint32_t r = (uint32_t)(e >> 42);
+      if (r >= t.n_ranks) { atomicOr(err, kErrPanic); return kNoRank; }
+      return r;
+    }
+    if (e == kEmpty) return kNoRank;
+    h = (h + 1) & t.merge_mask;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// doc-start bitmap
+
+__global__ void k_docstart(const uint64_t* __restrict__ off, uint32_t n_docs, uint32_t* __restrict__ bits) {
+  const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= n_docs) return;
+  const uint64_t a = off[d], b = off[d + 1];
+  if (a < b) atomicOr(&bits[a >> 5], 1u << (a & 31));
+}
+
+hipError_t launch_docstart(const Work& w, hipStream_t s) {
+  HIPCHK(hipMemsetAsync(w.docbits, 0, (size_t)(w.n_words + 2) * 4, s));
+  if (w.n_docs) k_docstart<<<(w.n_docs + 255) / 256, 256, 0, s>>>(w.doc_off, w.n_docs, w.docbits);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+// pre-tokenizer: piece-start bitmap.  One 256-thread workgroup per 4 KiB tile, 16 bytes per
+// thread, the tile plus a 32-byte halo each side staged in LDS.
+
+constexpr int kSegHalo = 32;
+constexpr int kSegN = kTile + 2 * kSegHalo;
+constexpr uint8_t kCont = 0xFF;  // continuation byte
+constexpr uint8_t kOut = 0xFE;   // outside the text
+
+struct SegCtx {
+  const uint8_t* b;
+  const uint32_t* cp;
+  const uint8_t* cl;
+  const uint32_t* doc;
+  int64_t base;       // global position of LDS index 0
+  int64_t wbase;      // global bitmap word of s_doc[0]
+  uint32_t n_bytes;
+
+  __device__ __forceinline__ bool docst(int i) const {
+    const int64_t g = base + i;
+    return (doc[(g >> 5) - wbase] >> (g & 31)) & 1u;
+  }
+  __device__ __forceinline__ int prev(int i) const {
+    if (docst(i)) return -1;
+    int j = i - 1;
+    while (cl[j] == kCont) --j;
+    return j;
+  }
+  __device__ __forceinline__ int next(int i) const {
+    const int j = i + u8len(b[i]);
+    if (base + j >= (int64_t)n_bytes || docst(j)) return -1;
+    return j;
+  }
+  // a single U+0020 that begins the following non-space run (the " ?" of the pattern)
+  __device__ __forceinline__ bool attached(int i) const {
+    if (cp[i] != ' ') return false;
+    const int n = next(i);
+    if (n < 0 || cl[n] == 0) return false;
+    const int p = prev(i);
+    return p < 0 || cl[p] != 0;
+  }
+  // length (1 or 2 letters) of a contraction 's|'t|'re|'ve|'m|'ll|'d that starts at i, else 0
+  __device__ __forceinline__ int con_len(int i) const {
+    if (cp[i] != '\'') return 0;
+    const int n1 = next(i);
+    if (n1 < 0 || cl[n1] != 1) return 0;
+    const int p = prev(i);
+    if (p >= 0 && (cl[p] == 3 || attached(p))) return 0;
+    const uint32_t a = cp[n1];
+    if (a == 's' || a == 't' || a == 'm' || a == 'd') return 1;
+    const int n2 = next(n1);
+    if (n2 < 0) return 0;
+    const uint32_t c = cp[n2];
+    if ((a == 'r' && c == 'e') || (a == 'v' && c == 'e') || (a == 'l' && c == 'l')) return 2;
+    return 0;
+  }
+  __device__ __forceinline__ bool start(int i) const {
+    if (docst(i)) return true;
+    const int p = prev(i);
+    if (cl[i] != cl[p]) {
+      if (attached(p)) return false;
+      if (con_len(p) > 0) return false;
+      return true;
+    }
+    if (cl[i] == 1) {  // a letter run may be cut after a contraction's letters
+      const int pp = prev(p);
+      if (pp >= 0) {
+        if (con_len(pp) == 1) return true;
+        const int ppp = prev(pp);
+        if (ppp >= 0 && con_len(ppp) == 2) return true;
+      }
+    }
+    return false;
+  }
+};
+
+__global__ __launch_bounds__(kSegThreads) void k_segment(Work w, Tables t) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_b[kSegN];
+  __shared__ uint32_t s_cp[kSegN];
+  __shared__ uint8_t s_cl[kSegN];
+  __shared__ uint32_t s_doc[kSegN / 32 + 4];
+  __shared__ uint32_t s_red[kSegThreads / 64];
+
+  const uint32_t tid = threadIdx.x;
+  const uint32_t t0 = blockIdx.x * kTile;
+  const int64_t base = (int64_t)t0 - kSegHalo;
+  const uint32_t B = w.n_bytes;
+
+  // stage bytes: the tile with 16-byte loads, the halos byte-wise
+  if ((uint64_t)t0 + kTile <= B) {
+    const uint4 v = *reinterpret_cast<const uint4*>(w.text + t0 + tid * 16);
+    *reinterpret_cast<uint4*>(s_b + kSegHalo + tid * 16) = v;
+  } else {
+    for (int k = 0; k < 16; k++) {
+      const uint64_t g = (uint64_t)t0 + tid * 16 + k;
+      s_b[kSegHalo + tid * 16 + k] = g < B ? w.text[g] : 0;
+    }
+  }
+  if (tid < 2 * kSegHalo) {
+    const int i = tid < kSegHalo ? (int)tid : kTile + (int)tid;
+    const int64_t g = base + i;
+    s_b[i] = (g >= 0 && g < (int64_t)B) ? w.text[g] : 0;
+  }
+  const int64_t wbase = (base >> 5);
+  for (int j = tid; j < kSegN / 32 + 4; j += kSegThreads) {
+    const int64_t wg = wbase + j;
+    s_doc[j] = (wg >= 0 && wg < (int64_t)w.n_words + 2) ? w.docbits[wg] : 0u;
+  }
+  __syncthreads();
+
+  // decode code points at lead bytes, classify
+  for (int i = tid; i < kSegN; i += kSegThreads) {
+    const int64_t g = base + i;
+    if (g < 0 || g >= (int64_t)B) { s_cl[i] = kOut; s_cp[i] = 0; continue; }
+    const uint8_t b0 = s_b[i];
+    if ((b0 & 0xC0) == 0x80) { s_cl[i] = kCont; s_cp[i] = 0; continue; }
+    const int len = u8len(b0);
+    if (i + len > kSegN) { s_cl[i] = kOut; s_cp[i] = 0; continue; }
+    uint32_t c;
+    if (len == 1) c = b0;
+    else if (len == 2) c = ((b0 & 0x1Fu) << 6) | (s_b[i + 1] & 0x3Fu);
+    else if (len == 3) c = ((b0 & 0x0Fu) << 12) | ((s_b[i + 1] & 0x3Fu) << 6) | (s_b[i + 2] & 0x3Fu);
+    else c = ((b0 & 0x07u) << 18) | ((s_b[i + 1] & 0x3Fu) << 12) | ((s_b[i + 2] & 0x3Fu) << 6) | (s_b[i + 3] & 0x3Fu);
+    s_cp[i] = c;
+    s_cl[i] = (uint8_t)cls_of(c, t);
+  }
+  __syncthreads();
+
+  SegCtx cx{s_b, s_cp, s_cl, s_doc, base, wbase, B};
+  uint32_t mask = 0;
+  for (int k = 0; k < 16; k++) {
+    const int i = kSegHalo + tid * 16 + k;
+    const uint8_t c = s_cl[i];
+    if (c >= kOut) continue;
+    if (cx.start(i)) mask |= 1u << k;
+  }
+  // pair up 16-bit masks into bitmap words
+  const uint32_t hi = (uint32_t)__shfl_down((int)mask, 1, 64);
+  const uint32_t word_idx = (t0 >> 5) + (tid >> 1);
+  if ((tid & 1) == 0 && word_idx < w.n_words) w.pbits[word_idx] = mask | (hi << 16);
+
+  uint32_t c = __popc(mask);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c += (uint32_t)__shfl_xor((int)c, o, 64);
+  if ((tid & 63) == 0) s_red[tid >> 6] = c;
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t s = 0;
+    for (int j = 0; j < kSegThreads / 64; j++) s += s_red[j];
+    w.tile_cnt[blockIdx.x] = s;
+  }
+}
+
+hipError_t launch_segment(const Work& w, const Tables& t, hipStream_t s) {
+  if (w.n_tiles) k_segment<<<w.n_tiles, kSegThreads, 0, s>>>(w, t);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+// piece list from the bitmap (tile_cnt already exclusive-scanned: tile_cnt[n_tiles] = P)
+
+__global__ __launch_bounds__(128) void k_pieces(Work w) {
+  __shared__ uint32_t s_scan[17];
+  const uint32_t tile = blockIdx.x;
+  const uint32_t wi = tile * (kTile / 32) + threadIdx.x;
+  uint32_t word = wi < w.n_words ? w.pbits[wi] : 0u;
+  const uint32_t excl = block_excl_scan<uint32_t>(__popc(word), s_scan, nullptr);
+  const uint32_t base = w.tile_cnt[tile] + excl;
+  if (wi < w.n_words) w.word_prefix[wi] = base;
+  uint32_t k = 0;
+  while (word) {
+    const uint32_t bit = __ffs(word) - 1;
+    w.pstart[base + k++] = wi * 32 + bit;
+    word &= word - 1;
+  }
+  if (tile == 0 && threadIdx.x == 0) w.pstart[w.tile_cnt[w.n_tiles]] = w.n_bytes;
+}
+
+__global__ void k_docpiece(Work w) {
+  const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d > w.n_docs) return;
+  const uint64_t x = w.doc_off[d];
+  uint32_t r;
+  if (x >= w.n_bytes) {
+    r = w.tile_cnt[w.n_tiles];
+  } else {
+    const uint32_t wi = (uint32_t)(x >> 5);
+    r = w.word_prefix[wi] + __popc(w.pbits[wi] & ((1u << (x & 31)) - 1u));
+  }
+  w.doc_piece[d] = r;
+}
+
+hipError_t launch_pieces(const Work& w, hipStream_t s) {
+  HIPCHK(scan_u32(w.tile_cnt, w.tile_cnt, w.n_tiles, nullptr, w.scan_tmp, w.scan_tmp_cap, s));
+  if (w.n_tiles) k_pieces<<<w.n_tiles, 128, 0, s>>>(w);
+  else {
+    const uint32_t zero = 0;
+    HIPCHK(hipMemcpyAsync(w.pstart, &zero, 4, hipMemcpyHostToDevice, s));
+  }
+  k_docpiece<<<(w.n_docs + 1 + 255) / 256, 256, 0, s>>>(w);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+// BPE, short pieces: one thread per piece, the working tokens and pair ranks in LDS
+// (thread-interleaved columns: entry j of thread t at [j*256 + t], conflict-free).
+
+struct AddedMatch {  // first occurrence of added token k in bytes[0, n) honouring its flags
+  __device__ static int64_t find(const Tables& t, uint32_t k, const uint8_t* s, uint32_t n) {
+    const uint8_t* pat = t.at_bytes + t.at_off[k];
+    const uint32_t m = t.at_off[k + 1] - t.at_off[k];
+    if (m > n) return -1;
+    for (uint32_t pos = 0; pos + m <= n; pos++) {
+      uint32_t j = 0;
+      while (j < m && s[pos + j] == pat[j]) j++;
+      if (j < m) continue;
+      // first occurrence found: the flags are checked only here (src/huggingface/mod.rs:637-675)
+      const uint8_t f = t.at_flags[k];
+      if (f & 1) {  // single_word: Rust is_alphanumeric of the neighbouring byte-mapped chars
+        if (pos > 0 && t.bytemap_alnum[s[pos - 1]]) return -1;
+        if (pos + m < n && t.bytemap_alnum[s[pos + m]]) return -1;
+      }
+      // byte-mapped chars are never White_Space: lstrip/rstrip pass only at the edges
+      if ((f & 2) && pos > 0) return -1;
+      if ((f & 4) && pos + m < n) return -1;
+      return pos;
+    }
+    return -1;
+  }
+};
+
+#define TOK(i) s_tok[(i) * 256 + tid]
+#define RK(i) s_rk[(i) * 256 + tid]
+
+// BPE over bytes[0, n) (n <= kShortMax), appending ids to out; returns the id count
+__device__ __forceinline__ uint32_t bpe_short(const Tables& t, const uint8_t* bytes, uint32_t n,
+                                              const int32_t* s_b2id, uint32_t* s_tok, uint32_t* s_rk,
+                                              uint32_t tid, uint32_t* out, uint32_t* err) {
+  uint32_t m = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    const int32_t id = s_b2id[bytes[i]];
+    if (id >= 0) TOK(m++) = (uint32_t)id;
+  }
+  if (m >= 2) {
+    for (uint32_t i = 0; i + 1 < m; i++) RK(i) = rank_of(t, TOK(i), TOK(i + 1), err);
+    while (m >= 2) {
+      uint32_t best = kNoRank, bi = 0;
+      for (uint32_t i = 0; i + 1 < m; i++) {
+        const uint32_t r = RK(i);
+        if (r < best) { best = r; bi = i; }
+      }
+      if (best == kNoRank) break;
+      TOK(bi) = t.rank_newid[best];
+      for (uint32_t i = bi + 1; i + 1 < m; i++) TOK(i) = TOK(i + 1);
+      for (uint32_t i = bi + 1; i + 2 < m; i++) RK(i) = RK(i + 1);
+      m--;
+      if (bi > 0) RK(bi - 1) = rank_of(t, TOK(bi - 1), TOK(bi), err);
+      if (bi + 1 < m) RK(bi) = rank_of(t, TOK(bi), TOK(bi + 1), err);
+    }
+  }
+  for (uint32_t i = 0; i < m; i++) out[i] = TOK(i);
+  return m;
+}
+
+__global__ __launch_bounds__(256) void k_bpe(Work w, Tables t) {
+  __shared__ uint32_t s_tok[kShortMax * 256];
+  __shared__ uint32_t s_rk[kShortMax * 256];
+  __shared__ int32_t s_b2id[256];
+  const uint32_t tid = threadIdx.x;
+  s_b2id[tid] = t.byte2id[tid];
+  __syncthreads();
+  const uint32_t P = w.tile_cnt[w.n_tiles];
+  uint32_t* err = &w.counters[2];
+  for (uint32_t p = blockIdx.x * 256 + tid; p < P; p += gridDim.x * 256) {
+    const uint32_t s = w.pstart[p];
+    const uint32_t n = w.pstart[p + 1] - s;
+    if (n > kShortMax) {
+      const uint32_t li = atomicAdd(&w.counters[0], 1u);
+      w.long_list[li] = p;
+      continue;
+    }
+    const uint8_t* bytes = w.text + s;
+    uint32_t* out = w.scratch + s;
+    uint32_t cnt = 0;
+    if (t.n_at == 0) {
+      cnt = bpe_short(t, bytes, n, s_b2id, s_tok, s_rk, tid, out, err);
+    } else {
+      // added-token split of the word (src/huggingface/mod.rs:566-610), on raw bytes
+      uint32_t pos = 0;
+      while (pos < n) {
+        int32_t best = -1;
+        uint32_t blen = 0;
+        for (uint32_t k = 0; k < t.n_at; k++) {
+          const uint32_t m = t.at_off[k + 1] - t.at_off[k];
+          if (AddedMatch::find(t, k, bytes + pos, n - pos) == 0 && (best < 0 || m > blen)) { best = (int32_t)k; blen = m; }
+        }
+        if (best >= 0) { out[cnt++] = t.at_id[best]; pos += blen; continue; }
+        uint32_t nxt = n - pos;
+        for (uint32_t k = 0; k < t.n_at; k++) {
+          const int64_t f = AddedMatch::find(t, k, bytes + pos, n - pos);
+          if (f > 0 && (uint32_t)f < nxt) nxt = (uint32_t)f;
+        }
+        cnt += bpe_short(t, bytes + pos, nxt, s_b2id, s_tok, s_rk, tid, out + cnt, err);
+        pos += nxt;
+      }
+    }
+    w.pcnt[p] = cnt;
+  }
+}
+
+#undef TOK
+#undef RK
+
+hipError_t launch_bpe(const Work& w, const Tables& t, hipStream_t s) {
+  uint32_t grid = (w.n_bytes / 4 + 255) / 256;  // pieces <= bytes; typical ~bytes/4.5
+  grid = grid < 1 ? 1 : grid > 8192 ? 8192 : grid;
+  k_bpe<<<grid, 256, 0, s>>>(w, t);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+// BPE, long pieces: one wavefront per piece over a doubly linked token list in global memory.
+// Each round finds the global minimum rank r (wave reduction).  If the merge table is
+// rank-monotone ("proper": every merge consuming token z ranks after every merge producing
+// z), the sequential algorithm applies all non-overlapping occurrences of r left to right
+// before any other merge, so they are applied in one parallel round; (x,x) chains and
+// non-monotone tables fall back to the exact sequential order.
+
+// Working state of one long piece.  GMEM = arrays in global memory (any length): every access
+// is an agent-scope relaxed atomic (`global_load/store ... sc1`, served by L2), so lanes of the
+// wave see each other's stores between rounds (the vector L1 does not).  LDS = arrays in the
+// wave's slice of LDS (pieces up to kLdsPos), accessed through address-space-3 pointers so the
+// compiler emits in-order ds_read/ds_write (never flat).
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+
+template <bool GMEM>
+struct LongState;
+
+template <>
+struct LongState<true> {
+  uint32_t* tok;
+  uint32_t* nxt;
+  uint32_t* prv;
+  uint32_t* rk;
+  static __device__ __forceinline__ uint32_t ld(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  static __device__ __forceinline__ void st(uint32_t* p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __device__ __forceinline__ uint32_t Tok(uint32_t i) const { return ld(tok + i); }
+  __device__ __forceinline__ uint32_t Nxt(uint32_t i) const { return ld(nxt + i); }
+  __device__ __forceinline__ uint32_t Prv(uint32_t i) const { return ld(prv + i); }
+  __device__ __forceinline__ uint32_t Rk(uint32_t i) const { return ld(rk + i); }
+  __device__ __forceinline__ void sTok(uint32_t i, uint32_t v) const { st(tok + i, v); }
+  __device__ __forceinline__ void sNxt(uint32_t i, uint32_t v) const { st(nxt + i, v); }
+  __device__ __forceinline__ void sPrv(uint32_t i, uint32_t v) const { st(prv + i, v); }
+  __device__ __forceinline__ void sRk(uint32_t i, uint32_t v) const { st(rk + i, v); }
+  static __device__ __forceinline__ void sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+  }
+};
+
+template <>
+struct LongState<false> {
+  lds_u32* tok;
+  lds_u32* nxt;
+  lds_u32* prv;
+  lds_u32* rk;
+  __device__ __forceinline__ uint32_t Tok(uint32_t i) const { return tok[i]; }
+  __device__ __forceinline__ uint32_t Nxt(uint32_t i) const { return nxt[i]; }
+  __device__ __forceinline__ uint32_t Prv(uint32_t i) const { return prv[i]; }
+  __device__ __forceinline__ uint32_t Rk(uint32_t i) const { return rk[i]; }
+  __device__ __forceinline__ void sTok(uint32_t i, uint32_t v) const { tok[i] = v; }
+  __device__ __forceinline__ void sNxt(uint32_t i, uint32_t v) const { nxt[i] = v; }
+  __device__ __forceinline__ void sPrv(uint32_t i, uint32_t v) const { prv[i] = v; }
+  __device__ __forceinline__ void sRk(uint32_t i, uint32_t v) const { rk[i] = v; }
+  static __device__ __forceinline__ void sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+  }
+};
+
+template <bool G>
+__device__ __forceinline__ void merge_one(const Tables& t, const LongState<G>& L, uint32_t i, uint32_t nid,
+                                          uint32_t* err) {
+  const uint32_t j = L.Nxt(i);
+  const uint32_t nj = L.Nxt(j);
+  L.sTok(i, nid);
+  L.sTok(j, kDead);
+  L.sRk(j, kNoRank);
+  L.sNxt(i, nj);
+  if (nj != kNone) L.sPrv(nj, i);
+  L.sRk(i, nj != kNone ? rank_of(t, nid, L.Tok(nj), err) : kNoRank);
+  const uint32_t p = L.Prv(i);
+  if (p != kNone) L.sRk(p, rank_of(t, L.Tok(p), nid, err));
+}
+
+// Wave-uniform values are moved to SGPRs with readfirstlane: the loop exits and the chain walk
+// then branch on scalars, so the wave can never split around the cross-lane reductions (a split
+// wave reduces over inactive lanes and never terminates).
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+template <bool G>
+__device__ uint32_t bpe_wave(const Tables& t, const uint8_t* bytes, uint32_t n, const LongState<G>& L, uint32_t* out,
+                             uint32_t* err) {
+  const uint32_t lane = threadIdx.x & 63;
+  // initial ids, dropping bytes whose char is not in the vocab (order-preserving compaction)
+  uint32_t m = 0;
+  for (uint32_t i0 = 0; i0 < n; i0 += 64) {
+    const uint32_t i = i0 + lane;
+    const int32_t id = i < n ? t.byte2id[bytes[i]] : -1;
+    const uint64_t bal = __ballot(id >= 0);
+    if (id >= 0) L.sTok(m + __popcll(bal & lanemask_lt()), (uint32_t)id);
+    m = uni(m + __popcll(bal));
+  }
+  L.sync();
+  if (m == 0) return 0;
+  for (uint32_t i = lane; i < m; i += 64) {
+    L.sNxt(i, i + 1 < m ? i + 1 : kNone);
+    L.sPrv(i, i > 0 ? i - 1 : kNone);
+    L.sRk(i, i + 1 < m ? rank_of(t, L.Tok(i), L.Tok(i + 1), err) : kNoRank);
+  }
+  L.sync();
+  for (;;) {
+    uint32_t lmin = kNoRank;
+    for (uint32_t i = lane; i < m; i += 64) lmin = min(lmin, L.Rk(i));
+    const uint32_t r = uni(wave_min_u32(lmin));
+    if (r == kNoRank) break;
+    const uint32_t nid = uni(t.rank_newid[r]);
+    uint32_t lpos = kNone;
+    for (uint32_t i = lane; i < m; i += 64) {
+      if (L.Rk(i) == r) { lpos = i; break; }
+    }
+    const uint32_t lm = uni(wave_min_u32(lpos));
+    const uint32_t chain = uni(L.Tok(lm) == L.Tok(L.Nxt(lm)) ? 1u : 0u);
+    if (!t.proper) {
+      merge_one(t, L, lm, nid, err);  // every lane performs the same update
+    } else if (chain) {
+      // (x,x) runs: the sequential left-to-right order, walked by the whole wave in lockstep
+      for (uint32_t i = lm; i != kNone; i = uni(L.Nxt(i))) {
+        if (uni(L.Rk(i)) == r) merge_one(t, L, i, nid, err);
+      }
+    } else {
+      // phase A: splice out the right token of every occurrence
+      for (uint32_t i = lane; i < m; i += 64) {
+        if (L.Rk(i) != r) continue;
+        const uint32_t j = L.Nxt(i);
+        const uint32_t nj = L.Nxt(j);
+        L.sTok(i, nid);
+        L.sTok(j, kDead);
+        L.sRk(j, kNoRank);
+        L.sRk(i, kSel);
+        L.sNxt(i, nj);
+        if (nj != kNone) L.sPrv(nj, i);
+      }
+      L.sync();
+      // phase B: ranks of the new pairs (left pair only when its left end is not a site)
+      for (uint32_t i = lane; i < m; i += 64) {
+        if (L.Rk(i) != kSel) continue;
+        const uint32_t nj = L.Nxt(i);
+        L.sRk(i, nj != kNone ? rank_of(t, nid, L.Tok(nj), err) : kNoRank);
+        const uint32_t p = L.Prv(i);
+        if (p != kNone && L.Rk(p) != kSel) L.sRk(p, rank_of(t, L.Tok(p), nid, err));
+      }
+    }
+    L.sync();
+    if (uni(__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) break;
+  }
+  // emit surviving tokens in order
+  uint32_t c = 0;
+  for (uint32_t i0 = 0; i0 < m; i0 += 64) {
+    const uint32_t i = i0 + lane;
+    const uint32_t v = i < m ? L.Tok(i) : kDead;
+    const uint64_t bal = __ballot(v != kDead);
+    if (v != kDead) out[c + __popcll(bal & lanemask_lt())] = v;
+    c = uni(c + __popcll(bal));
+  }
+  return c;
+}
+
+constexpr uint32_t kLdsPos = 2048;  // positions per wave in LDS (4 u32 arrays: 32 KiB per wave)
+
+template <bool G>
+__device__ uint32_t long_piece(const Tables& t, const uint8_t* bytes, uint32_t n, const LongState<G>& L,
+                               uint32_t* out, uint32_t* err) {
+  const uint32_t lane = threadIdx.x & 63;
+  if (t.n_at == 0) return bpe_wave<G>(t, bytes, n, L, out, err);
+  uint32_t cnt = 0, pos = 0;
+  while (pos < n) {  // every lane computes the same added-token split; kept in SGPRs
+    int32_t best = -1;
+    uint32_t blen = 0;
+    for (uint32_t k = 0; k < t.n_at; k++) {
+      const uint32_t m = t.at_off[k + 1] - t.at_off[k];
+      if (AddedMatch::find(t, k, bytes + pos, n - pos) == 0 && (best < 0 || m > blen)) { best = (int32_t)k; blen = m; }
+    }
+    best = (int32_t)uni((uint32_t)best);
+    blen = uni(blen);
+    if (best >= 0) {
+      if (lane == 0) out[cnt] = t.at_id[best];
+      cnt++;
+      pos += blen;
+      continue;
+    }
+    uint32_t nxt = n - pos;
+    for (uint32_t k = 0; k < t.n_at; k++) {
+      const int64_t f = AddedMatch::find(t, k, bytes + pos, n - pos);
+      if (f > 0 && (uint32_t)f < nxt) nxt = (uint32_t)f;
+    }
+    nxt = uni(nxt);
+    cnt = uni(cnt + bpe_wave<G>(t, bytes + pos, nxt, L, out + cnt, err));
+    pos += nxt;
+  }
+  return cnt;
+}
+
+// One wavefront per long piece, pieces dealt to waves by a static stride (no work-queue
+// atomics: every loop bound and index is a scalar, so the wave never splits).  GMEM selects the
+// tier: LDS for pieces up to kLdsPos positions, global memory beyond.
+template <bool GMEM>
+__global__ __launch_bounds__(256) void k_bpe_long(Work w, Tables t) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_long[];
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wid = uni(threadIdx.x >> 6);
+  const uint32_t n_long = uni(w.counters[0]);
+  const uint32_t n_waves = gridDim.x * (blockDim.x >> 6);
+  uint32_t* err = &w.counters[2];
+  const uint32_t B = w.n_bytes;
+  for (uint32_t li = uni(blockIdx.x * (blockDim.x >> 6) + wid); li < n_long; li += n_waves) {
+    const uint32_t p = uni(w.long_list[li]);
+    const uint32_t s = uni(w.pstart[p]);
+    const uint32_t n = uni(w.pstart[p + 1]) - s;
+    if (GMEM != (n > kLdsPos)) continue;
+    const uint8_t* bytes = w.text + s;
+    uint32_t* out = w.scratch + s;
+    uint32_t cnt;
+    if constexpr (GMEM) {
+      LongState<true> L{w.lw + s, w.lw + (size_t)B + s, w.lw + 2 * (size_t)B + s, w.lw + 3 * (size_t)B + s};
+      cnt = long_piece<true>(t, bytes, n, L, out, err);
+    } else {
+      lds_u32* lds = (lds_u32*)s_long + wid * 4 * kLdsPos;
+      LongState<false> L{lds, lds + kLdsPos, lds + 2 * kLdsPos, lds + 3 * kLdsPos};
+      cnt = long_piece<false>(t, bytes, n, L, out, err);
+    }
+    if (lane == 0) w.pcnt[p] = cnt;
+  }
+}
+
+hipError_t launch_bpe_long(const Work& w, const Tables& t, hipStream_t s) {
+  static bool attr = false;
+  const size_t lds = 4 * 4 * kLdsPos * sizeof(uint32_t);
+  if (!attr) {
+    HIPCHK(hipFuncSetAttribute((const void*)k_bpe_long<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    attr = true;
+  }
+  k_bpe_long<false><<<256, 256, lds, s>>>(w, t);
+  k_bpe_long<true><<<256, 256, 0, s>>>(w, t);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+// emission: ids[ptok[p] ...] = scratch[pstart[p] ...]; tok_off[d] = ptok[doc_piece[d]]
+
+__global__ void k_emit(Work w, uint32_t* __restrict__ ids, uint64_t ids_cap) {
+  const uint32_t P = w.tile_cnt[w.n_tiles];
+  for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x) {
+    const uint32_t o = w.pcnt[p], c = w.pcnt[p + 1] - o;
+    const uint32_t* src = w.scratch + w.pstart[p];
+    for (uint32_t k = 0; k < c; k++)
+      if (o + k < ids_cap) ids[o + k] = src[k];  // the host reports CTOK_E_CAPACITY when short
+  }
+}
+
+__global__ void k_tokoff(Work w, uint64_t* __restrict__ tok_off) {
+  const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d > w.n_docs) return;
+  tok_off[d] = w.pcnt[w.doc_piece[d]];
+}
+
+hipError_t launch_emit(const Work& w, uint32_t* ids, uint64_t ids_cap, uint64_t* tok_off, hipStream_t s) {
+  HIPCHK(scan_u32(w.pcnt, w.pcnt, (uint64_t)w.n_bytes, &w.tile_cnt[w.n_tiles], w.scan_tmp, w.scan_tmp_cap, s));
+  uint32_t grid = (w.n_bytes / 4 + 255) / 256;
+  grid = grid < 1 ? 1 : grid > 8192 ? 8192 : grid;
+  k_emit<<<grid, 256, 0, s>>>(w, ids, ids_cap);
+  k_tokoff<<<(w.n_docs + 1 + 255) / 256, 256, 0, s>>>(w, tok_off);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+// device-wide exclusive scan (4096 elements per 256-thread block, recursive over partials)
+
+constexpr int kScanPer = 16;
+constexpr int kScanBlock = 256 * kScanPer;
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_scan_reduce(const T* __restrict__ in, uint64_t n_max, const uint32_t* n_dev,
+                                                     T* __restrict__ part) {
+  __shared__ T s_scan[17];
+  const uint64_t n = n_dev ? (uint64_t)*n_dev : n_max;
+  const uint64_t b0 = (uint64_t)blockIdx.x * kScanBlock + threadIdx.x * kScanPer;
+  T s = 0;
+#pragma unroll
+  for (int k = 0; k < kScanPer; k++) {
+    const uint64_t i = b0 + k;
+    if (i < n) s += in[i];
+  }
+  T total;
+  block_excl_scan<T>(s, s_scan, &total);
+  if (threadIdx.x == 0) part[blockIdx.x] = total;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_scan_apply(const T* in, T* out, uint64_t n_max, const uint32_t* n_dev,
+                                                    const T* __restrict__ part_scanned, int write_total) {
+  __shared__ T s_scan[17];
+  const uint64_t n = n_dev ? (uint64_t)*n_dev : n_max;
+  const uint64_t b0 = (uint64_t)blockIdx.x * kScanBlock + threadIdx.x * kScanPer;
+  T v[kScanPer];
+  T s = 0;
+#pragma unroll
+  for (int k = 0; k < kScanPer; k++) {
+    const uint64_t i = b0 + k;
+    v[k] = i < n ? in[i] : T(0);
+    s += v[k];
+  }
+  T total;
+  T ex = block_excl_scan<T>(s, s_scan, &total);
+  const T base = part_scanned ? part_scanned[blockIdx.x] : T(0);
+  ex += base;
+#pragma unroll
+  for (int k = 0; k < kScanPer; k++) {
+    const uint64_t i = b0 + k;
+    if (i < n) out[i] = ex;
+    ex += v[k];
+  }
+  if (write_total && threadIdx.x == 0) out[n] = base + total;  // index n is read by no thread
+}
+
+template <typename T>
+__global__ void k_write_total(T* out, uint64_t n_max, const uint32_t* n_dev, const T* part, uint64_t nb) {
+  const uint64_t n = n_dev ? (uint64_t)*n_dev : n_max;
+  out[n] = part[nb];
+}
+
+// exclusive scan of in[0, n) into out[0, n) (in place allowed) and out[n] = total
+template <typename T>
+static hipError_t scan_impl(const T* in, T* out, uint64_t n_max, const uint32_t* n_dev, T* tmp, uint64_t tmp_cap,
+                            hipStream_t s) {
+  const uint64_t nb = (n_max + kScanBlock - 1) / kScanBlock;
+  if (nb <= 1) {
+    k_scan_apply<T><<<1, 256, 0, s>>>(in, out, n_max, n_dev, nullptr, 1);
+    return hipGetLastError();
+  }
+  if (nb + 1 > tmp_cap) return hipErrorInvalidValue;
+  T* part = tmp;
+  k_scan_reduce<T><<<(unsigned)nb, 256, 0, s>>>(in, n_max, n_dev, part);
+  HIPCHK(hipGetLastError());
+  HIPCHK(scan_impl<T>(part, part, nb, nullptr, tmp + nb + 1, tmp_cap - nb - 1, s));  // part[nb] = total
+  k_scan_apply<T><<<(unsigned)nb, 256, 0, s>>>(in, out, n_max, n_dev, part, 0);
+  HIPCHK(hipGetLastError());
+  k_write_total<T><<<1, 1, 0, s>>>(out, n_max, n_dev, part, nb);
+  return hipGetLastError();
+}
+
+uint64_t scan_tmp_elems(uint64_t n_max) {
+  uint64_t tot = 0;
+  uint64_t n = n_max;
+  for (;;) {
+    const uint64_t nb = (n + kScanBlock - 1) / kScanBlock;
+    if (nb <= 1) break;
+    tot += nb + 1;
+    n = nb;
+  }
+  return tot + 16;
+}
+
+hipError_t scan_u32(const uint32_t* in, uint32_t* out, uint64_t n_max, const uint32_t* n_dev, uint32_t* tmp,
+                    uint64_t tmp_cap, hipStream_t s) {
+  return scan_impl<uint32_t>(in, out, n_max, n_dev, tmp, tmp_cap, s);
+}
+
+hipError_t scan_u64(uint64_t* inout, uint64_t n, uint64_t* tmp, uint64_t tmp_cap, hipStream_t s) {
+  return scan_impl<uint64_t>(inout, inout, n, nullptr, tmp, tmp_cap, s);
+}
+
+// ------------------------------------------------------------------------------------------
+// NFC (src/normalizers.rs:47): quick check per chunk, exact normalisation per flagged doc.
+
+__device__ __forceinline__ uint16_t nfc16(const Tables& t, uint32_t cp) {
+  if (cp >= 0x110000) return 0;
+  return t.nfc_s2[t.nfc_s1[cp >> 8] * 256 + (cp & 255)];
+}
+
+__device__ __forceinline__ int dev_decode(const uint8_t* s, uint32_t n, uint32_t i, uint32_t* cp) {
+  const uint8_t b = s[i];
+  if (b < 0x80) { *cp = b; return 1; }
+  const int len = u8len(b);
+  if (i + len > n) { *cp = 0xFFFD; return 1; }
+  if (len == 2) *cp = ((b & 0x1Fu) << 6) | (s[i + 1] & 0x3Fu);
+  else if (len == 3) *cp = ((b & 0x0Fu) << 12) | ((s[i + 1] & 0x3Fu) << 6) | (s[i + 2] & 0x3Fu);
+  else *cp = ((b & 0x07u) << 18) | ((s[i + 1] & 0x3Fu) << 12) | ((s[i + 2] & 0x3Fu) << 6) | (s[i + 3] & 0x3Fu);
+  return len;
+}
+
+// one thread per 64-byte chunk; a doc is flagged when it holds any code point with
+// NFC_QC != Yes or a non-zero combining class (a superset of the docs NFC changes)
+__global__ void k_nfc_check(const uint8_t* __restrict__ text, uint64_t n_bytes, const uint64_t* __restrict__ off,
+                            uint32_t n_docs, Tables t, uint32_t* doc_flag, uint32_t* counter) {
+  const uint64_t c0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 64;
+  if (c0 >= n_bytes) return;
+  const uint64_t c1 = c0 + 64 < n_bytes ? c0 + 64 : n_bytes;
+  bool ascii = true;
+  if (c1 - c0 == 64) {
+    const uint4* v = reinterpret_cast<const uint4*>(text + c0);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint4 x = v[k];
+      if ((x.x | x.y | x.z | x.w) & 0x80808080u) ascii = false;
+    }
+  } else {
+    for (uint64_t i = c0; i < c1; i++) if (text[i] & 0x80) ascii = false;
+  }
+  if (ascii) return;
+  for (uint64_t i = c0; i < c1;) {
+    const uint8_t b = text[i];
+    if ((b & 0xC0) == 0x80) { i++; continue; }
+    uint32_t cp;
+    const int len = dev_decode(text, (uint32_t)(n_bytes > 0xFFFFFFFFull ? 0xFFFFFFFFu : n_bytes), (uint32_t)i, &cp);
+    const uint16_t f = nfc16(t, cp);
+    if (f != 0) {
+      // doc of byte i: last d with off[d] <= i and off[d+1] > i
+      uint32_t lo = 0, hi = n_docs;  // invariant off[lo] <= i < off[hi]
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (off[mid] <= i) lo = mid; else hi = mid;
+      }
+      if (atomicOr(&doc_flag[lo], 1u) == 0u) atomicAdd(counter, 1u);
+    }
+    i += len;
+  }
+}
+
+hipError_t launch_nfc_check(const uint8_t* text, uint64_t n_bytes, const uint64_t* doc_off, uint32_t n_docs,
+                            const Tables& t, uint32_t* doc_flag, uint32_t* counter, hipStream_t s) {
+  const uint64_t chunks = (n_bytes + 63) / 64;
+  if (chunks) k_nfc_check<<<(unsigned)((chunks + 255) / 256), 256, 0, s>>>(text, n_bytes, doc_off, n_docs, t, doc_flag, counter);
+  return hipGetLastError();
+}
+
+#define SBASE 0xAC00u
+#define LBASE 0x1100u
+#define VBASE 0x1161u
+#define TBASE 0x11A7u
+#define LCOUNT 19u
+#define VCOUNT 21u
+#define TCOUNT 28u
+#define NCOUNT (VCOUNT * TCOUNT)
+#define SCOUNT (LCOUNT * NCOUNT)
+
+__device__ int nfc_decompose(const Tables& t, uint32_t cp, uint32_t* o) {
+  if (cp >= SBASE && cp < SBASE + SCOUNT) {
+    const uint32_t s = cp - SBASE;
+    o[0] = LBASE + s / NCOUNT;
+    o[1] = VBASE + (s % NCOUNT) / TCOUNT;
+    if (s % TCOUNT) { o[2] = TBASE + s % TCOUNT; return 3; }
+    return 2;
+  }
+  int lo = 0, hi = (int)t.n_decomp - 1;
+  while (lo <= hi) {
+    const int mid = (lo + hi) >> 1;
+    const uint32_t c = t.decomp_cp[mid];
+    if (c == cp) {
+      int k = 0;
+      for (uint32_t j = t.decomp_off[mid]; j < t.decomp_off[mid + 1]; j++) o[k++] = t.decomp_data[j];
+      return k;
+    }
+    if (c < cp) lo = mid + 1; else hi = mid - 1;
+  }
+  o[0] = cp;
+  return 1;
+}
+
+__device__ uint32_t nfc_compose(const Tables& t, uint32_t a, uint32_t b) {
+  if (a >= LBASE && a < LBASE + LCOUNT && b >= VBASE && b < VBASE + VCOUNT)
+    return SBASE + ((a - LBASE) * VCOUNT + (b - VBASE)) * TCOUNT;
+  if (a >= SBASE && a < SBASE + SCOUNT && (a - SBASE) % TCOUNT == 0 && b > TBASE && b < TBASE + TCOUNT)
+    return a + (b - TBASE);
+  const uint64_t key = ((uint64_t)a << 21) | b;
+  int lo = 0, hi = (int)t.n_comp - 1;
+  while (lo <= hi) {
+    const int mid = (lo + hi) >> 1;
+    const uint64_t k = t.comp_key[mid];
+    if (k == key) return t.comp_val[mid];
+    if (k < key) lo = mid + 1; else hi = mid - 1;
+  }
+  return kNone;
+}
+
+// full NFC of s[0, n) into buf (capacity 4n code points); returns the code point count
+__device__ uint32_t nfc_doc(const Tables& t, const uint8_t* s, uint32_t n, uint32_t* buf) {
+  uint32_t k = 0;
+  for (uint32_t i = 0; i < n;) {
+    uint32_t cp;
+    i += dev_decode(s, n, i, &cp);
+    k += nfc_decompose(t, cp, buf + k);
+  }
+  for (uint32_t i = 1; i < k; i++) {  // canonical ordering (stable by combining class)
+    const uint32_t c = buf[i];
+    const int cc = nfc16(t, c) & 0xFF;
+    if (!cc) continue;
+    uint32_t j = i;
+    while (j > 0) {
+      const int pc = nfc16(t, buf[j - 1]) & 0xFF;
+      if (pc <= cc || pc == 0) break;
+      buf[j] = buf[j - 1];
+      j--;
+    }
+    buf[j] = c;
+  }
+  if (k == 0) return 0;
+  uint32_t starter = 0, comp = 1, sch = buf[0];
+  int last = nfc16(t, sch) & 0xFF;
+  if (last) last = 256;
+  for (uint32_t i = 1; i < k; i++) {
+    const uint32_t ch = buf[i];
+    const int cc = nfc16(t, ch) & 0xFF;
+    const uint32_t c = nfc_compose(t, sch, ch);
+    if (c != kNone && (last < cc || last == 0)) { buf[starter] = c; sch = c; continue; }
+    if (cc == 0) { starter = comp; sch = ch; }
+    last = cc;
+    buf[comp++] = ch;
+  }
+  return comp;
+}
+
+__device__ __forceinline__ uint32_t u8size(uint32_t cp) { return cp < 0x80 ? 1 : cp < 0x800 ? 2 : cp < 0x10000 ? 3 : 4; }
+
+// phase 0: new_len[d] = normalised length (flagged docs: NFC code points left in cp_scratch)
+// phase 1: write the normalised text at new_off[d] (new_len scanned into offsets)
+__global__ void k_norm(const uint8_t* __restrict__ text, const uint64_t* __restrict__ off, uint32_t n_docs,
+                       const uint32_t* __restrict__ doc_flag, int add_prefix, int nfc, Tables t,
+                       uint32_t* cp_scratch, uint32_t* ncp, uint64_t* newv, uint8_t* out, int phase) {
+  const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= n_docs) return;
+  const uint64_t a = off[d];
+  const uint32_t n = (uint32_t)(off[d + 1] - a);
+  const bool flagged = nfc && doc_flag[d];
+  uint32_t* buf = cp_scratch + 4 * a;
+  if (phase == 0) {
+    uint64_t len;
+    uint32_t first;
+    if (flagged) {
+      const uint32_t k = nfc_doc(t, text + a, n, buf);
+      ncp[d] = k;
+      len = 0;
+      for (uint32_t i = 0; i < k; i++) len += u8size(buf[i]);
+      first = k ? buf[0] : 0;
+    } else {
+      len = n;
+      first = n ? text[a] : 0;
+    }
+    if (add_prefix && len > 0 && first != ' ') len += 1;  // src/pretokenizers.rs:163-167
+    newv[d] = len;
+  } else {
+    uint8_t* o = out + newv[d];
+    const uint64_t o_end = newv[d + 1];
+    uint64_t len = 0;
+    if (flagged) {
+      const uint32_t k = ncp[d];
+      for (uint32_t i = 0; i < k; i++) len += u8size(buf[i]);
+      if (add_prefix && k > 0 && buf[0] != ' ') *o++ = ' ';
+      for (uint32_t i = 0; i < k; i++) {
+        const uint32_t c = buf[i];
+        if (c < 0x80) { *o++ = (uint8_t)c; }
+        else if (c < 0x800) { *o++ = (uint8_t)(0xC0 | (c >> 6)); *o++ = (uint8_t)(0x80 | (c & 0x3F)); }
+        else if (c < 0x10000) { *o++ = (uint8_t)(0xE0 | (c >> 12)); *o++ = (uint8_t)(0x80 | ((c >> 6) & 0x3F)); *o++ = (uint8_t)(0x80 | (c & 0x3F)); }
+        else { *o++ = (uint8_t)(0xF0 | (c >> 18)); *o++ = (uint8_t)(0x80 | ((c >> 12) & 0x3F)); *o++ = (uint8_t)(0x80 | ((c >> 6) & 0x3F)); *o++ = (uint8_t)(0x80 | (c & 0x3F)); }
+      }
+    } else {
+      if (add_prefix && n > 0 && text[a] != ' ') *o++ = ' ';
+      for (uint32_t i = 0; i < n; i++) *o++ = text[a + i];
+    }
+    (void)o_end;
+    (void)len;
+  }
+}
+
+hipError_t launch_norm(const uint8_t* text, const uint64_t* doc_off, uint32_t n_docs, const uint32_t* doc_flag,
+                       int add_prefix, int nfc, const Tables& t, uint32_t* cp_scratch, uint32_t* ncp,
+                       uint64_t* newv, uint8_t* out, int phase, hipStream_t s) {
+  if (n_docs) k_norm<<<(n_docs + 255) / 256, 256, 0, s>>>(text, doc_off, n_docs, doc_flag, add_prefix, nfc, t,
+                                                        cp_scratch, ncp, newv, out, phase);
+  return hipGetLastError();
+}
+
+void upload_done() {}
+
+}  // namespace ctok_dev

@@ -1,0 +1,110 @@
+/* ctok.h -- C ABI of the MI355X-native batch ByteLevel-BPE encode path.
+ *
+ * Drop-in boundary for the reference's PyO3 class `complexity_tokenizer.Tokenizer`
+ * (Complexity-ML/complexity-tokenizer v0.3.3, src/bindings/tokenizer.rs:11-14, registered at
+ * src/lib.rs:49).  Every entry point below names the reference method it replaces.  Plain
+ * pointers and sizes only; no torch or HIP types appear in the signatures (the stream is an
+ * opaque `void*` that the library casts to hipStream_t).
+ *
+ * Ownership: a `ctok*` is immutable after creation and safe to share between threads; calls on
+ * the same device serialise on that device's workspace.  Errors: every `int` return is 0
+ * (CTOK_OK) or a negative CTOK_E_* code; ctok_last_error() returns the message of the calling
+ * thread's last failure.
+ */
+#ifndef CTOK_H
+#define CTOK_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ctok ctok;
+
+enum {
+  CTOK_OK = 0,
+  CTOK_E_IO = -1,          /* file open/read failure              -> Python IOError   */
+  CTOK_E_PARSE = -2,       /* JSON / schema failure (serde error) -> Python IOError   */
+  CTOK_E_UNSUPPORTED = -3, /* component outside the encode hot path (e.g. Metaspace)  */
+  CTOK_E_ARG = -4,         /* bad argument (null pointer, unsorted offsets, ...)      */
+  CTOK_E_CAPACITY = -5,    /* ids_cap too small; tok_off[n_docs] holds the size needed */
+  CTOK_E_PANIC = -6,       /* the reference would panic (src/bpe.rs:141 index OOB)   */
+  CTOK_E_DEVICE = -7,      /* HIP runtime failure                                     */
+  CTOK_E_NOTFOUND = -8     /* token_to_id / id_to_token miss (Python None)            */
+};
+
+/* Message of the calling thread's last failing call ("" if none). */
+const char* ctok_last_error(void);
+/* Library version string, e.g. "0.3.3+mi355x.1". */
+const char* ctok_version(void);
+
+/* Tokenizer.from_file(path)                 src/bindings/tokenizer.rs:18-23
+ *   -> HuggingFaceTokenizer::from_file       src/huggingface/mod.rs:159-166, :247-334 */
+int ctok_create_from_file(const char* path, ctok** out);
+/* HuggingFaceTokenizer::from_str / from_buffer   src/huggingface/mod.rs:168-180 */
+int ctok_create_from_buffer(const char* json, size_t len, ctok** out);
+void ctok_destroy(ctok* tok);
+
+/* Tokenizer.vocab_size                      src/bindings/tokenizer.rs:271-274 -> mod.rs:856-858 */
+uint64_t ctok_vocab_size(const ctok* tok);
+/* Tokenizer.token_to_id(token)              src/bindings/tokenizer.rs:276-278 -> mod.rs:860-862 */
+int ctok_token_to_id(const ctok* tok, const char* token, size_t len, uint32_t* id);
+/* Tokenizer.id_to_token(id)                 src/bindings/tokenizer.rs:280-282 -> mod.rs:864-866
+ * Writes up to cap bytes and sets *len to the full length (call again with a larger buffer). */
+int ctok_id_to_token(const ctok* tok, uint32_t id, char* buf, size_t cap, size_t* len);
+/* Tokenizer.special_tokens (dict)           src/bindings/tokenizer.rs:284-289 */
+uint64_t ctok_num_special_tokens(const ctok* tok);
+int ctok_special_token(const ctok* tok, uint64_t i, char* buf, size_t cap, size_t* len, uint32_t* id);
+
+/* Execution / measurement options for one encode call. */
+typedef struct ctok_exec {
+  int device;       /* HIP device ordinal the work runs on                              */
+  void* stream;     /* hipStream_t to order the work on; NULL = the library's stream      */
+  uint32_t flags;   /* CTOK_F_* */
+} ctok_exec;
+
+#define CTOK_F_TIMING 1u  /* record per-kernel HIP events (fills ctok_stats.ms_*) */
+
+typedef struct ctok_stats {
+  double ms_total;        /* wall time of the call (host clock)                        */
+  double ms_device;       /* first kernel start -> last kernel end (HIP events)        */
+  double ms_bpe;          /* BPE merge kernels (short + long pieces)                   */
+  double ms_pretok;       /* normalise check + pre-tokenizer + piece list              */
+  double ms_emit;         /* token-count scan + compaction                             */
+  double ms_h2d, ms_d2h;  /* host-buffer copies (ctok_encode_batch only)               */
+  uint64_t bytes_in;      /* raw UTF-8 bytes of the batch                              */
+  uint64_t bytes_norm;    /* bytes after normalisation / prefix space                  */
+  uint64_t docs, pieces, long_pieces, tokens, nfc_docs;
+} ctok_stats;
+
+/* Upper bound on the ids of a batch whose docs total `n_bytes` bytes (ids <= 3*bytes + docs:
+ * NFC can grow UTF-8 at most 3x, add_prefix_space adds one byte per doc). */
+uint64_t ctok_ids_bound(const ctok* tok, uint64_t n_bytes, uint64_t n_docs);
+
+/* Tokenizer.encode_batch(texts) on host buffers   src/bindings/tokenizer.rs:207-210
+ *   -> HuggingFaceTokenizer::encode_batch          src/huggingface/mod.rs:694-696
+ * utf8[doc_off[d] .. doc_off[d+1]) is document d (valid UTF-8, doc_off[0] == 0,
+ * non-decreasing).  On success ids[tok_off[d] .. tok_off[d+1]) are its token ids.
+ * Tokenizer.encode(text) is the n_docs == 1 case (src/bindings/tokenizer.rs:203-205). */
+int ctok_encode_batch(const ctok* tok, const uint8_t* utf8, const uint64_t* doc_off, uint64_t n_docs,
+                      uint32_t* ids, uint64_t ids_cap, uint64_t* tok_off,
+                      const ctok_exec* exec, ctok_stats* stats);
+
+/* Same, with every buffer already resident in HBM of exec->device (device pointers) and the
+ * work ordered on exec->stream.  n_bytes = doc_off[n_docs] (passed so the host need not read
+ * device memory).  *n_tokens_out (host) receives the total number of ids written. */
+int ctok_encode_batch_device(const ctok* tok, const uint8_t* d_utf8, const uint64_t* d_doc_off,
+                             uint64_t n_docs, uint64_t n_bytes, uint32_t* d_ids, uint64_t ids_cap,
+                             uint64_t* d_tok_off, uint64_t* n_tokens_out,
+                             const ctok_exec* exec, ctok_stats* stats);
+
+/* Number of HIP devices visible to the library (0 when none; encode calls then fail with
+ * CTOK_E_DEVICE -- there is no CPU fallback). */
+int ctok_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CTOK_H */

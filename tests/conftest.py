@@ -1,0 +1,42 @@
+"""pytest configuration: import paths, the `gpu` marker and shared fixtures.
+
+`-m "not gpu"` tests run on any CPU host (oracle vs golden vectors, loader, C-ABI exports);
+`-m gpu` tests need an MI355X and compare the HIP path with the oracle (tests/README in
+DESIGN.md section 6).
+"""
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "complexity-tokenizer_amd")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device) -- parity tests of the HIP path")
+
+
+@pytest.fixture(scope="session")
+def fixture_dir(tmp_path_factory):
+    return str(tmp_path_factory.mktemp("tokjson"))
+
+
+@pytest.fixture(scope="session")
+def gpt2_path(fixture_dir):
+    from datagen.build_tokenizers import fixture_path
+    return fixture_path("gpt2_50k", fixture_dir)
+
+
+@pytest.fixture(scope="session")
+def llama3_path(fixture_dir):
+    from datagen.build_tokenizers import fixture_path
+    return fixture_path("llama3_128k", fixture_dir)
+
+
+@pytest.fixture(scope="session")
+def multi_path(fixture_dir):
+    from datagen.build_tokenizers import fixture_path
+    return fixture_path("multi_32k", fixture_dir)

@@ -1,0 +1,169 @@
+"""Parity of the HIP path (libctok.so through the C ABI) with the CPU oracle.
+
+Bit-exact token ids are required (integer work).  Oracle: oracle/ref_py.py (Python
+restatement of the reference) for small inputs, oracle/ctok_ref.c (faithful C port, checked
+against ref_py in tests/test_oracle.py) for large ones, plus the committed golden vectors.
+"""
+import json
+
+import numpy as np
+import pytest
+
+from complexity_tokenizer import PanicException, Tokenizer
+from datagen import corpus
+from oracle import ref_c, ref_py
+from tests import edge_cases, toys
+
+pytestmark = pytest.mark.gpu
+
+
+def gpu_tok(obj):
+    return Tokenizer.from_str(json.dumps(obj))
+
+
+def assert_same(gpu_ids, gpu_off, ref_ids, ref_off):
+    assert len(gpu_off) == len(ref_off)
+    if not (np.array_equal(gpu_off, ref_off) and np.array_equal(gpu_ids, ref_ids)):
+        bad = np.flatnonzero(gpu_off != ref_off)
+        d = int(bad[0]) - 1 if len(bad) else -1
+        if d < 0:
+            d = next(i for i in range(len(gpu_off) - 1)
+                     if not np.array_equal(gpu_ids[gpu_off[i]:gpu_off[i + 1]], ref_ids[ref_off[i]:ref_off[i + 1]]))
+        raise AssertionError("doc %d differs: gpu %s ref %s" % (
+            d, gpu_ids[gpu_off[d]:gpu_off[d + 1]].tolist(), ref_ids[ref_off[d]:ref_off[d + 1]].tolist()))
+
+
+@pytest.fixture(scope="module")
+def gpt2(gpt2_path):
+    with open(gpt2_path) as f:
+        obj = json.load(f)
+    return obj, Tokenizer.from_file(gpt2_path), ref_c.RefC(obj)
+
+
+def test_hello_kat():
+    assert gpu_tok(toys.hello_kat()).encode("hello") == [8]
+
+
+def test_edge_cases_vs_python_oracle(gpt2):
+    obj, tok, _ = gpt2
+    py = ref_py.RefTokenizer(obj)
+    got = tok.encode_batch(edge_cases.EDGE)
+    for s, g in zip(edge_cases.EDGE, got):
+        assert g == py.encode(s), repr(s)
+
+
+def test_c1_vs_oracles(gpt2):
+    obj, tok, rc = gpt2
+    text, off = corpus.corpus_c1()
+    ids, toff = tok.encode_packed(text, off)
+    rids, rtoff = rc.encode_packed(text, off)
+    assert_same(ids, toff, rids, rtoff)
+    py = ref_py.RefTokenizer(obj)
+    docs = [d.decode() for d in corpus.unpack(text, off)]
+    assert [ids[toff[i]:toff[i + 1]].tolist() for i in range(len(docs))] == py.encode_batch(docs)
+
+
+def test_c2_sample_vs_c_oracle(gpt2):
+    _, tok, rc = gpt2
+    text, off = corpus.corpus_c2(100_000)
+    ids, toff = tok.encode_packed(text, off)
+    assert_same(ids, toff, *rc.encode_packed(text, off))
+
+
+def test_long_pieces(gpt2):
+    obj, tok, rc = gpt2
+    docs = edge_cases.long_docs()
+    text, off = corpus.pack([d.encode() for d in docs])
+    ids, toff = tok.encode_packed(text, off)
+    assert_same(ids, toff, *rc.encode_packed(text, off))
+    assert tok.last_stats["long_pieces"] > 0
+
+
+def test_random_unicode(gpt2):
+    obj, tok, rc = gpt2
+    docs = edge_cases.random_unicode_docs(20_000, seed=11)
+    text, off = corpus.pack([d.encode() for d in docs])
+    ids, toff = tok.encode_packed(text, off)
+    assert_same(ids, toff, *rc.encode_packed(text, off))
+    py = ref_py.RefTokenizer(obj)
+    for i in range(0, 2000):
+        assert ids[toff[i]:toff[i + 1]].tolist() == py.encode(docs[i]), repr(docs[i])
+
+
+def test_empty_batch_and_empty_docs(gpt2):
+    _, tok, _ = gpt2
+    assert tok.encode_batch([]) == []
+    assert tok.encode_batch(["", "", ""]) == [[], [], []]
+    assert tok.encode("") == []
+    r = tok.encode_batch(["", "a b", "", "", "c"])
+    assert r[0] == [] and r[2] == [] and r[3] == [] and len(r[1]) > 0 and len(r[4]) > 0
+
+
+def test_llama3_sample(llama3_path):
+    with open(llama3_path) as f:
+        obj = json.load(f)
+    tok = Tokenizer.from_file(llama3_path)
+    rc = ref_c.RefC(obj)
+    text, off = corpus.corpus_c3(3000, seed=33)
+    ids, toff = tok.encode_packed(text, off)
+    assert_same(ids, toff, *rc.encode_packed(text, off))
+
+
+def test_multi_sample(multi_path):
+    with open(multi_path) as f:
+        obj = json.load(f)
+    tok = Tokenizer.from_file(multi_path)
+    rc = ref_c.RefC(obj)
+    text, off = corpus.corpus_c5(20_000, seed=55)
+    ids, toff = tok.encode_packed(text, off)
+    assert_same(ids, toff, *rc.encode_packed(text, off))
+
+
+def test_improper_table(gpt2):
+    obj, _, _ = gpt2
+    sh = toys.shuffled_merges(obj, seed=3)
+    tok, rc = gpu_tok(sh), ref_c.RefC(sh)
+    docs = edge_cases.long_docs() + edge_cases.EDGE
+    text, off = corpus.pack([d.encode() for d in docs])
+    ids, toff = tok.encode_packed(text, off)
+    assert_same(ids, toff, *rc.encode_packed(text, off))
+    text, off = corpus.corpus_c2(20_000, seed=9)
+    ids, toff = tok.encode_packed(text, off)
+    assert_same(ids, toff, *rc.encode_packed(text, off))
+
+
+def _parity_or_panic(tok, rc, text, off):
+    try:
+        want = rc.encode_packed(text, off)
+    except ref_py.PanicException:
+        with pytest.raises(PanicException):
+            tok.encode_packed(text, off)
+        return "panic"
+    assert_same(*tok.encode_packed(text, off), *want)
+    return "ok"
+
+
+def test_invalid_merges_shift_and_panic(gpt2):
+    obj, _, _ = gpt2
+    text, off = corpus.corpus_c2(20_000, seed=12)
+    seen = set()
+    for seed in range(3):
+        bad = toys.with_invalid_merges(obj, seed=seed, n_bad=30)
+        seen.add(_parity_or_panic(gpu_tok(bad), ref_c.RefC(bad), text, off))
+    # invalid merges only at the tail: indices of valid merges unchanged, never a panic
+    tail = toys.with_invalid_merges(obj, seed=4, n_bad=30, tail_only=True)
+    assert _parity_or_panic(gpu_tok(tail), ref_c.RefC(tail), text, off) == "ok"
+
+
+def test_panic_toy():
+    # rank of (a, b) is 1 but only one merge is valid: BpeTokenizer.merges[1] is out of range
+    bc = toys.byte_chars()
+    vocab = {c: i for i, c in enumerate(bc)}
+    vocab["ab"] = 256
+    obj = toys.tok_json(vocab, [("x", "yy"), ("a", "b")])
+    tok = gpu_tok(obj)
+    assert tok.encode("ba") == ref_py.RefTokenizer(obj).encode("ba")
+    with pytest.raises(PanicException):
+        tok.encode("ab")
+    with pytest.raises(ref_py.PanicException):
+        ref_py.RefTokenizer(obj).encode("ab")

@@ -1,0 +1,67 @@
+"""Small hand-built tokenizer.json objects for edge-case tests (shared by CPU and GPU tests)."""
+import json
+import random
+
+
+def byte_chars():
+    bs = list(range(0x21, 0x7F)) + list(range(0xA1, 0xAD)) + list(range(0xAE, 0x100))
+    cs = list(bs)
+    n = 0
+    for b in range(256):
+        if b not in bs:
+            bs.append(b)
+            cs.append(256 + n)
+            n += 1
+    return [chr(c) for c in cs]
+
+
+def tok_json(vocab, merges, added=(), normalizer=None, pre_tokenizer=None, merges_as_arrays=False):
+    obj = {"version": "1.0", "added_tokens": list(added), "normalizer": normalizer,
+           "pre_tokenizer": pre_tokenizer if pre_tokenizer is not None else
+           {"type": "ByteLevel", "add_prefix_space": False, "trim_offsets": True, "use_regex": True},
+           "post_processor": None, "decoder": None,
+           "model": {"type": "BPE", "vocab": vocab,
+                     "merges": [[a, b] for a, b in merges] if merges_as_arrays else ["%s %s" % m for m in merges]}}
+    return obj
+
+
+def hello_kat():
+    """reference src/bpe.rs:219-250 (toy vocab, lowest rank first) as a tokenizer.json."""
+    vocab = {"h": 0, "e": 1, "l": 2, "o": 3, "he": 4, "ll": 5, "hel": 6, "hell": 7, "hello": 8, "lo": 9, "llo": 10}
+    merges = [("h", "e"), ("he", "l"), ("hel", "l"), ("hell", "o"), ("l", "l"), ("l", "o"), ("l", "lo")]
+    return tok_json(vocab, merges)
+
+
+def loader_kat():
+    """reference src/huggingface/mod.rs:1566-1592."""
+    return {"version": "1.0", "model": {"type": "BPE", "vocab": {"h": 0, "e": 1, "l": 2, "o": 3, " ": 4, "w": 5,
+                                                                  "r": 6, "d": 7}, "merges": []},
+            "added_tokens": []}
+
+
+def derived(base_obj, mutate):
+    obj = json.loads(json.dumps(base_obj))
+    mutate(obj)
+    return obj
+
+
+def shuffled_merges(base_obj, seed):
+    """Same vocab, merge list permuted: valid merges with non-monotone ranks (improper table)."""
+    def m(o):
+        ms = list(o["model"]["merges"])
+        random.Random(seed).shuffle(ms)
+        o["model"]["merges"] = ms
+    return derived(base_obj, m)
+
+
+def with_invalid_merges(base_obj, seed, n_bad=50, tail_only=False):
+    """Insert merges whose parts are not in the vocab: shifts BpeTokenizer.merges indices
+    (reference src/bpe.rs:60-69 quirk); ranks past the valid list make lookups panic."""
+    def m(o):
+        ms = list(o["model"]["merges"])
+        rng = random.Random(seed)
+        for k in range(n_bad):
+            pos = len(ms) if tail_only else rng.randrange(len(ms) + 1)
+            ms.insert(pos, "zz%dq qq%dz" % (k, k))
+        o["model"]["merges"] = ms
+    return derived(base_obj, m)
