@@ -195,6 +195,21 @@ class Tokenizer:
             self.last_stats = st.as_dict()
             return ids[: int(tok_off[-1])], tok_off
 
+    def encode_packed_device(self, d_text: int, d_off: int, n_docs: int, n_bytes: int, d_ids: int, ids_cap: int,
+                             d_tok_off: int, stream: int = 0, timing: bool = False, device: int | None = None):
+        """Extension: encode a batch already resident in HBM (raw device pointers, e.g. from
+        torch tensors' data_ptr()).  Work is ordered on `stream` (a hipStream_t as int, 0 = the
+        library's own stream).  Returns the total number of ids written; stats in last_stats."""
+        ex = _n.Exec(self.device if device is None else device, stream or None, _n.CTOK_F_TIMING if timing else 0)
+        st = _n.Stats()
+        ntok = ctypes.c_uint64()
+        rc = _n.lib.ctok_encode_batch_device(self._h, d_text, d_off, n_docs, n_bytes, d_ids, ids_cap, d_tok_off,
+                                             ctypes.byref(ntok), ctypes.byref(ex), ctypes.byref(st))
+        if rc != _n.CTOK_OK:
+            _raise(rc)
+        self.last_stats = st.as_dict()
+        return int(ntok.value)
+
     def encode_batch_flat(self, texts):
         """Extension: list[str] -> (ids uint32[T], tok_off uint64[D+1])."""
         text, off = pack_texts(texts)

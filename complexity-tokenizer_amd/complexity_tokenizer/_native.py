@@ -35,8 +35,9 @@ class Exec(ctypes.Structure):
 
 
 class Stats(ctypes.Structure):
-    _fields_ = [("ms_total", ctypes.c_double), ("ms_device", ctypes.c_double), ("ms_bpe", ctypes.c_double),
-                ("ms_pretok", ctypes.c_double), ("ms_emit", ctypes.c_double), ("ms_h2d", ctypes.c_double),
+    _fields_ = [("ms_total", ctypes.c_double), ("ms_device", ctypes.c_double), ("ms_pretok", ctypes.c_double),
+                ("ms_bpe_short", ctypes.c_double), ("ms_bpe_long", ctypes.c_double),
+                ("ms_emit", ctypes.c_double), ("ms_h2d", ctypes.c_double),
                 ("ms_d2h", ctypes.c_double), ("bytes_in", ctypes.c_uint64), ("bytes_norm", ctypes.c_uint64),
                 ("docs", ctypes.c_uint64), ("pieces", ctypes.c_uint64), ("long_pieces", ctypes.c_uint64),
                 ("tokens", ctypes.c_uint64), ("nfc_docs", ctypes.c_uint64)]

@@ -643,13 +643,15 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
     st->tokens = ntok;
     st->nfc_docs = nfc_docs;
     if (timing) {
-      float a = 0, b = 0, c = 0, d = 0;
+      float a = 0, b = 0, b2 = 0, c = 0, d = 0;
       HIPTRY(hipEventElapsedTime(&a, ds->ev[0], ds->ev[1]));
-      HIPTRY(hipEventElapsedTime(&b, ds->ev[1], ds->ev[3]));
+      HIPTRY(hipEventElapsedTime(&b, ds->ev[1], ds->ev[2]));
+      HIPTRY(hipEventElapsedTime(&b2, ds->ev[2], ds->ev[3]));
       HIPTRY(hipEventElapsedTime(&c, ds->ev[3], ds->ev[4]));
       HIPTRY(hipEventElapsedTime(&d, ds->ev[0], ds->ev[4]));
       st->ms_pretok = a;
-      st->ms_bpe = b;
+      st->ms_bpe_short = b;
+      st->ms_bpe_long = b2;
       st->ms_emit = c;
       st->ms_device = d;
     }

@@ -70,8 +70,9 @@ typedef struct ctok_exec {
 typedef struct ctok_stats {
   double ms_total;        /* wall time of the call (host clock)                        */
   double ms_device;       /* first kernel start -> last kernel end (HIP events)        */
-  double ms_bpe;          /* BPE merge kernels (short + long pieces)                   */
   double ms_pretok;       /* normalise check + pre-tokenizer + piece list              */
+  double ms_bpe_short;    /* BPE merge kernel, pieces <= 32 bytes (thread per piece)   */
+  double ms_bpe_long;     /* BPE merge kernels, longer pieces (wavefront per piece)    */
   double ms_emit;         /* token-count scan + compaction                             */
   double ms_h2d, ms_d2h;  /* host-buffer copies (ctok_encode_batch only)               */
   uint64_t bytes_in;      /* raw UTF-8 bytes of the batch                              */

@@ -1,0 +1,118 @@
+#!/usr/bin/env python3
+"""Generate the committed golden vectors (run in the dev container; the outputs are data).
+
+  c1_gpt2_50k.npz     C1 corpus (1,000 docs) + ids from the Python oracle (ref_py), which is a
+                      line-by-line restatement of the reference; cross-checked with the C oracle.
+  edge_gpt2_50k.json  tests/edge_cases.py documents + their ids (ref_py).
+  digests.json        sha256 over (tok_off u64 LE, ids u32 LE) for the full benchmark configs,
+                      computed with the C oracle (ctok_ref.c), itself checked against ref_py on a
+                      sample of the same corpus first.  Also digests of the first 100k docs (CPU tests).
+
+Usage: python tests/golden/make_golden.py [c1 edge c2 c3 c5]
+"""
+import hashlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+from datagen import corpus  # noqa: E402
+from datagen.build_tokenizers import fixture_path  # noqa: E402
+from oracle import ref_c, ref_py  # noqa: E402
+from tests import edge_cases  # noqa: E402
+
+TMP = "/tmp/ctok_golden"
+
+
+def digest(ids, tok_off):
+    h = hashlib.sha256()
+    h.update(np.ascontiguousarray(tok_off, dtype="<u8").tobytes())
+    h.update(np.ascontiguousarray(ids, dtype="<u4").tobytes())
+    return h.hexdigest()
+
+
+def load(name):
+    p = fixture_path(name, TMP)
+    with open(p) as f:
+        return json.load(f)
+
+
+def c1():
+    obj = load("gpt2_50k")
+    py = ref_py.RefTokenizer(obj)
+    text, off = corpus.corpus_c1()
+    docs = [d.decode() for d in corpus.unpack(text, off)]
+    res = py.encode_batch(docs)
+    ids = np.array([i for r in res for i in r], dtype=np.uint32)
+    tok_off = np.zeros(len(res) + 1, dtype=np.uint64)
+    np.cumsum([len(r) for r in res], out=tok_off[1:])
+    cids, coff = ref_c.RefC(obj).encode_packed(text, off)
+    assert np.array_equal(cids, ids) and np.array_equal(coff, tok_off)
+    np.savez_compressed(os.path.join(HERE, "c1_gpt2_50k.npz"), text=text, off=off, ids=ids, tok_off=tok_off)
+    print("c1:", len(docs), "docs", len(ids), "ids")
+
+
+def edge():
+    obj = load("gpt2_50k")
+    py = ref_py.RefTokenizer(obj)
+    docs = edge_cases.EDGE + edge_cases.long_docs()
+    out = [[d, py.encode(d)] for d in docs]
+    with open(os.path.join(HERE, "edge_gpt2_50k.json"), "w") as f:
+        json.dump(out, f, ensure_ascii=True)
+    print("edge:", len(out), "docs")
+
+
+CONFIGS = {  # name -> (tokenizer fixture, corpus fn)
+    "C2": ("gpt2_50k", corpus.corpus_c2),
+    "C3": ("llama3_128k", corpus.corpus_c3),
+    "C5": ("multi_32k", corpus.corpus_c5),
+}
+
+
+def big(name):
+    tok, fn = CONFIGS[name]
+    obj = load(tok)
+    t = time.time()
+    text, off = fn()
+    print(name, "corpus", len(off) - 1, "docs", len(text), "bytes in %.1fs" % (time.time() - t))
+    rc = ref_c.RefC(obj)
+    py = ref_py.RefTokenizer(obj)
+    # pin the C oracle against the Python restatement on a sample of this corpus
+    ns = 3000
+    sample_docs = [d.decode() for d in corpus.unpack(text[: int(off[ns])], off[: ns + 1])]
+    want = py.encode_batch(sample_docs)
+    got = rc.encode_batch(sample_docs)
+    assert want == got, name + ": C oracle disagrees with ref_py on the sample"
+    t = time.time()
+    ids, tok_off = rc.encode_packed(text, off)
+    print(name, "C oracle %.1fs" % (time.time() - t), len(ids), "ids")
+    n1 = min(100_000, len(off) - 1)
+    ids1, off1 = ids[: int(tok_off[n1])], tok_off[: n1 + 1]
+    path = os.path.join(HERE, "digests.json")
+    d = json.load(open(path)) if os.path.exists(path) else {}
+    d[name] = {"tokenizer": tok, "docs": len(off) - 1, "bytes": int(len(text)), "tokens": int(len(ids)),
+               "sha256": digest(ids, tok_off), "first_docs": n1, "first_tokens": int(len(ids1)),
+               "first_sha256": digest(ids1, off1)}
+    with open(path, "w") as f:
+        json.dump(d, f, indent=1, sort_keys=True)
+
+
+def main(args):
+    os.makedirs(TMP, exist_ok=True)
+    for a in args or ["c1", "edge", "c2", "c3", "c5"]:
+        if a == "c1":
+            c1()
+        elif a == "edge":
+            edge()
+        else:
+            big(a.upper())
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])
