@@ -169,7 +169,7 @@ struct DeviceState {
   DevBuf<uint64_t> comp_key;
   Tables t{};
   // workspace
-  DevBuf<uint32_t> docbits, pbits, tile_cnt, word_prefix, pstart, pcnt, scratch, doc_piece, long_list, counters, lw;
+  DevBuf<uint32_t> docbits, pbits, tile_cnt, word_prefix, pstart, pcnt, scratch, doc_piece, long_list, mid_list, region, cnt16, counters, lw;
   DevBuf<uint64_t> scan_tmp;
   DevBuf<uint32_t> doc_flag, ncp;
   DevBuf<uint64_t> norm_off;
@@ -207,6 +207,7 @@ struct ctok {
   std::vector<uint32_t> at_off{0}, at_id;
   std::vector<uint8_t> at_flags;
   bool proper = true;
+  bool compact = false;
   // per device
   std::mutex dev_mu;
   std::map<int, std::unique_ptr<DeviceState>> devs;
@@ -343,6 +344,18 @@ void load(ctok* t, const char* buf, size_t len) {
   }
   if (merges.size() >= (size_t)kNoRank - 2) throw_err(CTOK_E_UNSUPPORTED, "more than 4M merges");
   t->rank_newid = valid_new;
+  // compact table: values are the new ids themselves when new id is strictly increasing in rank
+  {
+    std::vector<std::pair<uint32_t, uint32_t>> rv;  // (rank, new id) of the entries that can merge
+    rv.reserve(ranks.size());
+    for (const auto& kv : ranks)
+      if (kv.second < valid_new.size()) rv.push_back({kv.second, valid_new[kv.second]});
+    std::sort(rv.begin(), rv.end());
+    t->compact = true;
+    for (size_t i = 1; i < rv.size(); i++)
+      if (rv[i].second <= rv[i - 1].second) { t->compact = false; break; }
+    if (getenv("CTOK_FORCE_WIDE")) t->compact = false;
+  }
   size_t cap = 1024;
   while (cap < ranks.size() * 2 + 16) cap <<= 1;
   t->merge_tab.assign(cap, kEmpty);
@@ -350,7 +363,9 @@ void load(ctok* t, const char* buf, size_t len) {
   for (const auto& kv : ranks) {
     uint32_t a = (uint32_t)(kv.first >> 32), b = (uint32_t)kv.first;
     if (a > kMaxId || b > kMaxId) throw_err(CTOK_E_UNSUPPORTED, "token ids above 2^21-2 are not supported by the device merge table");
-    uint64_t e = ((uint64_t)kv.second << 42) | ((uint64_t)a << kIdBits) | b;
+    uint64_t val = kv.second;
+    if (t->compact) val = kv.second < valid_new.size() ? valid_new[kv.second] : kPanicVal;
+    uint64_t e = (val << 42) | ((uint64_t)a << kIdBits) | b;
     uint32_t h = mhash_host(a, b) & t->merge_mask;
     while (t->merge_tab[h] != kEmpty) h = (h + 1) & t->merge_mask;
     t->merge_tab[h] = e;
@@ -507,6 +522,7 @@ DeviceState* device_state(ctok* t, int device) {
   tb.at_flags = ds->at_flags.p;
   tb.n_at = (uint32_t)t->at_id.size();
   tb.proper = (t->proper && !getenv("CTOK_FORCE_IMPROPER")) ? 1 : 0;
+  tb.compact = t->compact ? 1 : 0;
   tb.dbg = getenv("CTOK_DBG_MODE") ? (uint32_t)atoi(getenv("CTOK_DBG_MODE")) : 0;
   DeviceState* r = ds.get();
   t->devs[device] = std::move(ds);
@@ -598,6 +614,11 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   ds->scratch.ensure(B + 2);
   ds->doc_piece.ensure(n_docs + 2);
   ds->long_list.ensure(B / kShortMax + 2);
+  ds->mid_list.ensure(B / 2 + 2);
+  uint32_t grid1 = (uint32_t)std::min<uint64_t>(16384, std::max<uint64_t>(1, (B / 4 + 2047) / 2048));
+  uint32_t region_len = (uint32_t)((B + 1 + grid1 - 1) / grid1);  // pieces <= B: per-block share
+  ds->region.ensure((size_t)grid1 * region_len + 16);
+  ds->cnt16.ensure(2 * (size_t)grid1 + 18);  // [cnt16 | cntmid], each grid1 + 1
   ds->lw.ensure(4 * B + 64);
   ds->scan_tmp.ensure(scan_tmp_elems(std::max<uint64_t>(B + 1, n_docs + 1)) + 64);
   w.docbits = ds->docbits.p;
@@ -609,6 +630,12 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   w.scratch = ds->scratch.p;
   w.doc_piece = ds->doc_piece.p;
   w.long_list = ds->long_list.p;
+  w.mid_list = ds->mid_list.p;
+  w.region = ds->region.p;
+  w.region_len = region_len;
+  w.grid1 = grid1;
+  w.cnt16 = ds->cnt16.p;
+  w.cntmid = ds->cnt16.p + grid1 + 1;
   w.counters = ds->counters.p;
   w.lw = ds->lw.p;
   w.scan_tmp = (uint32_t*)ds->scan_tmp.p;

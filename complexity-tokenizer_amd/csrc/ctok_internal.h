@@ -14,7 +14,7 @@ constexpr uint32_t kIdBits = 21;
 constexpr uint64_t kKeyMask = (1ull << 42) - 1;
 constexpr uint32_t kNoRank = 0x3FFFFFu;      // "no merge" (22-bit all ones)
 constexpr uint32_t kMaxId = (1u << kIdBits) - 2;
-constexpr uint32_t kPanicId = 0xFFFFFFFFu;   // rank_newid value for an out-of-range rank
+constexpr uint32_t kPanicVal = kNoRank - 1;  // compact-table value of an entry whose lookup panics
 
 // Error bits written by kernels into Workspace::err (host checks after the call).
 constexpr uint32_t kErrPanic = 1u;
@@ -49,6 +49,7 @@ struct Tables {            // device pointers, owned by the host runtime
   const uint8_t* at_flags;  // bit0 single_word, bit1 lstrip, bit2 rstrip
   uint32_t n_at;
   uint32_t proper;          // 1: merge table is rank-monotone (parallel same-rank rounds exact)
+  uint32_t compact;         // 1: entry values are new ids (strictly increasing in rank), else ranks
   uint32_t dbg;             // debug mode (CTOK_DBG_MODE), 0 in production
 };
 
@@ -68,7 +69,13 @@ struct Work {              // device pointers, sized by the host for one call
   uint32_t* scratch;       // n_bytes: tokens of piece p at scratch[pstart[p]..]
   uint32_t* doc_piece;     // n_docs + 1
   uint32_t* long_list;     // n_bytes / kShortMax + 1
-  uint32_t* counters;      // [0] long count, [1] long work cursor, [2] err, [3] nfc docs
+  uint32_t* mid_list;      // pieces for the generic thread-per-piece kernel
+  uint32_t* region;        // per first-pass block: 9..16-byte pieces from the front, 17..32 from the back
+  uint32_t region_len;     // entries per block (>= pieces per block)
+  uint32_t grid1;          // blocks of the first BPE pass
+  uint32_t* cnt16;         // [grid1] 9..16-byte pieces per block
+  uint32_t* cntmid;        // [grid1] 17..32-byte pieces per block
+  uint32_t* counters;      // [0] long count, [2] err, [3] nfc docs, [4] mid count, [5] list16 count
   uint32_t* lw;            // long-piece workspace: 4 * n_bytes u32
   uint32_t* scan_tmp;      // scan partials
   uint64_t scan_tmp_cap;

@@ -101,7 +101,17 @@ __device__ __forceinline__ uint32_t mhash(uint32_t a, uint32_t b) {
   return h ^ (h >> 15);
 }
 
-// rank of pair (a, b) or kNoRank.  Sets the panic bit when the reference would index
+// Merge-table value of an entry: the merge priority.  Compact tables (new ids strictly increasing
+// in rank, the usual layout) store the merged token id itself, so the minimum value is both the
+// winning pair and its new id; otherwise the rank is stored and the new id is looked up.
+__device__ __forceinline__ bool value_panics(const Tables& t, uint32_t v) {
+  return t.compact ? v == kPanicVal : v >= t.n_ranks;
+}
+__device__ __forceinline__ uint32_t new_id_of(const Tables& t, uint32_t v) {
+  return t.compact ? v : t.rank_newid[v];
+}
+
+// value of pair (a, b) or kNoRank.  Sets the panic bit when the reference would index
 // BpeTokenizer.merges out of range (src/bpe.rs:141).
 __device__ __forceinline__ uint32_t rank_of(const Tables& t, uint32_t a, uint32_t b, uint32_t* err) {
   const uint64_t key = ((uint64_t)a << kIdBits) | b;
@@ -110,7 +120,7 @@ __device__ __forceinline__ uint32_t rank_of(const Tables& t, uint32_t a, uint32_
     const uint64_t e = t.merge_tab[h];
     if ((e & kKeyMask) == key) {
       const uint32_t r = (uint32_t)(e >> 42);
-      if (r >= t.n_ranks) { atomicOr(err, kErrPanic); return kNoRank; }
+      if (value_panics(t, r)) { atomicOr(err, kErrPanic); return kNoRank; }
       return r;
     }
     if (e == kEmpty) return kNoRank;
@@ -386,7 +396,7 @@ __device__ __forceinline__ uint32_t bpe_short(const Tables& t, const uint8_t* by
         if (r < best) { best = r; bi = i; }
       }
       if (best == kNoRank) break;
-      TOK(bi) = t.rank_newid[best];
+      TOK(bi) = new_id_of(t, best);
       for (uint32_t i = bi + 1; i + 1 < m; i++) TOK(i) = TOK(i + 1);
       for (uint32_t i = bi + 1; i + 2 < m; i++) RK(i) = RK(i + 1);
       m--;
@@ -398,16 +408,32 @@ __device__ __forceinline__ uint32_t bpe_short(const Tables& t, const uint8_t* by
   return m;
 }
 
-__global__ __launch_bounds__(256) void k_bpe(Work w, Tables t) {
+// Generic thread-per-piece kernel (LDS working arrays, handles dropped bytes and added
+// tokens).  list == nullptr: every piece (used when the tokenizer has matchable added tokens),
+// routing pieces longer than kShortMax to the long list; else: the pieces named in list.
+__global__ __launch_bounds__(256) void k_bpe_generic(Work w, Tables t, const uint32_t* list, const uint32_t* list_n,
+                                                     int from_region) {
   __shared__ uint32_t s_tok[kShortMax * 256];
   __shared__ uint32_t s_rk[kShortMax * 256];
   __shared__ int32_t s_b2id[256];
   const uint32_t tid = threadIdx.x;
   s_b2id[tid] = t.byte2id[tid];
   __syncthreads();
-  const uint32_t P = w.tile_cnt[w.n_tiles];
   uint32_t* err = &w.counters[2];
-  for (uint32_t p = blockIdx.x * 256 + tid; p < P; p += gridDim.x * 256) {
+  if (from_region) {  // block b: the medium pieces the first pass stored at the back of region b
+    const uint32_t* region = w.region + (size_t)blockIdx.x * w.region_len;
+    const uint32_t nb = w.cntmid[blockIdx.x];
+    for (uint32_t q = tid; q < nb; q += 256) {
+      const uint32_t p = region[w.region_len - 1 - q];
+      const uint32_t s = w.pstart[p];
+      const uint32_t n = w.pstart[p + 1] - s;
+      w.pcnt[p] = bpe_short(t, w.text + s, n, s_b2id, s_tok, s_rk, tid, w.scratch + s, err);
+    }
+    return;
+  }
+  const uint32_t P = list ? *list_n : w.tile_cnt[w.n_tiles];
+  for (uint32_t q = blockIdx.x * 256 + tid; q < P; q += gridDim.x * 256) {
+    const uint32_t p = list ? list[q] : q;
     const uint32_t s = w.pstart[p];
     const uint32_t n = w.pstart[p + 1] - s;
     if (n > kShortMax) {
@@ -444,13 +470,180 @@ __global__ __launch_bounds__(256) void k_bpe(Work w, Tables t) {
   }
 }
 
-#undef TOK
-#undef RK
+// ------------------------------------------------------------------------------------------
+// BPE fast path: pieces of <= kRegMax bytes merged by one thread with the tokens and pair ranks
+// in registers (fully unrolled, compile-time slot indices; no LDS, so occupancy is set by
+// VGPRs alone).  All first-probe loads of the initial pairs issue back to back.  Longer pieces
+// go to the medium (LDS) or long (wavefront) lists.
+
+__device__ __forceinline__ uint32_t resolve_rank(const Tables& t, uint64_t key, uint32_t h, uint64_t e, uint32_t* err) {
+  for (;;) {
+    if ((e & kKeyMask) == key) {
+      const uint32_t r = (uint32_t)(e >> 42);
+      if (value_panics(t, r)) { atomicOr(err, kErrPanic); return kNoRank; }
+      return r;
+    }
+    if (e == kEmpty) return kNoRank;
+    h = (h + 1) & t.merge_mask;
+    e = t.merge_tab[h];
+  }
+}
+
+__device__ __forceinline__ uint64_t pair_key(uint32_t a, uint32_t b) { return ((uint64_t)a << kIdBits) | b; }
+
+// Pieces of at most N bytes.  FIRST: the pass over every piece, which routes longer pieces to
+// the 16-byte list / medium (LDS) list / long (wavefront) list; else: the pieces of list16.
+// block b of the first pass holding dense index g of a class whose per-block counts were
+// exclusive-scanned into off[0..grid1] (off[grid1] = total)
+__device__ __forceinline__ uint32_t owner_block(const uint32_t* off, uint32_t n, uint32_t g) {
+  uint32_t lo = 0, hi = n;  // off[lo] <= g < off[hi]
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (off[mid] <= g) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
+// FIRST (N = 8): this block's contiguous range of pieces; pieces of 9..16 bytes are stored at the
+// front of the block's region, 17..32 at the back, longer ones in the long list.  Else: the
+// 9..16-byte (N = 16) or 17..32-byte (N = 32) pieces, as one dense index space over the regions.
+template <int N, bool FIRST, bool COMPACT>
+__global__ __launch_bounds__(256) void k_bpe_reg(Work w, Tables t) {
+  __shared__ int32_t s_b2id[256];
+  __shared__ uint32_t s_cnt[2];
+  const uint32_t tid = threadIdx.x;
+  s_b2id[tid] = t.byte2id[tid];
+  if (tid < 2) s_cnt[tid] = 0;
+  __syncthreads();
+  uint32_t* err = &w.counters[2];
+  const uint32_t* coff = N == 16 ? w.cnt16 : w.cntmid;  // scanned counts (second pass)
+  const uint32_t P = FIRST ? w.tile_cnt[w.n_tiles] : coff[w.grid1];
+  const uint32_t per = (P + gridDim.x - 1) / gridDim.x;
+  const uint32_t q0 = FIRST ? blockIdx.x * per : blockIdx.x * 256;
+  const uint32_t q1 = FIRST ? min(P, q0 + per) : P;
+  const uint32_t step = FIRST ? 256 : gridDim.x * 256;
+  uint32_t* region = w.region + (size_t)blockIdx.x * w.region_len;
+  for (uint32_t q = q0 + tid; q < q1; q += step) {
+    uint32_t p;
+    if (FIRST) {
+      p = q;
+    } else {
+      const uint32_t b = owner_block(coff, w.grid1, q);
+      const uint32_t* rg = w.region + (size_t)b * w.region_len;
+      p = N == 16 ? rg[q - coff[b]] : rg[w.region_len - 1 - (q - coff[b])];
+    }
+    const uint32_t s = w.pstart[p];
+    const uint32_t n = w.pstart[p + 1] - s;
+    if (FIRST && n > N) {
+      if (n > kShortMax) w.long_list[atomicAdd(&w.counters[0], 1u)] = p;  // rare: one global counter
+      else if (n > 16) region[w.region_len - 1 - atomicAdd(&s_cnt[1], 1u)] = p;
+      else region[atomicAdd(&s_cnt[0], 1u)] = p;
+      continue;
+    }
+    const uint8_t* bytes = w.text + s;
+    uint32_t tk[N], rk[N];
+    bool missing = false;
+#pragma unroll
+    for (int k = 0; k < N; k++) {
+      int32_t id = -1;
+      if ((uint32_t)k < n) {
+        id = s_b2id[bytes[k]];
+        missing |= id < 0;
+      }
+      tk[k] = (uint32_t)id;
+    }
+    if (missing) {  // a byte char absent from the vocab is dropped: generic path
+      w.mid_list[atomicAdd(&w.counters[4], 1u)] = p;
+      continue;
+    }
+#pragma unroll
+    for (int k0 = 0; k0 < N - 1; k0 += 8) {  // first probes of 8 pairs in flight together
+      uint32_t hh[8];
+      uint64_t ee[8];
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        const int k = k0 + j;
+        if (k < N - 1 && (uint32_t)k + 1 < n) {
+          hh[j] = mhash(tk[k], tk[k + 1]) & t.merge_mask;
+          ee[j] = t.merge_tab[hh[j]];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        const int k = k0 + j;
+        if (k < N - 1) rk[k] = ((uint32_t)k + 1 < n) ? resolve_rank(t, pair_key(tk[k], tk[k + 1]), hh[j], ee[j], err) : kNoRank;
+      }
+    }
+    rk[N - 1] = kNoRank;
+    uint32_t m = n;
+    for (;;) {
+      uint32_t best = kNoRank, bi = 0;
+#pragma unroll
+      for (int k = 0; k < N - 1; k++)
+        if (rk[k] < best) { best = rk[k]; bi = (uint32_t)k; }
+      if (best == kNoRank) break;
+      const uint32_t nid = COMPACT ? best : t.rank_newid[best];
+      uint32_t L = 0, R = 0;
+#pragma unroll
+      for (int k = 0; k < N; k++) {
+        if ((uint32_t)k + 1 == bi) L = tk[k];
+        if ((uint32_t)k == bi + 2) R = tk[k];
+      }
+      const bool has_l = bi > 0, has_r = bi + 2 < m;
+      const uint32_t hl = mhash(L, nid) & t.merge_mask, hr = mhash(nid, R) & t.merge_mask;
+      const uint64_t el = has_l ? t.merge_tab[hl] : kEmpty;  // both new pairs probe in parallel
+      const uint64_t er = has_r ? t.merge_tab[hr] : kEmpty;
+#pragma unroll
+      for (int k = 0; k < N; k++) {  // ascending: tk[k+1] is read before it is overwritten
+        const uint32_t nxt_t = k + 1 < N ? tk[k + 1] : kDead;
+        const uint32_t nxt_r = k + 1 < N ? rk[k + 1] : kNoRank;
+        if ((uint32_t)k == bi) tk[k] = nid;
+        else if ((uint32_t)k > bi) { tk[k] = nxt_t; rk[k] = nxt_r; }
+      }
+      m--;
+      const uint32_t rl = has_l ? resolve_rank(t, pair_key(L, nid), hl, el, err) : kNoRank;
+      const uint32_t rr = has_r ? resolve_rank(t, pair_key(nid, R), hr, er, err) : kNoRank;
+#pragma unroll
+      for (int k = 0; k < N; k++) {
+        if ((uint32_t)k + 1 == bi) rk[k] = rl;
+        if ((uint32_t)k == bi) rk[k] = rr;
+      }
+    }
+    uint32_t* out = w.scratch + s;
+#pragma unroll
+    for (int k = 0; k < N; k++)
+      if ((uint32_t)k < m) out[k] = tk[k];
+    w.pcnt[p] = m;
+  }
+  if (FIRST) {
+    __syncthreads();
+    if (tid == 0) {
+      w.cnt16[blockIdx.x] = s_cnt[0];
+      w.cntmid[blockIdx.x] = s_cnt[1];
+    }
+  }
+}
+
+template <bool C>
+static hipError_t launch_bpe_reg(const Work& w, const Tables& t, hipStream_t s) {
+  k_bpe_reg<8, true, C><<<w.grid1, 256, 0, s>>>(w, t);
+  HIPCHK(hipGetLastError());
+  // per-block class counts -> dense offsets (cnt16 and cntmid are adjacent: one scan each)
+  HIPCHK(scan_u32(w.cnt16, w.cnt16, w.grid1, nullptr, w.scan_tmp, w.scan_tmp_cap, s));
+  HIPCHK(scan_u32(w.cntmid, w.cntmid, w.grid1, nullptr, w.scan_tmp, w.scan_tmp_cap, s));
+  const uint32_t g2 = w.grid1 / 8 + 1;
+  k_bpe_reg<16, false, C><<<g2, 256, 0, s>>>(w, t);
+  k_bpe_reg<32, false, C><<<g2, 256, 0, s>>>(w, t);
+  return hipGetLastError();
+}
 
 hipError_t launch_bpe(const Work& w, const Tables& t, hipStream_t s) {
-  uint32_t grid = (w.n_bytes / 4 + 255) / 256;  // pieces <= bytes; typical ~bytes/4.5
-  grid = grid < 1 ? 1 : grid > 8192 ? 8192 : grid;
-  k_bpe<<<grid, 256, 0, s>>>(w, t);
+  if (t.n_at == 0) {
+    HIPCHK(t.compact ? launch_bpe_reg<true>(w, t, s) : launch_bpe_reg<false>(w, t, s));
+    k_bpe_generic<<<64, 256, 0, s>>>(w, t, w.mid_list, &w.counters[4], 0);  // pieces with dropped bytes
+  } else {
+    k_bpe_generic<<<w.grid1, 256, 0, s>>>(w, t, nullptr, nullptr, 0);
+  }
   return hipGetLastError();
 }
 
@@ -563,7 +756,7 @@ __device__ uint32_t bpe_wave(const Tables& t, const uint8_t* bytes, uint32_t n, 
     for (uint32_t i = lane; i < m; i += 64) lmin = min(lmin, L.Rk(i));
     const uint32_t r = uni(wave_min_u32(lmin));
     if (r == kNoRank) break;
-    const uint32_t nid = uni(t.rank_newid[r]);
+    const uint32_t nid = uni(new_id_of(t, r));
     uint32_t lpos = kNone;
     for (uint32_t i = lane; i < m; i += 64) {
       if (L.Rk(i) == r) { lpos = i; break; }

@@ -167,3 +167,16 @@ def test_panic_toy():
         tok.encode("ab")
     with pytest.raises(ref_py.PanicException):
         ref_py.RefTokenizer(obj).encode("ab")
+
+
+def test_wide_table_mode(gpt2, monkeypatch):
+    """The rank-valued (wide) merge table must give the same ids as the compact one."""
+    obj, _, rc = gpt2
+    monkeypatch.setenv("CTOK_FORCE_WIDE", "1")
+    tok = gpu_tok(obj)
+    monkeypatch.delenv("CTOK_FORCE_WIDE")
+    text, off = corpus.corpus_c2(30_000, seed=21)
+    assert_same(*tok.encode_packed(text, off), *rc.encode_packed(text, off))
+    docs = edge_cases.long_docs() + edge_cases.EDGE
+    text, off = corpus.pack([d.encode() for d in docs])
+    assert_same(*tok.encode_packed(text, off), *rc.encode_packed(text, off))
