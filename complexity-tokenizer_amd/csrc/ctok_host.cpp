@@ -159,8 +159,11 @@ struct DeviceState {
   std::mutex mu;
   hipStream_t stream = nullptr;
   hipEvent_t ev[8] = {};
+  hipEvent_t ev_sync = nullptr;   // spin-waited completion marker (no blocking-wait wakeup latency)
+  uint64_t* host = nullptr;       // pinned host words for small device->host readbacks
   // tables
   DevBuf<uint64_t> merge_tab;
+  DevBuf<uint32_t> piece_tab;
   DevBuf<uint32_t> rank_newid;
   DevBuf<int32_t> byte2id;
   DevBuf<uint8_t> cls_s1, cls_s2, nfc_s1, alnum, at_bytes, at_flags;
@@ -169,7 +172,7 @@ struct DeviceState {
   DevBuf<uint64_t> comp_key;
   Tables t{};
   // workspace
-  DevBuf<uint32_t> docbits, pbits, tile_cnt, word_prefix, pstart, pcnt, scratch, doc_piece, long_list, mid_list, region, cnt16, counters, lw;
+  DevBuf<uint32_t> docbits, pbits, tile_cnt, word_prefix, pstart, pcnt, scratch, doc_piece, long_list, mid_list, region, region2, ccnt, counters, lw;
   DevBuf<uint64_t> scan_tmp;
   DevBuf<uint32_t> doc_flag, ncp;
   DevBuf<uint64_t> norm_off;
@@ -182,6 +185,8 @@ struct DeviceState {
     if (device >= 0) {
       (void)hipSetDevice(device);
       for (auto& e : ev) if (e) (void)hipEventDestroy(e);
+      if (ev_sync) (void)hipEventDestroy(ev_sync);
+      if (host) (void)hipHostFree(host);
       if (stream) (void)hipStreamDestroy(stream);
     }
   }
@@ -201,6 +206,8 @@ struct ctok {
   // compiled tables
   std::vector<uint64_t> merge_tab;
   uint32_t merge_mask = 0;
+  std::vector<uint32_t> piece_tab;  // 4 u32 per slot (see ctok_internal.h piece_hash)
+  uint32_t piece_mask = 0;
   std::vector<uint32_t> rank_newid;
   int32_t byte2id[256];
   std::string at_bytes;
@@ -400,6 +407,62 @@ void load(ctok* t, const char* buf, size_t len) {
     t->byte2id[b] = it == t->vocab.end() ? -1 : (int32_t)it->second;
   }
 
+  // whole-piece table: every vocab entry of <= 8 raw bytes whose own BPE is that single token
+  {
+    std::unordered_map<uint32_t, int> inv0;  // mapped code point -> byte
+    for (int b = 0; b < 256; b++) inv0[bm[b]] = b;
+    std::vector<std::pair<std::string, uint32_t>> ents;
+    std::vector<uint32_t> cps, tk;
+    for (const auto& kv : t->vocab) {
+      if (!decode_utf8(kv.first, cps) || cps.empty() || cps.size() > 8) continue;
+      std::string raw;
+      bool ok = true;
+      for (uint32_t c : cps) {
+        auto it = inv0.find(c);
+        if (it == inv0.end()) { ok = false; break; }
+        raw += (char)it->second;
+      }
+      if (!ok) continue;
+      // the reference merge loop (src/bpe.rs:88-153) on these bytes
+      tk.clear();
+      for (unsigned char c : raw) {
+        if (t->byte2id[c] < 0) { ok = false; break; }
+        tk.push_back((uint32_t)t->byte2id[c]);
+      }
+      if (!ok) continue;
+      for (;;) {
+        size_t bi = 0;
+        uint32_t best = UINT32_MAX;
+        for (size_t i = 0; i + 1 < tk.size(); i++) {
+          auto r = ranks.find(((uint64_t)tk[i] << 32) | tk[i + 1]);
+          if (r == ranks.end()) continue;
+          if (r->second >= valid_new.size()) { ok = false; break; }  // would panic: leave to the kernels
+          if (r->second < best) { best = r->second; bi = i; }
+        }
+        if (!ok || best == UINT32_MAX) break;
+        tk[bi] = valid_new[best];
+        tk.erase(tk.begin() + bi + 1);
+      }
+      if (ok && tk.size() == 1 && tk[0] == kv.second) ents.push_back({raw, kv.second});
+    }
+    size_t pcap = 1024;
+    while (pcap < ents.size() * 2 + 16) pcap <<= 1;
+    t->piece_tab.assign(pcap * 4, 0);
+    t->piece_mask = (uint32_t)(pcap - 1);
+    for (const auto& e : ents) {
+      uint64_t v = 0;
+      for (size_t i = 0; i < e.first.size(); i++) v |= (uint64_t)(uint8_t)e.first[i] << (8 * i);
+      const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32), len = (uint32_t)e.first.size();
+      uint32_t h = piece_hash(lo, hi, len) & t->piece_mask;
+      while (t->piece_tab[4 * h + 2] != 0) h = (h + 1) & t->piece_mask;
+      t->piece_tab[4 * h] = lo;
+      t->piece_tab[4 * h + 1] = hi;
+      t->piece_tab[4 * h + 2] = len;
+      t->piece_tab[4 * h + 3] = e.second;
+    }
+    if (getenv("CTOK_NO_PIECE_TABLE")) std::fill(t->piece_tab.begin(), t->piece_tab.end(), 0u);
+  }
+
   // added tokens (mod.rs:103-116 schema, :274-305 maps)
   std::vector<std::pair<std::string, std::pair<uint32_t, uint8_t>>> added;  // content -> (id, flags)
   if (const ctj::Value* at = root.get("added_tokens")) {
@@ -479,9 +542,12 @@ DeviceState* device_state(ctok* t, int device) {
   ds->device = device;
   HIPTRY(hipStreamCreateWithFlags(&ds->stream, hipStreamNonBlocking));
   for (auto& e : ds->ev) HIPTRY(hipEventCreate(&e));
+  HIPTRY(hipEventCreateWithFlags(&ds->ev_sync, hipEventDisableTiming));
+  HIPTRY(hipHostMalloc((void**)&ds->host, 4096, hipHostMallocDefault));
   hipStream_t s = ds->stream;
   upload(ds->merge_tab, t->merge_tab.data(), t->merge_tab.size(), s);
   upload(ds->rank_newid, t->rank_newid.data(), t->rank_newid.size(), s);
+  upload(ds->piece_tab, t->piece_tab.data(), t->piece_tab.size(), s);
   upload(ds->byte2id, t->byte2id, 256, s);
   upload(ds->cls_s1, ct_cls_stage1, sizeof(ct_cls_stage1), s);
   upload(ds->cls_s2, ct_cls_stage2, sizeof(ct_cls_stage2), s);
@@ -501,6 +567,8 @@ DeviceState* device_state(ctok* t, int device) {
   Tables& tb = ds->t;
   tb.merge_tab = ds->merge_tab.p;
   tb.merge_mask = t->merge_mask;
+  tb.piece_tab = (const uint4*)ds->piece_tab.p;
+  tb.piece_mask = t->piece_mask;
   tb.rank_newid = ds->rank_newid.p;
   tb.n_ranks = (uint32_t)t->rank_newid.size();
   tb.byte2id = ds->byte2id.p;
@@ -545,6 +613,17 @@ bool debug_sync() {
     }                                                                                    \
   } while (0)
 
+// Wait for all work on s by spinning on an event: a blocking stream synchronise can add
+// hundreds of microseconds of wake-up latency per call on this path's few sync points.
+void spin_sync(DeviceState* ds, hipStream_t s) {
+  HIPTRY(hipEventRecord(ds->ev_sync, s));
+  for (;;) {
+    hipError_t e = hipEventQuery(ds->ev_sync);
+    if (e == hipSuccess) return;
+    if (e != hipErrorNotReady) throw_err(CTOK_E_DEVICE, std::string("hipEventQuery: ") + hipGetErrorString(e));
+  }
+}
+
 double now_ms() {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -569,9 +648,9 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
     ds->doc_flag.ensure(n_docs + 1);
     HIPTRY(hipMemsetAsync(ds->doc_flag.p, 0, (n_docs + 1) * 4, s));
     STEP("nfc_check", launch_nfc_check(d_text, n_bytes, d_off, (uint32_t)n_docs, tb, ds->doc_flag.p, ds->counters.p + 3, s));
-    uint32_t cnt = 0;
-    HIPTRY(hipMemcpyAsync(&cnt, ds->counters.p + 3, 4, hipMemcpyDeviceToHost, s));
-    HIPTRY(hipStreamSynchronize(s));
+    HIPTRY(hipMemcpyAsync(ds->host, ds->counters.p + 3, 4, hipMemcpyDeviceToHost, s));
+    spin_sync(ds, s);
+    const uint32_t cnt = *(volatile uint32_t*)ds->host;
     nfc_docs = cnt;
     if (cnt) norm = true;
   }
@@ -585,9 +664,9 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
                        ds->lw.p, ds->ncp.p, ds->norm_off.p, nullptr, 0, s));
     ds->scan_tmp.ensure(scan_tmp_elems(n_docs + 1) + 64);
     HIPTRY(scan_u64(ds->norm_off.p, n_docs, ds->scan_tmp.p, ds->scan_tmp.cap, s));
-    uint64_t nb = 0;
-    HIPTRY(hipMemcpyAsync(&nb, ds->norm_off.p + n_docs, 8, hipMemcpyDeviceToHost, s));
-    HIPTRY(hipStreamSynchronize(s));
+    HIPTRY(hipMemcpyAsync(ds->host, ds->norm_off.p + n_docs, 8, hipMemcpyDeviceToHost, s));
+    spin_sync(ds, s);
+    const uint64_t nb = *(volatile uint64_t*)ds->host;
     if (nb >= 0xF0000000ull) throw_err(CTOK_E_ARG, "normalised batch exceeds 3.75 GiB; split the batch");
     ds->norm_text.ensure(nb + 16);
     STEP("norm1", launch_norm(d_text, d_off, (uint32_t)n_docs, ds->doc_flag.p, t->add_prefix_space, t->nfc && nfc_docs, tb,
@@ -618,7 +697,8 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   uint32_t grid1 = (uint32_t)std::min<uint64_t>(16384, std::max<uint64_t>(1, (B / 4 + 2047) / 2048));
   uint32_t region_len = (uint32_t)((B + 1 + grid1 - 1) / grid1);  // pieces <= B: per-block share
   ds->region.ensure((size_t)grid1 * region_len + 16);
-  ds->cnt16.ensure(2 * (size_t)grid1 + 18);  // [cnt16 | cntmid], each grid1 + 1
+  ds->region2.ensure((size_t)grid1 * region_len + 16);
+  ds->ccnt.ensure(3 * ((size_t)grid1 + 1) + 16);
   ds->lw.ensure(4 * B + 64);
   ds->scan_tmp.ensure(scan_tmp_elems(std::max<uint64_t>(B + 1, n_docs + 1)) + 64);
   w.docbits = ds->docbits.p;
@@ -634,8 +714,8 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   w.region = ds->region.p;
   w.region_len = region_len;
   w.grid1 = grid1;
-  w.cnt16 = ds->cnt16.p;
-  w.cntmid = ds->cnt16.p + grid1 + 1;
+  w.region2 = ds->region2.p;
+  w.ccnt = ds->ccnt.p;
   w.counters = ds->counters.p;
   w.lw = ds->lw.p;
   w.scan_tmp = (uint32_t*)ds->scan_tmp.p;
@@ -651,13 +731,14 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   if (timing) HIPTRY(hipEventRecord(ds->ev[3], s));
   STEP("emit", launch_emit(w, d_ids, ids_cap, d_tok_off, s));
   if (timing) HIPTRY(hipEventRecord(ds->ev[4], s));
-  uint64_t ntok = 0;
-  uint32_t cnt[4] = {0, 0, 0, 0};
-  HIPTRY(hipMemcpyAsync(&ntok, d_tok_off + n_docs, 8, hipMemcpyDeviceToHost, s));
-  HIPTRY(hipMemcpyAsync(cnt, ds->counters.p, 16, hipMemcpyDeviceToHost, s));
-  uint32_t P = 0;
-  HIPTRY(hipMemcpyAsync(&P, ds->tile_cnt.p + w.n_tiles, 4, hipMemcpyDeviceToHost, s));
-  HIPTRY(hipStreamSynchronize(s));
+  HIPTRY(hipMemcpyAsync(ds->host, d_tok_off + n_docs, 8, hipMemcpyDeviceToHost, s));
+  HIPTRY(hipMemcpyAsync(ds->host + 1, ds->counters.p, 16, hipMemcpyDeviceToHost, s));
+  HIPTRY(hipMemcpyAsync(ds->host + 3, ds->tile_cnt.p + w.n_tiles, 4, hipMemcpyDeviceToHost, s));
+  spin_sync(ds, s);
+  const uint64_t ntok = ((volatile uint64_t*)ds->host)[0];
+  uint32_t cnt[4];
+  for (int i = 0; i < 4; i++) cnt[i] = ((volatile uint32_t*)(ds->host + 1))[i];
+  const uint32_t P = ((volatile uint32_t*)(ds->host + 3))[0];
   if (cnt[2] & kErrPanic)
     throw_err(CTOK_E_PANIC, "index out of bounds: a merge rank points past the list of valid merges (reference src/bpe.rs:141 panics)");
   if (ntok > ids_cap) throw_err(CTOK_E_CAPACITY, "ids_cap too small: tok_off[n_docs] holds the number of ids needed");

@@ -24,9 +24,19 @@ constexpr int kSegThreads = 256;   // 16 bytes per thread
 constexpr int kHalo = 16;
 constexpr int kShortMax = 32;      // pieces up to this many bytes are merged thread-per-piece
 
+// Whole-piece table: raw byte strings of <= 8 bytes whose BPE is exactly one token (checked at
+// load time by running the merge loop on every vocab entry).  Entry = {lo32, hi32, len, id} of
+// the zero-padded bytes; len == 0 marks an empty slot.
+__host__ __device__ inline uint32_t piece_hash(uint32_t lo, uint32_t hi, uint32_t len) {
+  uint32_t h = lo * 0x9E3779B1u ^ (hi + 0x632BE5ABu) * 0x85EBCA77u ^ len * 0xC2B2AE3Du;
+  return h ^ (h >> 16);
+}
+
 struct Tables {            // device pointers, owned by the host runtime
   const uint64_t* merge_tab;
   uint32_t merge_mask;     // capacity - 1 (power of two)
+  const uint4* piece_tab;  // whole-piece table (see piece_hash)
+  uint32_t piece_mask;
   const uint32_t* rank_newid;
   uint32_t n_ranks;
   const int32_t* byte2id;  // [256], -1 = byte char missing from vocab (dropped)
@@ -70,11 +80,11 @@ struct Work {              // device pointers, sized by the host for one call
   uint32_t* doc_piece;     // n_docs + 1
   uint32_t* long_list;     // n_bytes / kShortMax + 1
   uint32_t* mid_list;      // pieces for the generic thread-per-piece kernel
-  uint32_t* region;        // per first-pass block: 9..16-byte pieces from the front, 17..32 from the back
+  uint32_t* region;        // per routing block: class-0 pieces from the front, class 1 from the back
+  uint32_t* region2;       // per routing block: class-2 pieces
   uint32_t region_len;     // entries per block (>= pieces per block)
-  uint32_t grid1;          // blocks of the first BPE pass
-  uint32_t* cnt16;         // [grid1] 9..16-byte pieces per block
-  uint32_t* cntmid;        // [grid1] 17..32-byte pieces per block
+  uint32_t grid1;          // blocks of the routing pass
+  uint32_t* ccnt;          // [3][grid1 + 1] pieces per block and class, scanned to offsets
   uint32_t* counters;      // [0] long count, [2] err, [3] nfc docs, [4] mid count, [5] list16 count
   uint32_t* lw;            // long-piece workspace: 4 * n_bytes u32
   uint32_t* scan_tmp;      // scan partials

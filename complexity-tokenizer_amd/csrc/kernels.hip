@@ -411,8 +411,7 @@ __device__ __forceinline__ uint32_t bpe_short(const Tables& t, const uint8_t* by
 // Generic thread-per-piece kernel (LDS working arrays, handles dropped bytes and added
 // tokens).  list == nullptr: every piece (used when the tokenizer has matchable added tokens),
 // routing pieces longer than kShortMax to the long list; else: the pieces named in list.
-__global__ __launch_bounds__(256) void k_bpe_generic(Work w, Tables t, const uint32_t* list, const uint32_t* list_n,
-                                                     int from_region) {
+__global__ __launch_bounds__(256) void k_bpe_generic(Work w, Tables t, const uint32_t* list, const uint32_t* list_n) {
   __shared__ uint32_t s_tok[kShortMax * 256];
   __shared__ uint32_t s_rk[kShortMax * 256];
   __shared__ int32_t s_b2id[256];
@@ -420,17 +419,6 @@ __global__ __launch_bounds__(256) void k_bpe_generic(Work w, Tables t, const uin
   s_b2id[tid] = t.byte2id[tid];
   __syncthreads();
   uint32_t* err = &w.counters[2];
-  if (from_region) {  // block b: the medium pieces the first pass stored at the back of region b
-    const uint32_t* region = w.region + (size_t)blockIdx.x * w.region_len;
-    const uint32_t nb = w.cntmid[blockIdx.x];
-    for (uint32_t q = tid; q < nb; q += 256) {
-      const uint32_t p = region[w.region_len - 1 - q];
-      const uint32_t s = w.pstart[p];
-      const uint32_t n = w.pstart[p + 1] - s;
-      w.pcnt[p] = bpe_short(t, w.text + s, n, s_b2id, s_tok, s_rk, tid, w.scratch + s, err);
-    }
-    return;
-  }
   const uint32_t P = list ? *list_n : w.tile_cnt[w.n_tiles];
   for (uint32_t q = blockIdx.x * 256 + tid; q < P; q += gridDim.x * 256) {
     const uint32_t p = list ? list[q] : q;
@@ -504,42 +492,79 @@ __device__ __forceinline__ uint32_t owner_block(const uint32_t* off, uint32_t n,
   return lo;
 }
 
-// FIRST (N = 8): this block's contiguous range of pieces; pieces of 9..16 bytes are stored at the
-// front of the block's region, 17..32 at the back, longer ones in the long list.  Else: the
-// 9..16-byte (N = 16) or 17..32-byte (N = 32) pieces, as one dense index space over the regions.
-template <int N, bool FIRST, bool COMPACT>
-__global__ __launch_bounds__(256) void k_bpe_reg(Work w, Tables t) {
-  __shared__ int32_t s_b2id[256];
-  __shared__ uint32_t s_cnt[2];
+// Routing pass: block b takes a contiguous range of pieces.  A piece of <= 8 bytes that is one
+// self-encoding vocab token is finished here with a single whole-piece probe; every other piece
+// is filed by length so that the merge passes run dense, length-uniform waves:
+//   class 0 (<= 8 B, probe missed) front of regionA[b], class 1 (9..16 B) back of regionA[b],
+//   class 2 (17..32 B) front of regionB[b], longer pieces in the long list (one global counter).
+__global__ __launch_bounds__(256) void k_route(Work w, Tables t) {
+  __shared__ uint32_t s_cnt[3];
   const uint32_t tid = threadIdx.x;
-  s_b2id[tid] = t.byte2id[tid];
-  if (tid < 2) s_cnt[tid] = 0;
+  if (tid < 3) s_cnt[tid] = 0;
   __syncthreads();
-  uint32_t* err = &w.counters[2];
-  const uint32_t* coff = N == 16 ? w.cnt16 : w.cntmid;  // scanned counts (second pass)
-  const uint32_t P = FIRST ? w.tile_cnt[w.n_tiles] : coff[w.grid1];
+  const uint32_t P = w.tile_cnt[w.n_tiles];
   const uint32_t per = (P + gridDim.x - 1) / gridDim.x;
-  const uint32_t q0 = FIRST ? blockIdx.x * per : blockIdx.x * 256;
-  const uint32_t q1 = FIRST ? min(P, q0 + per) : P;
-  const uint32_t step = FIRST ? 256 : gridDim.x * 256;
-  uint32_t* region = w.region + (size_t)blockIdx.x * w.region_len;
-  for (uint32_t q = q0 + tid; q < q1; q += step) {
-    uint32_t p;
-    if (FIRST) {
-      p = q;
-    } else {
-      const uint32_t b = owner_block(coff, w.grid1, q);
-      const uint32_t* rg = w.region + (size_t)b * w.region_len;
-      p = N == 16 ? rg[q - coff[b]] : rg[w.region_len - 1 - (q - coff[b])];
-    }
+  const uint32_t q0 = blockIdx.x * per, q1 = min(P, q0 + per);
+  uint32_t* ra = w.region + (size_t)blockIdx.x * w.region_len;
+  uint32_t* rb = w.region2 + (size_t)blockIdx.x * w.region_len;
+  for (uint32_t p = q0 + tid; p < q1; p += 256) {
     const uint32_t s = w.pstart[p];
     const uint32_t n = w.pstart[p + 1] - s;
-    if (FIRST && n > N) {
-      if (n > kShortMax) w.long_list[atomicAdd(&w.counters[0], 1u)] = p;  // rare: one global counter
-      else if (n > 16) region[w.region_len - 1 - atomicAdd(&s_cnt[1], 1u)] = p;
-      else region[atomicAdd(&s_cnt[0], 1u)] = p;
+    if (n > 8) {
+      if (n > kShortMax) w.long_list[atomicAdd(&w.counters[0], 1u)] = p;
+      else if (n > 16) rb[atomicAdd(&s_cnt[2], 1u)] = p;
+      else ra[w.region_len - 1 - atomicAdd(&s_cnt[1], 1u)] = p;
       continue;
     }
+    const uint8_t* bytes = w.text + s;
+    uint32_t lo = 0, hi = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      if ((uint32_t)k < n) {
+        const uint32_t c = bytes[k];
+        if (k < 4) lo |= c << (8 * k);
+        else hi |= c << (8 * (k - 4));
+      }
+    }
+    uint32_t h = piece_hash(lo, hi, n) & t.piece_mask;
+    uint32_t hit = kNone;
+    for (;;) {
+      const uint4 e = t.piece_tab[h];
+      if (e.z == 0) break;
+      if (e.x == lo && e.y == hi && e.z == n) { hit = e.w; break; }
+      h = (h + 1) & t.piece_mask;
+    }
+    if (hit != kNone) {
+      w.scratch[s] = hit;
+      w.pcnt[p] = 1;
+    } else {
+      ra[atomicAdd(&s_cnt[0], 1u)] = p;
+    }
+  }
+  __syncthreads();
+  if (tid < 3) w.ccnt[tid * (w.grid1 + 1) + blockIdx.x] = s_cnt[tid];
+}
+
+// Merge pass over one length class (N = 8, 16, 32 slots) as a dense index space over the
+// routing pass's per-block lists (counts exclusive-scanned in w.ccnt).
+template <int N, bool COMPACT>
+__global__ __launch_bounds__(256) void k_bpe_reg(Work w, Tables t) {
+  __shared__ int32_t s_b2id[256];
+  const uint32_t tid = threadIdx.x;
+  s_b2id[tid] = t.byte2id[tid];
+  __syncthreads();
+  uint32_t* err = &w.counters[2];
+  const int cls = N == 8 ? 0 : N == 16 ? 1 : 2;
+  const uint32_t* coff = w.ccnt + cls * (w.grid1 + 1);
+  const uint32_t P = coff[w.grid1];
+  for (uint32_t q = blockIdx.x * 256 + tid; q < P; q += gridDim.x * 256) {
+    const uint32_t b = owner_block(coff, w.grid1, q);
+    const uint32_t j = q - coff[b];
+    const uint32_t p = cls == 0 ? w.region[(size_t)b * w.region_len + j]
+                     : cls == 1 ? w.region[(size_t)b * w.region_len + w.region_len - 1 - j]
+                                : w.region2[(size_t)b * w.region_len + j];
+    const uint32_t s = w.pstart[p];
+    const uint32_t n = w.pstart[p + 1] - s;
     const uint8_t* bytes = w.text + s;
     uint32_t tk[N], rk[N];
     bool missing = false;
@@ -615,34 +640,29 @@ __global__ __launch_bounds__(256) void k_bpe_reg(Work w, Tables t) {
       if ((uint32_t)k < m) out[k] = tk[k];
     w.pcnt[p] = m;
   }
-  if (FIRST) {
-    __syncthreads();
-    if (tid == 0) {
-      w.cnt16[blockIdx.x] = s_cnt[0];
-      w.cntmid[blockIdx.x] = s_cnt[1];
-    }
-  }
 }
 
 template <bool C>
 static hipError_t launch_bpe_reg(const Work& w, const Tables& t, hipStream_t s) {
-  k_bpe_reg<8, true, C><<<w.grid1, 256, 0, s>>>(w, t);
+  k_route<<<w.grid1, 256, 0, s>>>(w, t);
   HIPCHK(hipGetLastError());
-  // per-block class counts -> dense offsets (cnt16 and cntmid are adjacent: one scan each)
-  HIPCHK(scan_u32(w.cnt16, w.cnt16, w.grid1, nullptr, w.scan_tmp, w.scan_tmp_cap, s));
-  HIPCHK(scan_u32(w.cntmid, w.cntmid, w.grid1, nullptr, w.scan_tmp, w.scan_tmp_cap, s));
-  const uint32_t g2 = w.grid1 / 8 + 1;
-  k_bpe_reg<16, false, C><<<g2, 256, 0, s>>>(w, t);
-  k_bpe_reg<32, false, C><<<g2, 256, 0, s>>>(w, t);
+  for (int c = 0; c < 3; c++) {  // per-block class counts -> dense offsets
+    uint32_t* cc = w.ccnt + c * (w.grid1 + 1);
+    HIPCHK(scan_u32(cc, cc, w.grid1, nullptr, w.scan_tmp, w.scan_tmp_cap, s));
+  }
+  const uint32_t g2 = w.grid1 / 4 + 1;
+  k_bpe_reg<8, C><<<g2, 256, 0, s>>>(w, t);
+  k_bpe_reg<16, C><<<g2, 256, 0, s>>>(w, t);
+  k_bpe_reg<32, C><<<g2, 256, 0, s>>>(w, t);
   return hipGetLastError();
 }
 
 hipError_t launch_bpe(const Work& w, const Tables& t, hipStream_t s) {
   if (t.n_at == 0) {
     HIPCHK(t.compact ? launch_bpe_reg<true>(w, t, s) : launch_bpe_reg<false>(w, t, s));
-    k_bpe_generic<<<64, 256, 0, s>>>(w, t, w.mid_list, &w.counters[4], 0);  // pieces with dropped bytes
+    k_bpe_generic<<<64, 256, 0, s>>>(w, t, w.mid_list, &w.counters[4]);  // pieces with dropped bytes
   } else {
-    k_bpe_generic<<<w.grid1, 256, 0, s>>>(w, t, nullptr, nullptr, 0);
+    k_bpe_generic<<<w.grid1, 256, 0, s>>>(w, t, nullptr, nullptr);
   }
   return hipGetLastError();
 }

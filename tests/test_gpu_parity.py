@@ -180,3 +180,13 @@ def test_wide_table_mode(gpt2, monkeypatch):
     docs = edge_cases.long_docs() + edge_cases.EDGE
     text, off = corpus.pack([d.encode() for d in docs])
     assert_same(*tok.encode_packed(text, off), *rc.encode_packed(text, off))
+
+
+def test_without_piece_table(gpt2, monkeypatch):
+    """Disabling the whole-piece table (every piece through the merge loop) gives the same ids."""
+    obj, _, rc = gpt2
+    monkeypatch.setenv("CTOK_NO_PIECE_TABLE", "1")
+    tok = gpu_tok(obj)
+    monkeypatch.delenv("CTOK_NO_PIECE_TABLE")
+    text, off = corpus.corpus_c2(30_000, seed=22)
+    assert_same(*tok.encode_packed(text, off), *rc.encode_packed(text, off))
