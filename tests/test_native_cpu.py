@@ -1,0 +1,144 @@
+"""CPU tests of the product's host side: the C-ABI library loads and exports every entry point
+declared in include/ctok.h, the tokenizer.json loader reproduces the reference's accept/reject
+decisions and getters, and encode fails loudly (no CPU fallback) when no GPU is visible."""
+import ctypes
+import json
+import os
+import re
+
+import numpy as np
+import pytest
+
+import complexity_tokenizer as ct
+from complexity_tokenizer import Tokenizer, UnsupportedConfigError
+from complexity_tokenizer import _native
+from oracle import ref_py
+from tests import toys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_exports_every_declared_symbol():
+    with open(os.path.join(ROOT, "include", "ctok.h")) as f:
+        hdr = f.read()
+    names = sorted(set(re.findall(r"\b(ctok_[a-z_0-9]+)\s*\(", hdr)))
+    assert len(names) >= 14
+    lib = ctypes.CDLL(_native.LIB_PATH)
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    assert set(names) <= set(_native.SIGS), set(names) - set(_native.SIGS)
+
+
+def test_version():
+    assert ct.__version__ == "0.3.3"
+    assert _native.lib.ctok_version().startswith(b"0.3.3")
+
+
+@pytest.mark.parametrize("fixture", ["gpt2_path", "llama3_path", "multi_path"])
+def test_loader_getters_match_oracle(fixture, request):
+    path = request.getfixturevalue(fixture)
+    with open(path) as f:
+        obj = json.load(f)
+    tok = Tokenizer.from_file(path)
+    py = ref_py.RefTokenizer(obj)
+    assert tok.vocab_size == py.vocab_size
+    assert tok.special_tokens == py.special_tokens
+    for s in list(obj["model"]["vocab"])[:2000:7] + ["Ġthe", "nonexistent-token", ""]:
+        assert tok.token_to_id(s) == py.token_to_id(s), s
+    for i in list(range(0, 300)) + [len(obj["model"]["vocab"]) - 1, 10 ** 7]:
+        assert tok.id_to_token(i) == py.id_to_token(i), i
+
+
+def test_loader_kat_and_from_str():
+    assert Tokenizer.from_str(json.dumps(toys.loader_kat())).vocab_size == 8
+
+
+def test_load_errors(tmp_path):
+    with pytest.raises(IOError):
+        Tokenizer.from_file(str(tmp_path / "missing.json"))
+    bad = tmp_path / "bad.json"
+    bad.write_text("{not json")
+    with pytest.raises(IOError):
+        Tokenizer.from_file(str(bad))
+    for broken in ({}, {"model": {}}, {"model": {"vocab": {"a": -1}}}, {"model": {"vocab": {"a": 1.5}}},
+                   {"model": {"vocab": {"a": 0}, "merges": 3}},
+                   {"model": {"vocab": {"a": 0}}, "added_tokens": [{"id": 1, "content": "x"}]}):
+        with pytest.raises(IOError):
+            Tokenizer.from_str(json.dumps(broken))
+
+
+@pytest.mark.parametrize("pre,norm", [
+    ({"type": "Metaspace"}, None),
+    ({"type": "Whitespace"}, None),
+    ({"type": "Split", "pattern": {"Regex": "\\s+"}, "behavior": "Isolated"}, None),
+    (None, {"type": "Lowercase"}),
+    (None, {"type": "NFKC"}),
+])
+def test_unsupported_components_fail_loudly(pre, norm):
+    obj = toys.tok_json({"a": 0}, [], normalizer=norm, pre_tokenizer=pre)
+    with pytest.raises(UnsupportedConfigError):
+        Tokenizer.from_str(json.dumps(obj))
+    with pytest.raises(ref_py.UnsupportedConfig):
+        ref_py.RefTokenizer(obj)
+
+
+def test_supported_shapes_load():
+    vocab = {c: i for i, c in enumerate(toys.byte_chars())}
+    llama_split = {"type": "Split", "pattern": {"Regex": "\\s+(?!\\S)|\\s+"}, "behavior": "Isolated"}
+    for pre in (None, {"type": "ByteLevel", "add_prefix_space": True},
+                {"type": "Sequence", "pretokenizers": [llama_split, {"type": "ByteLevel", "use_regex": False}]}):
+        for norm in (None, {"type": "NFC"}, {"type": "Sequence", "normalizers": [{"type": "NFC"}]}, {"type": "Foo"}):
+            Tokenizer.from_str(json.dumps(toys.tok_json(vocab, [], normalizer=norm, pre_tokenizer=pre)))
+
+
+def test_empty_added_token_rejected():
+    obj = toys.tok_json({"a": 0}, [], added=[{"id": 1, "content": "", "special": True}])
+    with pytest.raises(UnsupportedConfigError):
+        Tokenizer.from_str(json.dumps(obj))
+
+
+def test_from_pretrained_local_cache(tmp_path, monkeypatch, gpt2_path):
+    monkeypatch.setenv("XDG_CACHE_HOME", str(tmp_path))
+    d = tmp_path / "huggingface" / "hub" / "org--name"
+    d.mkdir(parents=True)
+    with open(gpt2_path, "rb") as f:
+        (d / "tokenizer.json").write_bytes(f.read())
+    assert Tokenizer.from_pretrained("org/name", local_files_only=True).vocab_size == 50257
+    with pytest.raises(IOError):
+        Tokenizer.from_pretrained("org/other", local_files_only=True)
+    with pytest.raises(IOError):
+        Tokenizer.from_pretrained("org/name")  # network fetch: unavailable
+
+
+def test_pack_texts_type_errors():
+    with pytest.raises(TypeError):
+        ct.pack_texts("not a list")
+    with pytest.raises(TypeError):
+        ct.pack_texts(["ok", 3])
+    text, off = ct.pack_texts(["ab", "", "é"])
+    assert off.tolist() == [0, 2, 2, 4] and text[:4].tobytes() == "abé".encode()
+
+
+@pytest.mark.skipif(ct.device_count() > 0, reason="a HIP device is present")
+def test_encode_without_gpu_fails_loudly(gpt2_path):
+    tok = Tokenizer.from_file(gpt2_path)
+    with pytest.raises(ct.DeviceError):
+        tok.encode("hello world")
+
+
+def test_shard_bounds_cover_and_balance():
+    from complexity_tokenizer.parallel import concat_results, shard_bounds
+    rng = np.random.default_rng(0)
+    lens = rng.integers(0, 300, size=1001)
+    lens[::17] = 0
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    for world in (1, 2, 3, 8):
+        ranges = [shard_bounds(off, world, r) for r in range(world)]
+        assert ranges[0][0] == 0 and ranges[-1][1] == len(lens)
+        assert all(ranges[i][1] == ranges[i + 1][0] for i in range(world - 1))
+        sizes = [int(off[b] - off[a]) for a, b in ranges]
+        assert max(sizes) - min(sizes) <= 2 * 300 + int(off[-1]) // world // 10 + 1
+    parts = [(np.array([1, 2], np.uint32), np.array([0, 2], np.uint64)),
+             (np.array([3], np.uint32), np.array([0, 0, 1], np.uint64))]
+    ids, toff = concat_results(parts)
+    assert ids.tolist() == [1, 2, 3] and toff.tolist() == [0, 2, 2, 3]

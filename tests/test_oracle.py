@@ -1,0 +1,240 @@
+"""CPU tests of the oracle (oracle/ref_py.py, oracle/ctok_ref.c): pinned against the reference's
+own known-answer tests, the committed golden vectors, the `regex` module, and HF `tokenizers` on
+the input domain where the two provably agree.  Also pins, on the CPU, the
+per-code-point piece-start rules the HIP pre-tokenizer kernel evaluates (kernels.hip SegCtx)."""
+import hashlib
+import json
+import os
+import random
+import unicodedata
+
+import numpy as np
+import pytest
+
+from datagen import corpus
+from oracle import ref_c, ref_py
+from tests import edge_cases, toys
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.fixture(scope="module")
+def gpt2_obj(gpt2_path):
+    with open(gpt2_path) as f:
+        return json.load(f)
+
+
+# ----------------------------------------------------------------- reference known-answer tests
+
+def test_kat_bpe_hello():
+    """src/bpe.rs:219-250: lowest rank first, encode("hello") == [8]."""
+    obj = toys.hello_kat()
+    assert ref_py.RefTokenizer(obj).encode("hello") == [8]
+    assert ref_c.RefC(obj).encode_batch(["hello"]) == [[8]]
+
+
+def test_kat_bytes_to_unicode():
+    """src/models.rs:955-969 and src/trainer.rs:659-667."""
+    enc = ref_py.bytes_to_unicode()
+    assert len(enc) == 256
+    assert enc[ord(" ")] == "Ġ"
+    assert enc[ord("a")] == "a" and enc[ord("Z")] == "Z"
+    dec = {v: k for k, v in enc.items()}
+    assert all(dec[enc[b]] == b for b in range(256))
+
+
+def test_kat_nfc():
+    """src/normalizers.rs:223-230."""
+    assert unicodedata.normalize("NFC", "é") == "é"
+    assert ref_c.nfc_bytes("é".encode()) == "é".encode()
+
+
+def test_kat_loader_vocab_size():
+    """src/huggingface/mod.rs:1566-1592."""
+    assert ref_py.RefTokenizer(toys.loader_kat()).vocab_size == 8
+
+
+def test_kat_gpt2_split():
+    """src/pretokenizers.rs:625-630 (the reference only asserts > 1 piece); exact pieces here."""
+    pcs = [m.group(0) for m in ref_py.GPT2_PATTERN.finditer("Hello, world!")]
+    assert pcs == ["Hello", ",", " world", "!"]
+
+
+# ----------------------------------------------------------------- golden vectors
+
+def test_golden_c1(gpt2_obj):
+    g = np.load(os.path.join(GOLDEN, "c1_gpt2_50k.npz"))
+    text, off = corpus.corpus_c1()
+    assert np.array_equal(text, g["text"]) and np.array_equal(off, g["off"]), "C1 generator drifted"
+    py = ref_py.RefTokenizer(gpt2_obj)
+    docs = [d.decode() for d in corpus.unpack(text, off)]
+    got = py.encode_batch(docs)
+    ids, toff = g["ids"], g["tok_off"]
+    assert got == [ids[toff[i]:toff[i + 1]].tolist() for i in range(len(docs))]
+    cids, coff = ref_c.RefC(gpt2_obj).encode_packed(text, off)
+    assert np.array_equal(cids, ids) and np.array_equal(coff, toff)
+
+
+def test_golden_edge(gpt2_obj):
+    with open(os.path.join(GOLDEN, "edge_gpt2_50k.json")) as f:
+        cases = json.load(f)
+    py = ref_py.RefTokenizer(gpt2_obj)
+    rc = ref_c.RefC(gpt2_obj)
+    docs = [c[0] for c in cases]
+    assert py.encode_batch(docs) == [c[1] for c in cases]
+    assert rc.encode_batch(docs) == [c[1] for c in cases]
+
+
+def _digest(ids, tok_off):
+    h = hashlib.sha256()
+    h.update(np.ascontiguousarray(tok_off, dtype="<u8").tobytes())
+    h.update(np.ascontiguousarray(ids, dtype="<u4").tobytes())
+    return h.hexdigest()
+
+
+def test_golden_c2_first_100k_c_oracle(gpt2_obj):
+    with open(os.path.join(GOLDEN, "digests.json")) as f:
+        gold = json.load(f)["C2"]
+    text, off = corpus.corpus_c2()
+    n = gold["first_docs"]
+    ids, toff = ref_c.RefC(gpt2_obj).encode_packed(text[: int(off[n])], off[: n + 1])
+    assert len(ids) == gold["first_tokens"] and _digest(ids, toff) == gold["first_sha256"]
+
+
+# ----------------------------------------------------------------- the two oracles agree
+
+def test_c_oracle_matches_python_oracle(gpt2_obj):
+    docs = edge_cases.EDGE + edge_cases.long_docs() + edge_cases.random_unicode_docs(4000, seed=5)
+    assert ref_c.RefC(gpt2_obj).encode_batch(docs) == ref_py.RefTokenizer(gpt2_obj).encode_batch(docs)
+
+
+@pytest.mark.parametrize("variant", ["shuffled", "invalid_tail", "invalid_mixed"])
+def test_oracles_agree_on_quirky_tables(gpt2_obj, variant):
+    if variant == "shuffled":
+        obj = toys.shuffled_merges(gpt2_obj, seed=1)
+    elif variant == "invalid_tail":
+        obj = toys.with_invalid_merges(gpt2_obj, seed=2, n_bad=40, tail_only=True)
+    else:
+        obj = toys.with_invalid_merges(gpt2_obj, seed=3, n_bad=40)
+    docs = edge_cases.EDGE + edge_cases.random_unicode_docs(1500, seed=6)
+    py, rc = ref_py.RefTokenizer(obj), ref_c.RefC(obj)
+    try:
+        want = py.encode_batch(docs)
+    except ref_py.PanicException:
+        with pytest.raises(ref_py.PanicException):
+            rc.encode_batch(docs)
+        return
+    assert rc.encode_batch(docs) == want
+
+
+def test_nfc_matches_unicodedata():
+    rng = random.Random(9)
+    pool = [chr(c) for c in list(range(0x20, 0x250)) + list(range(0x300, 0x370)) + list(range(0x1100, 0x1176))
+            + list(range(0x11A8, 0x11C3)) + list(range(0xAC00, 0xAC40)) + list(range(0x1E00, 0x1F00))
+            + [0xF900, 0xFA10, 0x212B, 0x2126, 0x0F73, 0x0F75, 0x1D160, 0x0344, 0x0958, 0x09DC]]
+    for _ in range(3000):
+        s = "".join(rng.choice(pool) for _ in range(rng.randint(0, 12)))
+        assert ref_c.nfc_bytes(s.encode()) == unicodedata.normalize("NFC", s).encode(), repr(s)
+
+
+def test_piece_boundaries_match_regex():
+    for s in edge_cases.EDGE + edge_cases.random_unicode_docs(3000, seed=8):
+        assert [p.decode() for p in ref_c.pieces(s.encode())] == [m.group(0) for m in ref_py.GPT2_PATTERN.finditer(s)]
+
+
+# ----------------------------------------------------------------- the GPU segmentation rules
+
+def _cls(c):
+    if ref_py._rust_ws(c):
+        return 0
+    import regex
+    if regex.match(r"\p{L}", c):
+        return 1
+    if regex.match(r"\p{N}", c):
+        return 2
+    return 3
+
+
+def gpu_rule_pieces(s):
+    """Python transcription of kernels.hip SegCtx::start (run-class segmentation)."""
+    u = list(s)
+    c = [_cls(x) for x in u]
+    n = len(u)
+
+    def prev(i):
+        return i - 1 if i > 0 else -1
+
+    def nxt(i):
+        return i + 1 if i + 1 < n else -1
+
+    def attached(i):
+        if u[i] != " ":
+            return False
+        j = nxt(i)
+        if j < 0 or c[j] == 0:
+            return False
+        p = prev(i)
+        return p < 0 or c[p] != 0
+
+    def con_len(i):
+        if u[i] != "'":
+            return 0
+        n1 = nxt(i)
+        if n1 < 0 or c[n1] != 1:
+            return 0
+        p = prev(i)
+        if p >= 0 and (c[p] == 3 or attached(p)):
+            return 0
+        a = u[n1]
+        if a in "stmd":
+            return 1
+        n2 = nxt(n1)
+        if n2 < 0:
+            return 0
+        return 2 if a + u[n2] in ("re", "ve", "ll") else 0
+
+    def start(i):
+        if i == 0:
+            return True
+        p = prev(i)
+        if c[i] != c[p]:
+            return not (attached(p) or con_len(p) > 0)
+        if c[i] == 1:
+            pp = prev(p)
+            if pp >= 0:
+                if con_len(pp) == 1:
+                    return True
+                ppp = prev(pp)
+                if ppp >= 0 and con_len(ppp) == 2:
+                    return True
+        return False
+
+    cuts = [i for i in range(n) if start(i)] + [n]
+    return ["".join(u[a:b]) for a, b in zip(cuts[:-1], cuts[1:])]
+
+
+def test_gpu_segmentation_rules_equal_regex():
+    docs = edge_cases.EDGE + edge_cases.random_unicode_docs(20000, seed=10, max_len=24)
+    for s in docs:
+        assert gpu_rule_pieces(s) == [m.group(0) for m in ref_py.GPT2_PATTERN.finditer(s)], repr(s)
+
+
+# ----------------------------------------------------------------- independent BPE cross-check
+
+def test_hf_tokenizers_agree_on_shared_domain(gpt2_path, gpt2_obj):
+    """HF `tokenizers` (Rust) BPE equals the oracle where both apply the same split: single spaces
+    between words, no other whitespace, NFC-stable text, no added-token strings."""
+    tokenizers = pytest.importorskip("tokenizers")
+    hf = tokenizers.Tokenizer.from_file(gpt2_path)
+    py = ref_py.RefTokenizer(gpt2_obj)
+    rng = random.Random(12)
+    words = ["the", "and", "of", "don't", "it's", "12", "3456", "hello", "world", "!", "?!", ".", "café",
+             "naïve", "x1", "a", "I", "we'll", "(", ")", "世界", "\U0001f600"]
+    text, off = corpus.corpus_c1()
+    lex = [w for d in corpus.unpack(text, off) for w in d.decode().split() if w.isascii()][:3000]
+    for _ in range(1500):
+        k = rng.randint(1, 12)
+        s = " ".join(rng.choice(words + lex) for _ in range(k))
+        if rng.random() < 0.5:
+            s = " " + s
+        assert hf.encode(s, add_special_tokens=False).ids == py.encode(s), repr(s)
