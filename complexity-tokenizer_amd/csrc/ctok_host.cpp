@@ -172,7 +172,7 @@ struct DeviceState {
   DevBuf<uint64_t> comp_key;
   Tables t{};
   // workspace
-  DevBuf<uint32_t> docbits, pbits, tile_cnt, word_prefix, pstart, pcnt, scratch, doc_piece, long_list, mid_list, region, region2, ccnt, counters, lw;
+  DevBuf<uint32_t> docbits, pbits, tile_cnt, word_prefix, pstart, pcnt, scratch, doc_piece, long_list, mid_list, region, region2, ccnt, dense, counters, lw;
   DevBuf<uint64_t> scan_tmp;
   DevBuf<uint32_t> doc_flag, ncp;
   DevBuf<uint64_t> norm_off;
@@ -699,6 +699,7 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   ds->region.ensure((size_t)grid1 * region_len + 16);
   ds->region2.ensure((size_t)grid1 * region_len + 16);
   ds->ccnt.ensure(3 * ((size_t)grid1 + 1) + 16);
+  ds->dense.ensure(B + 16);
   ds->lw.ensure(4 * B + 64);
   ds->scan_tmp.ensure(scan_tmp_elems(std::max<uint64_t>(B + 1, n_docs + 1)) + 64);
   w.docbits = ds->docbits.p;
@@ -716,6 +717,7 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   w.grid1 = grid1;
   w.region2 = ds->region2.p;
   w.ccnt = ds->ccnt.p;
+  w.dense = ds->dense.p;
   w.counters = ds->counters.p;
   w.lw = ds->lw.p;
   w.scan_tmp = (uint32_t*)ds->scan_tmp.p;

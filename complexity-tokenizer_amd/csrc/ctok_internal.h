@@ -85,6 +85,7 @@ struct Work {              // device pointers, sized by the host for one call
   uint32_t region_len;     // entries per block (>= pieces per block)
   uint32_t grid1;          // blocks of the routing pass
   uint32_t* ccnt;          // [3][grid1 + 1] pieces per block and class, scanned to offsets
+  uint32_t* dense;         // the three class lists gathered densely (k_compact)
   uint32_t* counters;      // [0] long count, [2] err, [3] nfc docs, [4] mid count, [5] list16 count
   uint32_t* lw;            // long-piece workspace: 4 * n_bytes u32
   uint32_t* scan_tmp;      // scan partials

@@ -145,153 +145,161 @@ hipError_t launch_docstart(const Work& w, hipStream_t s) {
 }
 
 // ------------------------------------------------------------------------------------------
-// pre-tokenizer: piece-start bitmap.  One 256-thread workgroup per 4 KiB tile, 16 bytes per
-// thread, the tile plus a 32-byte halo each side staged in LDS.
+// pre-tokenizer: piece-start bitmap, bit-parallel.
+//
+// A wavefront owns 16 consecutive 64-byte words of a 4 KiB tile (4 waves per workgroup).  Lane l
+// classifies byte 64*g + l (continuation bytes take their lead's class); __ballot turns every
+// per-byte predicate into one 64-bit scalar mask, and the "piece starts here" predicate of
+// GPT2_PATTERN becomes a few dozen SALU ops per word over those
+// masks and their one-, two- and three-bit neighbours.  prev/next across word edges come from
+// the previous/next word's masks, carried in registers.  Positions >= n_bytes read as doc
+// starts (D), which closes every run at the end of the text.
 
-constexpr int kSegHalo = 32;
-constexpr int kSegN = kTile + 2 * kSegHalo;
-constexpr uint8_t kCont = 0xFF;  // continuation byte
-constexpr uint8_t kOut = 0xFE;   // outside the text
-
-struct SegCtx {
-  const uint8_t* b;
-  const uint32_t* cp;
-  const uint8_t* cl;
-  const uint32_t* doc;
-  int64_t base;       // global position of LDS index 0
-  int64_t wbase;      // global bitmap word of s_doc[0]
-  uint32_t n_bytes;
-
-  __device__ __forceinline__ bool docst(int i) const {
-    const int64_t g = base + i;
-    return (doc[(g >> 5) - wbase] >> (g & 31)) & 1u;
-  }
-  __device__ __forceinline__ int prev(int i) const {
-    if (docst(i)) return -1;
-    int j = i - 1;
-    while (cl[j] == kCont) --j;
-    return j;
-  }
-  __device__ __forceinline__ int next(int i) const {
-    const int j = i + u8len(b[i]);
-    if (base + j >= (int64_t)n_bytes || docst(j)) return -1;
-    return j;
-  }
-  // a single U+0020 that begins the following non-space run (the " ?" of the pattern)
-  __device__ __forceinline__ bool attached(int i) const {
-    if (cp[i] != ' ') return false;
-    const int n = next(i);
-    if (n < 0 || cl[n] == 0) return false;
-    const int p = prev(i);
-    return p < 0 || cl[p] != 0;
-  }
-  // length (1 or 2 letters) of a contraction 's|'t|'re|'ve|'m|'ll|'d that starts at i, else 0
-  __device__ __forceinline__ int con_len(int i) const {
-    if (cp[i] != '\'') return 0;
-    const int n1 = next(i);
-    if (n1 < 0 || cl[n1] != 1) return 0;
-    const int p = prev(i);
-    if (p >= 0 && (cl[p] == 3 || attached(p))) return 0;
-    const uint32_t a = cp[n1];
-    if (a == 's' || a == 't' || a == 'm' || a == 'd') return 1;
-    const int n2 = next(n1);
-    if (n2 < 0) return 0;
-    const uint32_t c = cp[n2];
-    if ((a == 'r' && c == 'e') || (a == 'v' && c == 'e') || (a == 'l' && c == 'l')) return 2;
-    return 0;
-  }
-  __device__ __forceinline__ bool start(int i) const {
-    if (docst(i)) return true;
-    const int p = prev(i);
-    if (cl[i] != cl[p]) {
-      if (attached(p)) return false;
-      if (con_len(p) > 0) return false;
-      return true;
-    }
-    if (cl[i] == 1) {  // a letter run may be cut after a contraction's letters
-      const int pp = prev(p);
-      if (pp >= 0) {
-        if (con_len(pp) == 1) return true;
-        const int ppp = prev(pp);
-        if (ppp >= 0 && con_len(ppp) == 2) return true;
-      }
-    }
-    return false;
-  }
+struct SegMasks {
+  uint64_t W, L, N;       // class White_Space / letter / number (other = none of them)
+  uint64_t S, Q;          // ' ' and '\''
+  uint64_t T1, R, Le, V, LL;  // 's','t','m','d' / 'r' / 'e' / 'v' / 'l'
+  uint64_t D;             // doc start (or past the end of the text)
 };
 
-__global__ __launch_bounds__(kSegThreads) void k_segment(Work w, Tables t) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_b[kSegN];
-  __shared__ uint32_t s_cp[kSegN];
-  __shared__ uint8_t s_cl[kSegN];
-  __shared__ uint32_t s_doc[kSegN / 32 + 4];
-  __shared__ uint32_t s_red[kSegThreads / 64];
+__device__ __forceinline__ uint64_t p1(uint64_t c, uint64_t p) { return (c << 1) | (p >> 63); }
+__device__ __forceinline__ uint64_t p2(uint64_t c, uint64_t p) { return (c << 2) | (p >> 62); }
+__device__ __forceinline__ uint64_t p3(uint64_t c, uint64_t p) { return (c << 3) | (p >> 61); }
+__device__ __forceinline__ uint64_t n1(uint64_t c, uint64_t n) { return (c >> 1) | (n << 63); }
+__device__ __forceinline__ uint64_t n2(uint64_t c, uint64_t n) { return (c >> 2) | (n << 62); }
 
-  const uint32_t tid = threadIdx.x;
-  const uint32_t t0 = blockIdx.x * kTile;
-  const int64_t base = (int64_t)t0 - kSegHalo;
+// class of the code point byte x belongs to (x < B; non-ASCII slow path)
+__device__ __noinline__ int seg_cls_wide(const uint8_t* text, uint32_t B, uint32_t x, const Tables& t) {
+  uint32_t j = x;
+#pragma unroll
+  for (int k = 0; k < 3; k++)
+    if (j > 0 && (text[j] & 0xC0) == 0x80) j--;
+  const uint32_t b0 = text[j];
+  const int len = u8len((uint8_t)b0);
+  auto at = [&](uint32_t i) -> uint32_t { return text[min(i, B - 1)] & 0x3Fu; };
+  uint32_t c;
+  if (len == 1) c = b0;
+  else if (len == 2) c = ((b0 & 0x1Fu) << 6) | at(j + 1);
+  else if (len == 3) c = ((b0 & 0x0Fu) << 12) | (at(j + 1) << 6) | at(j + 2);
+  else c = ((b0 & 0x07u) << 18) | (at(j + 1) << 12) | (at(j + 2) << 6) | at(j + 3);
+  return cls_of(c, t);
+}
+
+// masks of 64-byte word g given this lane's byte b (already loaded; 0 past the end)
+__device__ __forceinline__ SegMasks seg_masks(const Work& w, const Tables& t, int64_t g, uint32_t b) {
+  SegMasks m;
+  const uint32_t B = w.n_bytes;
+  if (g < 0) {
+    m.W = m.L = m.N = m.S = m.Q = m.T1 = m.R = m.Le = m.V = m.LL = m.D = 0;
+    return m;
+  }
+  const uint64_t x0 = (uint64_t)g * 64;
+  if (x0 >= B) {
+    m.W = m.L = m.N = m.S = m.Q = m.T1 = m.R = m.Le = m.V = m.LL = 0;
+    m.D = ~0ull;
+    return m;
+  }
+  const uint32_t x = (uint32_t)x0 + (threadIdx.x & 63);
+  const bool in = x < B;
+  int c = cls_ascii(b);
+  if (__ballot(b >= 0x80)) {
+    if (b >= 0x80) c = seg_cls_wide(w.text, B, x, t);
+  }
+  m.W = __ballot(in && c == 0);
+  m.L = __ballot(in && c == 1);
+  m.N = __ballot(in && c == 2);
+  m.S = __ballot(b == ' ');
+  m.Q = __ballot(b == '\'');
+  m.T1 = __ballot(b == 's' || b == 't' || b == 'm' || b == 'd');
+  m.R = __ballot(b == 'r');
+  m.Le = __ballot(b == 'e');
+  m.V = __ballot(b == 'v');
+  m.LL = __ballot(b == 'l');
+  const uint32_t wi = (uint32_t)(x0 >> 5);
+  const uint64_t doc = (uint64_t)w.docbits[wi] | ((uint64_t)w.docbits[wi + 1] << 32);
+  m.D = doc | ~__ballot(in);
+  return m;
+}
+
+struct SegDerived { uint64_t A, C1, C2; };  // attached space, 1- and 2-letter contraction at i
+
+// rp/rc/rn = masks of words g-1, g, g+1; A_prev = attached-space mask of word g-1
+__device__ __forceinline__ SegDerived seg_derive(const SegMasks& rp, const SegMasks& rc, const SegMasks& rn,
+                                                 uint64_t A_prev) {
+  SegDerived d;
+  const uint64_t P = ~(rc.W | rc.L | rc.N), Pp = ~(rp.W | rp.L | rp.N);
+  const uint64_t E = n1(rc.D, rn.D);  // run ends after i (next position starts a doc)
+  // ' ' that begins the following non-space run: next exists and is not White_Space, and
+  // the previous code point is absent or not White_Space
+  d.A = rc.S & ~E & ~n1(rc.W, rn.W) & (rc.D | ~p1(rc.W, rp.W));
+  // '\'' followed by a letter, previous absent or (not other and not an attached space)
+  const uint64_t Cb = rc.Q & ~E & n1(rc.L, rn.L) & (rc.D | (~p1(P, Pp) & ~p1(d.A, A_prev)));
+  const uint64_t t1 = n1(rc.T1, rn.T1);
+  d.C1 = Cb & t1;
+  d.C2 = Cb & ~t1 & ~n2(rc.D, rn.D) &
+         (((n1(rc.R, rn.R) | n1(rc.V, rn.V)) & n2(rc.Le, rn.Le)) | (n1(rc.LL, rn.LL) & n2(rc.LL, rn.LL)));
+  return d;
+}
+
+constexpr int kSegWordsPerWave = kTile / 64 / (kSegThreads / 64);  // 16
+
+__global__ __launch_bounds__(kSegThreads) void k_segment(Work w, Tables t) {
+  __shared__ uint32_t s_red[kSegThreads / 64];
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t g0 = (int64_t)blockIdx.x * (kTile / 64) + (int64_t)wid * kSegWordsPerWave;
   const uint32_t B = w.n_bytes;
 
-  // stage bytes: the tile with 16-byte loads, the halos byte-wise
-  if ((uint64_t)t0 + kTile <= B) {
-    const uint4 v = *reinterpret_cast<const uint4*>(w.text + t0 + tid * 16);
-    *reinterpret_cast<uint4*>(s_b + kSegHalo + tid * 16) = v;
-  } else {
-    for (int k = 0; k < 16; k++) {
-      const uint64_t g = (uint64_t)t0 + tid * 16 + k;
-      s_b[kSegHalo + tid * 16 + k] = g < B ? w.text[g] : 0;
-    }
-  }
-  if (tid < 2 * kSegHalo) {
-    const int i = tid < kSegHalo ? (int)tid : kTile + (int)tid;
-    const int64_t g = base + i;
-    s_b[i] = (g >= 0 && g < (int64_t)B) ? w.text[g] : 0;
-  }
-  const int64_t wbase = (base >> 5);
-  for (int j = tid; j < kSegN / 32 + 4; j += kSegThreads) {
-    const int64_t wg = wbase + j;
-    s_doc[j] = (wg >= 0 && wg < (int64_t)w.n_words + 2) ? w.docbits[wg] : 0u;
-  }
-  __syncthreads();
-
-  // decode code points at lead bytes, classify
-  for (int i = tid; i < kSegN; i += kSegThreads) {
-    const int64_t g = base + i;
-    if (g < 0 || g >= (int64_t)B) { s_cl[i] = kOut; s_cp[i] = 0; continue; }
-    const uint8_t b0 = s_b[i];
-    if ((b0 & 0xC0) == 0x80) { s_cl[i] = kCont; s_cp[i] = 0; continue; }
-    const int len = u8len(b0);
-    if (i + len > kSegN) { s_cl[i] = kOut; s_cp[i] = 0; continue; }
-    uint32_t c;
-    if (len == 1) c = b0;
-    else if (len == 2) c = ((b0 & 0x1Fu) << 6) | (s_b[i + 1] & 0x3Fu);
-    else if (len == 3) c = ((b0 & 0x0Fu) << 12) | ((s_b[i + 1] & 0x3Fu) << 6) | (s_b[i + 2] & 0x3Fu);
-    else c = ((b0 & 0x07u) << 18) | ((s_b[i + 1] & 0x3Fu) << 12) | ((s_b[i + 2] & 0x3Fu) << 6) | (s_b[i + 3] & 0x3Fu);
-    s_cp[i] = c;
-    s_cl[i] = (uint8_t)cls_of(c, t);
-  }
-  __syncthreads();
-
-  SegCtx cx{s_b, s_cp, s_cl, s_doc, base, wbase, B};
-  uint32_t mask = 0;
-  for (int k = 0; k < 16; k++) {
-    const int i = kSegHalo + tid * 16 + k;
-    const uint8_t c = s_cl[i];
-    if (c >= kOut) continue;
-    if (cx.start(i)) mask |= 1u << k;
-  }
-  // pair up 16-bit masks into bitmap words
-  const uint32_t hi = (uint32_t)__shfl_down((int)mask, 1, 64);
-  const uint32_t word_idx = (t0 >> 5) + (tid >> 1);
-  if ((tid & 1) == 0 && word_idx < w.n_words) w.pbits[word_idx] = mask | (hi << 16);
-
-  uint32_t c = __popc(mask);
+  // this lane's byte of words g0-1 .. g0+16, all loads issued up front
+  uint32_t by[kSegWordsPerWave + 2];
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) c += (uint32_t)__shfl_xor((int)c, o, 64);
-  if ((tid & 63) == 0) s_red[tid >> 6] = c;
+  for (int k = 0; k < kSegWordsPerWave + 2; k++) {
+    const int64_t x = (g0 - 1 + k) * 64 + lane;
+    const int64_t xc = x < 0 ? 0 : (x >= (int64_t)B ? (int64_t)B - 1 : x);
+    const uint32_t v = w.text[xc];
+    by[k] = (x >= 0 && x < (int64_t)B) ? v : 0u;
+  }
+
+  SegMasks rp, rc, rn;
+  {
+    SegMasks rz = seg_masks(w, t, -1, 0);
+    rc = seg_masks(w, t, g0 - 1, by[0]);
+    rn = seg_masks(w, t, g0, by[1]);
+    // word g0-1: only its top three bits are used below, and they do not depend on word g0-2
+    SegDerived d = seg_derive(rz, rc, rn, 0);
+    rp = rc;
+    rc = rn;
+    // carry
+    uint32_t out = 0, cnt = 0;
+    uint64_t A_p = d.A, C1_p = d.C1, C2_p = d.C2;
+#pragma unroll
+    for (int k = 0; k < kSegWordsPerWave; k++) {
+      const int64_t g = g0 + k;
+      rn = seg_masks(w, t, g + 1, by[k + 2]);
+      const SegDerived dc = seg_derive(rp, rc, rn, A_p);
+      const uint64_t chg = (rc.W ^ p1(rc.W, rp.W)) | (rc.L ^ p1(rc.L, rp.L)) | (rc.N ^ p1(rc.N, rp.N));
+      const uint64_t cc = dc.C1 | dc.C2, cc_p = C1_p | C2_p;
+      uint64_t st = rc.D | (chg & ~p1(dc.A, A_p) & ~p1(cc, cc_p)) |
+                    (~chg & rc.L & (p2(dc.C1, C1_p) | p3(dc.C2, C2_p)));
+      const uint64_t x0 = (uint64_t)g * 64;
+      st = x0 >= B ? 0ull : (B - x0 >= 64 ? st : st & ((1ull << (B - x0)) - 1));
+      cnt += __popcll(st);
+      if (lane == 2 * k) out = (uint32_t)st;
+      if (lane == 2 * k + 1) out = (uint32_t)(st >> 32);
+      rp = rc;
+      rc = rn;
+      A_p = dc.A;
+      C1_p = dc.C1;
+      C2_p = dc.C2;
+    }
+    const uint64_t wi = (uint64_t)g0 * 2 + lane;
+    if (lane < 2 * kSegWordsPerWave && wi < w.n_words) w.pbits[wi] = out;
+    if (lane == 0) s_red[wid] = cnt;
+  }
   __syncthreads();
-  if (tid == 0) {
+  if (threadIdx.x == 0) {
     uint32_t s = 0;
+#pragma unroll
     for (int j = 0; j < kSegThreads / 64; j++) s += s_red[j];
     w.tile_cnt[blockIdx.x] = s;
   }
@@ -481,16 +489,23 @@ __device__ __forceinline__ uint64_t pair_key(uint32_t a, uint32_t b) { return ((
 
 // Pieces of at most N bytes.  FIRST: the pass over every piece, which routes longer pieces to
 // the 16-byte list / medium (LDS) list / long (wavefront) list; else: the pieces of list16.
-// block b of the first pass holding dense index g of a class whose per-block counts were
-// exclusive-scanned into off[0..grid1] (off[grid1] = total)
-__device__ __forceinline__ uint32_t owner_block(const uint32_t* off, uint32_t n, uint32_t g) {
-  uint32_t lo = 0, hi = n;  // off[lo] <= g < off[hi]
-  while (hi - lo > 1) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (off[mid] <= g) lo = mid; else hi = mid;
-  }
-  return lo;
+// Bytes s .. s + 4*NW - 1 of the text as NW little-endian words, read with NW + 1 aligned dword
+// loads whose addresses are clamped into the buffer: every load is unconditional (a predicated
+// per-byte load makes hipcc branch and wait vmcnt(0) around each one); bytes past the piece or the
+// text are garbage and must be masked by the caller.
+template <int NW>
+__device__ __forceinline__ void load_words(const uint8_t* text, uint32_t s, uint32_t n_bytes, uint32_t (&wv)[NW]) {
+  const uint32_t a0 = s & ~3u;
+  const uint32_t last = (n_bytes - 1) & ~3u;
+  uint32_t d[NW + 1];
+#pragma unroll
+  for (int j = 0; j <= NW; j++) d[j] = *reinterpret_cast<const uint32_t*>(text + min(a0 + 4 * j, last));
+  const uint32_t sh = s & 3u;
+#pragma unroll
+  for (int j = 0; j < NW; j++) wv[j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh);
 }
+
+__device__ __forceinline__ uint32_t byte_of(uint32_t w, int k) { return (w >> (8 * (k & 3))) & 255u; }
 
 // Routing pass: block b takes a contiguous range of pieces.  A piece of <= 8 bytes that is one
 // self-encoding vocab token is finished here with a single whole-piece probe; every other piece
@@ -516,16 +531,10 @@ __global__ __launch_bounds__(256) void k_route(Work w, Tables t) {
       else ra[w.region_len - 1 - atomicAdd(&s_cnt[1], 1u)] = p;
       continue;
     }
-    const uint8_t* bytes = w.text + s;
-    uint32_t lo = 0, hi = 0;
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-      if ((uint32_t)k < n) {
-        const uint32_t c = bytes[k];
-        if (k < 4) lo |= c << (8 * k);
-        else hi |= c << (8 * (k - 4));
-      }
-    }
+    uint32_t wv[2];
+    load_words<2>(w.text, s, w.n_bytes, wv);
+    const uint32_t lo = n >= 4 ? wv[0] : wv[0] & ((1u << (8 * n)) - 1u);
+    const uint32_t hi = n >= 8 ? wv[1] : n <= 4 ? 0u : wv[1] & ((1u << (8 * (n - 4))) - 1u);
     uint32_t h = piece_hash(lo, hi, n) & t.piece_mask;
     uint32_t hit = kNone;
     for (;;) {
@@ -545,8 +554,23 @@ __global__ __launch_bounds__(256) void k_route(Work w, Tables t) {
   if (tid < 3) w.ccnt[tid * (w.grid1 + 1) + blockIdx.x] = s_cnt[tid];
 }
 
-// Merge pass over one length class (N = 8, 16, 32 slots) as a dense index space over the
-// routing pass's per-block lists (counts exclusive-scanned in w.ccnt).
+// Gather the routing pass's per-block class lists into one dense array: class 0 at
+// [0, T0), class 1 at [T0, T0 + T1), class 2 after (per-block counts already exclusive-scanned).
+__global__ __launch_bounds__(256) void k_compact(Work w) {
+  const uint32_t b = blockIdx.x, G1 = w.grid1 + 1;
+  const uint32_t* c0 = w.ccnt;
+  const uint32_t* c1 = w.ccnt + G1;
+  const uint32_t* c2 = w.ccnt + 2 * G1;
+  const uint32_t T0 = c0[w.grid1], T1 = c1[w.grid1];
+  const uint32_t* ra = w.region + (size_t)b * w.region_len;
+  const uint32_t* rb = w.region2 + (size_t)b * w.region_len;
+  const uint32_t n0 = c0[b + 1] - c0[b], n1 = c1[b + 1] - c1[b], n2 = c2[b + 1] - c2[b];
+  for (uint32_t j = threadIdx.x; j < n0; j += 256) w.dense[c0[b] + j] = ra[j];
+  for (uint32_t j = threadIdx.x; j < n1; j += 256) w.dense[T0 + c1[b] + j] = ra[w.region_len - 1 - j];
+  for (uint32_t j = threadIdx.x; j < n2; j += 256) w.dense[T0 + T1 + c2[b] + j] = rb[j];
+}
+
+// Merge pass over one length class (N = 8, 16, 32 slots) of the dense list.
 template <int N, bool COMPACT>
 __global__ __launch_bounds__(256) void k_bpe_reg(Work w, Tables t) {
   __shared__ int32_t s_b2id[256];
@@ -554,41 +578,38 @@ __global__ __launch_bounds__(256) void k_bpe_reg(Work w, Tables t) {
   s_b2id[tid] = t.byte2id[tid];
   __syncthreads();
   uint32_t* err = &w.counters[2];
-  const int cls = N == 8 ? 0 : N == 16 ? 1 : 2;
-  const uint32_t* coff = w.ccnt + cls * (w.grid1 + 1);
-  const uint32_t P = coff[w.grid1];
+  const uint32_t G1 = w.grid1 + 1;
+  const uint32_t T0 = w.ccnt[w.grid1], T1 = w.ccnt[G1 + w.grid1], T2 = w.ccnt[2 * G1 + w.grid1];
+  const uint32_t base = N == 8 ? 0 : N == 16 ? T0 : T0 + T1;
+  const uint32_t P = N == 8 ? T0 : N == 16 ? T1 : T2;
   for (uint32_t q = blockIdx.x * 256 + tid; q < P; q += gridDim.x * 256) {
-    const uint32_t b = owner_block(coff, w.grid1, q);
-    const uint32_t j = q - coff[b];
-    const uint32_t p = cls == 0 ? w.region[(size_t)b * w.region_len + j]
-                     : cls == 1 ? w.region[(size_t)b * w.region_len + w.region_len - 1 - j]
-                                : w.region2[(size_t)b * w.region_len + j];
+    const uint32_t p = w.dense[base + q];
     const uint32_t s = w.pstart[p];
     const uint32_t n = w.pstart[p + 1] - s;
-    const uint8_t* bytes = w.text + s;
     uint32_t tk[N], rk[N];
     bool missing = false;
+    {
+      uint32_t wv[N / 4];
+      load_words<N / 4>(w.text, s, w.n_bytes, wv);
 #pragma unroll
-    for (int k = 0; k < N; k++) {
-      int32_t id = -1;
-      if ((uint32_t)k < n) {
-        id = s_b2id[bytes[k]];
-        missing |= id < 0;
+      for (int k = 0; k < N; k++) {
+        const int32_t id = s_b2id[byte_of(wv[k >> 2], k)];
+        missing |= ((uint32_t)k < n) & (id < 0);
+        tk[k] = (uint32_t)id;
       }
-      tk[k] = (uint32_t)id;
     }
     if (missing) {  // a byte char absent from the vocab is dropped: generic path
       w.mid_list[atomicAdd(&w.counters[4], 1u)] = p;
       continue;
     }
 #pragma unroll
-    for (int k0 = 0; k0 < N - 1; k0 += 8) {  // first probes of 8 pairs in flight together
+    for (int k0 = 0; k0 < N - 1; k0 += 8) {  // first probes of 8 pairs in flight together (unconditional)
       uint32_t hh[8];
       uint64_t ee[8];
 #pragma unroll
       for (int j = 0; j < 8; j++) {
         const int k = k0 + j;
-        if (k < N - 1 && (uint32_t)k + 1 < n) {
+        if (k < N - 1) {
           hh[j] = mhash(tk[k], tk[k + 1]) & t.merge_mask;
           ee[j] = t.merge_tab[hh[j]];
         }
@@ -616,8 +637,10 @@ __global__ __launch_bounds__(256) void k_bpe_reg(Work w, Tables t) {
       }
       const bool has_l = bi > 0, has_r = bi + 2 < m;
       const uint32_t hl = mhash(L, nid) & t.merge_mask, hr = mhash(nid, R) & t.merge_mask;
-      const uint64_t el = has_l ? t.merge_tab[hl] : kEmpty;  // both new pairs probe in parallel
-      const uint64_t er = has_r ? t.merge_tab[hr] : kEmpty;
+      const uint64_t el0 = t.merge_tab[hl];  // both new pairs probe in parallel, unconditionally
+      const uint64_t er0 = t.merge_tab[hr];
+      const uint64_t el = has_l ? el0 : kEmpty;
+      const uint64_t er = has_r ? er0 : kEmpty;
 #pragma unroll
       for (int k = 0; k < N; k++) {  // ascending: tk[k+1] is read before it is overwritten
         const uint32_t nxt_t = k + 1 < N ? tk[k + 1] : kDead;
@@ -650,6 +673,7 @@ static hipError_t launch_bpe_reg(const Work& w, const Tables& t, hipStream_t s) 
     uint32_t* cc = w.ccnt + c * (w.grid1 + 1);
     HIPCHK(scan_u32(cc, cc, w.grid1, nullptr, w.scan_tmp, w.scan_tmp_cap, s));
   }
+  k_compact<<<w.grid1, 256, 0, s>>>(w);
   const uint32_t g2 = w.grid1 / 4 + 1;
   k_bpe_reg<8, C><<<g2, 256, 0, s>>>(w, t);
   k_bpe_reg<16, C><<<g2, 256, 0, s>>>(w, t);

@@ -1,7 +1,8 @@
 """CPU tests of the oracle (oracle/ref_py.py, oracle/ctok_ref.c): pinned against the reference's
 own known-answer tests, the committed golden vectors, the `regex` module, and HF `tokenizers` on
 the input domain where the two provably agree.  Also pins, on the CPU, the
-per-code-point piece-start rules the HIP pre-tokenizer kernel evaluates (kernels.hip SegCtx)."""
+piece-start rules the HIP pre-tokenizer kernel evaluates, per code point and in the
+bit-parallel form of kernels.hip k_segment."""
 import hashlib
 import json
 import os
@@ -156,7 +157,8 @@ def _cls(c):
 
 
 def gpu_rule_pieces(s):
-    """Python transcription of kernels.hip SegCtx::start (run-class segmentation, SURVEY.md 8a)."""
+    """Per-code-point form of the run-class segmentation rules that k_segment
+    evaluates bit-parallel (bitparallel_starts below)."""
     u = list(s)
     c = [_cls(x) for x in u]
     n = len(u)
@@ -217,6 +219,86 @@ def test_gpu_segmentation_rules_equal_regex():
     docs = edge_cases.EDGE + edge_cases.random_unicode_docs(20000, seed=10, max_len=24)
     for s in docs:
         assert gpu_rule_pieces(s) == [m.group(0) for m in ref_py.GPT2_PATTERN.finditer(s)], repr(s)
+
+
+def bitparallel_starts(text, docstart):
+    """Python transcription of kernels.hip k_segment: the piece-start predicate evaluated on
+    64-bit masks of 64-byte words (SegMasks / seg_derive), word neighbours carried across edges."""
+    M = (1 << 64) - 1
+    B = len(text)
+
+    def masks(g):
+        m = dict.fromkeys(("W", "L", "N", "S", "Q", "T1", "R", "Le", "V", "LL", "D"), 0)
+        if g < 0:
+            return m
+        for k in range(64):
+            x = g * 64 + k
+            if x >= B:
+                m["D"] |= 1 << k
+                continue
+            b = text[x]
+            j = x
+            while (text[j] & 0xC0) == 0x80:
+                j -= 1
+            c = _cls(text[j:j + 4].decode("utf-8", errors="ignore")[:1])
+            for key, hit in (("W", c == 0), ("L", c == 1), ("N", c == 2), ("S", b == 32), ("Q", b == 39),
+                             ("T1", b in b"stmd"), ("R", b == 114), ("Le", b == 101), ("V", b == 118),
+                             ("LL", b == 108), ("D", docstart[x])):
+                if hit:
+                    m[key] |= 1 << k
+        return m
+
+    def p(c, q, k):
+        return ((c << k) | (q >> (64 - k))) & M
+
+    def n(c, q, k):
+        return ((c >> k) | (q << (64 - k))) & M
+
+    def derive(rp, rc, rn, a_prev):
+        P = ~(rc["W"] | rc["L"] | rc["N"]) & M
+        Pp = ~(rp["W"] | rp["L"] | rp["N"]) & M
+        E = n(rc["D"], rn["D"], 1)
+        A = rc["S"] & ~E & ~n(rc["W"], rn["W"], 1) & (rc["D"] | ~p(rc["W"], rp["W"], 1)) & M
+        Cb = rc["Q"] & ~E & n(rc["L"], rn["L"], 1) & (rc["D"] | (~p(P, Pp, 1) & ~p(A, a_prev, 1))) & M
+        t1 = n(rc["T1"], rn["T1"], 1)
+        C2 = Cb & ~t1 & ~n(rc["D"], rn["D"], 2) & (
+            ((n(rc["R"], rn["R"], 1) | n(rc["V"], rn["V"], 1)) & n(rc["Le"], rn["Le"], 2))
+            | (n(rc["LL"], rn["LL"], 1) & n(rc["LL"], rn["LL"], 2))) & M
+        return A, Cb & t1, C2
+
+    out = []
+    rp, rc, rn = masks(-2), masks(-1), masks(0)
+    a_p, c1_p, c2_p = derive(rp, rc, rn, 0)
+    rp, rc = rc, rn
+    for g in range((B + 63) // 64):
+        rn = masks(g + 1)
+        A, C1, C2 = derive(rp, rc, rn, a_p)
+        chg = 0
+        for key in ("W", "L", "N"):
+            chg |= rc[key] ^ p(rc[key], rp[key], 1)
+        st = rc["D"] | (chg & ~p(A, a_p, 1) & ~p(C1 | C2, c1_p | c2_p, 1) & M) | (
+            ~chg & rc["L"] & (p(C1, c1_p, 2) | p(C2, c2_p, 3)) & M)
+        out += [g * 64 + k for k in range(64) if (st >> k) & 1 and g * 64 + k < B]
+        rp, rc = rc, rn
+        a_p, c1_p, c2_p = A, C1, C2
+    return out
+
+
+def test_gpu_bitparallel_segmentation_equals_regex():
+    rng = random.Random(11)
+    for trial in range(150):
+        docs = edge_cases.EDGE if trial == 0 else edge_cases.random_unicode_docs(
+            rng.randint(1, 40), seed=rng.randint(0, 10 ** 9), max_len=40)
+        text = b"".join(d.encode() for d in docs)
+        ds = [0] * len(text)
+        want, o = [], 0
+        for d in docs:
+            e = d.encode()
+            if e:
+                ds[o] = 1
+            want += [o + len(d[:m.start()].encode()) for m in ref_py.GPT2_PATTERN.finditer(d)]
+            o += len(e)
+        assert bitparallel_starts(text, ds) == want, docs
 
 
 # ----------------------------------------------------------------- independent BPE cross-check
