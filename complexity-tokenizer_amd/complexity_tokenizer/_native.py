@@ -40,7 +40,8 @@ class Stats(ctypes.Structure):
                 ("ms_emit", ctypes.c_double), ("ms_h2d", ctypes.c_double),
                 ("ms_d2h", ctypes.c_double), ("bytes_in", ctypes.c_uint64), ("bytes_norm", ctypes.c_uint64),
                 ("docs", ctypes.c_uint64), ("pieces", ctypes.c_uint64), ("long_pieces", ctypes.c_uint64),
-                ("tokens", ctypes.c_uint64), ("nfc_docs", ctypes.c_uint64)]
+                ("tokens", ctypes.c_uint64), ("nfc_docs", ctypes.c_uint64), ("ms_segment", ctypes.c_double),
+                ("ms_bpe8", ctypes.c_double), ("ms_bpe16", ctypes.c_double), ("ms_bpe32", ctypes.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -158,7 +158,7 @@ struct DeviceState {
   int device = -1;
   std::mutex mu;
   hipStream_t stream = nullptr;
-  hipEvent_t ev[8] = {};
+  hipEvent_t ev[10] = {};
   hipEvent_t ev_sync = nullptr;   // spin-waited completion marker (no blocking-wait wakeup latency)
   uint64_t* host = nullptr;       // pinned host words for small device->host readbacks
   // tables
@@ -172,8 +172,9 @@ struct DeviceState {
   DevBuf<uint64_t> comp_key;
   Tables t{};
   // workspace
-  DevBuf<uint32_t> docbits, pbits, tile_cnt, word_prefix, pstart, pcnt, scratch, doc_piece, long_list, mid_list, region, region2, ccnt, dense, counters, lw;
-  DevBuf<uint64_t> scan_tmp;
+  DevBuf<uint32_t> docbits, pbits, tile_np, tile_tok, tcls, list0, list1, list2, tcnt, scratch, counters, lw;
+  DevBuf<uint16_t> wpref, tpos;
+  DevBuf<uint64_t> long_list, mid_list, scan_tmp;
   DevBuf<uint32_t> doc_flag, ncp;
   DevBuf<uint64_t> norm_off;
   DevBuf<uint8_t> norm_text;
@@ -684,63 +685,69 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   w.n_docs = (uint32_t)n_docs;
   w.n_words = (uint32_t)((B + 31) / 32);
   w.n_tiles = (uint32_t)((B + kTile - 1) / kTile);
+  const size_t nt = w.n_tiles;
   ds->docbits.ensure(w.n_words + 8);
   ds->pbits.ensure(w.n_words + 8);
-  ds->tile_cnt.ensure(w.n_tiles + 2);
-  ds->word_prefix.ensure(w.n_words + 8);
-  ds->pstart.ensure(B + 2);
-  ds->pcnt.ensure(B + 2);
-  ds->scratch.ensure(B + 2);
-  ds->doc_piece.ensure(n_docs + 2);
-  ds->long_list.ensure(B / kShortMax + 2);
-  ds->mid_list.ensure(B / 2 + 2);
-  uint32_t grid1 = (uint32_t)std::min<uint64_t>(16384, std::max<uint64_t>(1, (B / 4 + 2047) / 2048));
-  uint32_t region_len = (uint32_t)((B + 1 + grid1 - 1) / grid1);  // pieces <= B: per-block share
-  ds->region.ensure((size_t)grid1 * region_len + 16);
-  ds->region2.ensure((size_t)grid1 * region_len + 16);
-  ds->ccnt.ensure(3 * ((size_t)grid1 + 1) + 16);
-  ds->dense.ensure(B + 16);
+  ds->wpref.ensure(nt * 64 + 8);
+  ds->tile_np.ensure(nt + 8);
+  ds->tile_tok.ensure(nt + 8);
+  ds->tcls.ensure(3 * nt + 8);
+  ds->list0.ensure(nt * kCap0 + 8);
+  if (tb.n_at == 0) {
+    ds->list1.ensure(nt * kCap1 + 8);
+    ds->list2.ensure(nt * kCap2 + 8);
+  }
+  ds->tpos.ensure(nt * kTileSlots + 8);
+  ds->tcnt.ensure(nt * kTileSlots + 8);
+  ds->scratch.ensure(B + 8);
+  ds->long_list.ensure(B / kShortMax + nt + 8);
+  ds->mid_list.ensure(B / 2 + 8);
   ds->lw.ensure(4 * B + 64);
-  ds->scan_tmp.ensure(scan_tmp_elems(std::max<uint64_t>(B + 1, n_docs + 1)) + 64);
+  ds->scan_tmp.ensure(scan_tmp_elems(std::max<uint64_t>(nt + 1, n_docs + 1)) + 64);
   w.docbits = ds->docbits.p;
   w.pbits = ds->pbits.p;
-  w.tile_cnt = ds->tile_cnt.p;
-  w.word_prefix = ds->word_prefix.p;
-  w.pstart = ds->pstart.p;
-  w.pcnt = ds->pcnt.p;
+  w.wpref = ds->wpref.p;
+  w.tile_np = ds->tile_np.p;
+  w.tile_tok = ds->tile_tok.p;
+  w.tcls = ds->tcls.p;
+  w.list0 = ds->list0.p;
+  w.list1 = ds->list1.p;
+  w.list2 = ds->list2.p;
+  w.tpos = ds->tpos.p;
+  w.tcnt = ds->tcnt.p;
   w.scratch = ds->scratch.p;
-  w.doc_piece = ds->doc_piece.p;
   w.long_list = ds->long_list.p;
   w.mid_list = ds->mid_list.p;
-  w.region = ds->region.p;
-  w.region_len = region_len;
-  w.grid1 = grid1;
-  w.region2 = ds->region2.p;
-  w.ccnt = ds->ccnt.p;
-  w.dense = ds->dense.p;
   w.counters = ds->counters.p;
   w.lw = ds->lw.p;
   w.scan_tmp = (uint32_t*)ds->scan_tmp.p;
   w.scan_tmp_cap = ds->scan_tmp.cap * 2;
 
+  // events: 0 start | 1 segment | 2 class 0 | 3 class 1 | 4 class 2 + dropped-byte pieces |
+  //         5 long pieces | 6 emit
   STEP("docstart", launch_docstart(w, s));
+  if (timing) HIPTRY(hipEventRecord(ds->ev[7], s));
   STEP("segment", launch_segment(w, tb, s));
-  STEP("pieces", launch_pieces(w, s));
   if (timing) HIPTRY(hipEventRecord(ds->ev[1], s));
-  STEP("bpe", launch_bpe(w, tb, s));
+  STEP("bpe0", launch_bpe_class(w, tb, 0, s));
   if (timing) HIPTRY(hipEventRecord(ds->ev[2], s));
-  STEP("bpe_long", launch_bpe_long(w, tb, s));
+  STEP("bpe1", launch_bpe_class(w, tb, 1, s));
   if (timing) HIPTRY(hipEventRecord(ds->ev[3], s));
-  STEP("emit", launch_emit(w, d_ids, ids_cap, d_tok_off, s));
+  STEP("bpe2", launch_bpe_class(w, tb, 2, s));
+  STEP("bpe_mid", launch_bpe_class(w, tb, 3, s));
   if (timing) HIPTRY(hipEventRecord(ds->ev[4], s));
+  STEP("bpe_long", launch_bpe_long(w, tb, s));
+  if (timing) HIPTRY(hipEventRecord(ds->ev[5], s));
+  STEP("emit", launch_emit(w, d_ids, ids_cap, d_tok_off, s));
+  if (timing) HIPTRY(hipEventRecord(ds->ev[6], s));
+  if (st && w.n_tiles) STEP("count", launch_count_pieces(w, s));
   HIPTRY(hipMemcpyAsync(ds->host, d_tok_off + n_docs, 8, hipMemcpyDeviceToHost, s));
-  HIPTRY(hipMemcpyAsync(ds->host + 1, ds->counters.p, 16, hipMemcpyDeviceToHost, s));
-  HIPTRY(hipMemcpyAsync(ds->host + 3, ds->tile_cnt.p + w.n_tiles, 4, hipMemcpyDeviceToHost, s));
+  HIPTRY(hipMemcpyAsync(ds->host + 1, ds->counters.p, 24, hipMemcpyDeviceToHost, s));
   spin_sync(ds, s);
   const uint64_t ntok = ((volatile uint64_t*)ds->host)[0];
-  uint32_t cnt[4];
-  for (int i = 0; i < 4; i++) cnt[i] = ((volatile uint32_t*)(ds->host + 1))[i];
-  const uint32_t P = ((volatile uint32_t*)(ds->host + 3))[0];
+  uint32_t cnt[6];
+  for (int i = 0; i < 6; i++) cnt[i] = ((volatile uint32_t*)(ds->host + 1))[i];
+  const uint32_t P = cnt[5];
   if (cnt[2] & kErrPanic)
     throw_err(CTOK_E_PANIC, "index out of bounds: a merge rank points past the list of valid merges (reference src/bpe.rs:141 panics)");
   if (ntok > ids_cap) throw_err(CTOK_E_CAPACITY, "ids_cap too small: tok_off[n_docs] holds the number of ids needed");
@@ -753,17 +760,20 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
     st->tokens = ntok;
     st->nfc_docs = nfc_docs;
     if (timing) {
-      float a = 0, b = 0, b2 = 0, c = 0, d = 0;
-      HIPTRY(hipEventElapsedTime(&a, ds->ev[0], ds->ev[1]));
-      HIPTRY(hipEventElapsedTime(&b, ds->ev[1], ds->ev[2]));
-      HIPTRY(hipEventElapsedTime(&b2, ds->ev[2], ds->ev[3]));
-      HIPTRY(hipEventElapsedTime(&c, ds->ev[3], ds->ev[4]));
-      HIPTRY(hipEventElapsedTime(&d, ds->ev[0], ds->ev[4]));
-      st->ms_pretok = a;
-      st->ms_bpe_short = b;
-      st->ms_bpe_long = b2;
-      st->ms_emit = c;
-      st->ms_device = d;
+      auto el = [&](int i, int j) {
+        float v = 0;
+        HIPTRY(hipEventElapsedTime(&v, ds->ev[i], ds->ev[j]));
+        return (double)v;
+      };
+      st->ms_pretok = el(0, 1);
+      st->ms_segment = el(7, 1);
+      st->ms_bpe8 = el(1, 2);
+      st->ms_bpe16 = el(2, 3);
+      st->ms_bpe32 = el(3, 4);
+      st->ms_bpe_short = el(1, 4);
+      st->ms_bpe_long = el(4, 5);
+      st->ms_emit = el(5, 6);
+      st->ms_device = el(0, 6);
     }
   }
   return ntok;

@@ -19,10 +19,18 @@ constexpr uint32_t kPanicVal = kNoRank - 1;  // compact-table value of an entry 
 // Error bits written by kernels into Workspace::err (host checks after the call).
 constexpr uint32_t kErrPanic = 1u;
 
-constexpr int kTile = 4096;        // bytes per pre-tokenizer tile
-constexpr int kSegThreads = 256;   // 16 bytes per thread
-constexpr int kHalo = 16;
+// A tile is 62 64-byte bitmap words: one wavefront classifies the previous word, the tile's
+// words and the next tile's first word (where the tile's last piece ends) in its 64 lanes.
+constexpr int kTileWords = 62;
+constexpr int kTile = kTileWords * 64;  // 3968 bytes per pre-tokenizer tile (piece starts are tile-local)
+constexpr int kTileSlots = 4096;        // per-tile stride of the piece-indexed arrays (pieces <= kTile)
+constexpr int kSegWaves = 4;            // tiles (wavefronts) per k_segment workgroup
 constexpr int kShortMax = 32;      // pieces up to this many bytes are merged thread-per-piece
+// Per-tile piece lists by length class: <= 8 B (whole-piece probe missed), 9..16 B, 17..32 B.
+// Capacities are the most pieces of that class that can start in one tile.
+constexpr uint32_t kCap0 = kTile, kCap1 = (kTile + 8) / 9, kCap2 = (kTile + 16) / 17;
+// List entry (u32): start within the tile [0,12), piece index within the tile [12,24), length [24,30).
+__host__ __device__ inline uint32_t list_entry(uint32_t sl, uint32_t j, uint32_t n) { return sl | (j << 12) | (n << 24); }
 
 // Whole-piece table: raw byte strings of <= 8 bytes whose BPE is exactly one token (checked at
 // load time by running the merge loop on every vocab entry).  Entry = {lo32, hi32, len, id} of
@@ -68,25 +76,23 @@ struct Work {              // device pointers, sized by the host for one call
   uint32_t n_bytes;
   const uint64_t* doc_off; // (normalised) offsets, n_docs + 1
   uint32_t n_docs;
-  uint32_t* docbits;       // doc-start bitmap, n_words + 2
-  uint32_t* pbits;         // piece-start bitmap
+  uint32_t* docbits;       // doc-start bitmap (u32 words), n_words + 8
+  uint32_t* pbits;         // piece-start bitmap (u32 words), n_words + 8
   uint32_t n_words;
-  uint32_t* tile_cnt;      // n_tiles + 1 (exclusive-scanned in place into tile_base)
   uint32_t n_tiles;
-  uint32_t* word_prefix;   // n_words
-  uint32_t* pstart;        // n_bytes + 1
-  uint32_t* pcnt;          // n_bytes + 1 (scanned into ptok in place)
-  uint32_t* scratch;       // n_bytes: tokens of piece p at scratch[pstart[p]..]
-  uint32_t* doc_piece;     // n_docs + 1
-  uint32_t* long_list;     // n_bytes / kShortMax + 1
-  uint32_t* mid_list;      // pieces for the generic thread-per-piece kernel
-  uint32_t* region;        // per routing block: class-0 pieces from the front, class 1 from the back
-  uint32_t* region2;       // per routing block: class-2 pieces
-  uint32_t region_len;     // entries per block (>= pieces per block)
-  uint32_t grid1;          // blocks of the routing pass
-  uint32_t* ccnt;          // [3][grid1 + 1] pieces per block and class, scanned to offsets
-  uint32_t* dense;         // the three class lists gathered densely (k_compact)
-  uint32_t* counters;      // [0] long count, [2] err, [3] nfc docs, [4] mid count, [5] list16 count
+  uint16_t* wpref;         // [n_tiles * 64] pieces of the tile before each 64-byte word
+  uint32_t* tile_np;       // [n_tiles] pieces starting in the tile
+  uint32_t* tile_tok;      // [n_tiles + 1] tokens per tile, scanned in place to the tile's first id
+  uint32_t* tcls;          // [3][n_tiles] entries of each class list
+  uint32_t* list0;         // [n_tiles * kCap0] (also every <= 32 B piece when added tokens can match)
+  uint32_t* list1;         // [n_tiles * kCap1]
+  uint32_t* list2;         // [n_tiles * kCap2]
+  uint16_t* tpos;          // [n_tiles * kTileSlots] start (within the tile) of piece j
+  uint32_t* tcnt;          // [n_tiles * kTileSlots] ids of piece j, then (k_emit) its first id within the tile
+  uint32_t* scratch;       // [n_bytes] ids of the piece starting at byte s at scratch[s ..]
+  uint64_t* long_list;     // pieces > kShortMax B (or of unknown length at a tile end): s | j << 32
+  uint64_t* mid_list;      // pieces with dropped bytes for the generic kernel: s | j << 32 | n << 48
+  uint32_t* counters;      // [0] long count, [2] err, [3] nfc docs, [4] mid count, [5] pieces (stats)
   uint32_t* lw;            // long-piece workspace: 4 * n_bytes u32
   uint32_t* scan_tmp;      // scan partials
   uint64_t scan_tmp_cap;
@@ -101,8 +107,8 @@ hipError_t launch_norm(const uint8_t* text, const uint64_t* doc_off, uint32_t n_
                        int add_prefix, int nfc, const Tables& t, uint32_t* cp_scratch, uint32_t* ncp,
                        uint64_t* new_len_then_off, uint8_t* out_text, int phase, hipStream_t s);
 hipError_t launch_segment(const Work& w, const Tables& t, hipStream_t s);
-hipError_t launch_pieces(const Work& w, hipStream_t s);
-hipError_t launch_bpe(const Work& w, const Tables& t, hipStream_t s);
+hipError_t launch_count_pieces(const Work& w, hipStream_t s);
+hipError_t launch_bpe_class(const Work& w, const Tables& t, int cls, hipStream_t s);  // 0,1,2 lists; 3 dropped-byte pieces
 hipError_t launch_bpe_long(const Work& w, const Tables& t, hipStream_t s);
 hipError_t launch_emit(const Work& w, uint32_t* ids, uint64_t ids_cap, uint64_t* tok_off, hipStream_t s);
 // exclusive scan of n u32 (n read from *n_dev when non-null, else n_max); out[n] = total

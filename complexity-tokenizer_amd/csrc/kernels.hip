@@ -10,18 +10,20 @@
 //
 // Data layout in HBM (all offsets u32: one call covers < 4 GiB of text):
 //   text[B] u8, doc_off[D+1] u64 (input) ->
-//   docbits / pbits: 1 bit per byte (doc start / piece start) ->
-//   pstart[P+1] u32 (piece start byte), word_prefix[B/32] u32 (pieces before each bitmap word) ->
-//   scratch[B] u32: the ids of piece p at scratch[pstart[p] ...] (ids <= bytes per piece) ->
-//   pcnt[P+1] u32 scanned in place to the token offset of each piece ->
+//   docbits / pbits: 1 bit per byte (doc start / piece start), 4 KiB tiles of 64 64-byte words ->
+//   per tile: wpref (pieces before each word), tpos[j] (start of piece j in the tile), three
+//   class lists of pieces still to merge, tile_np, tile_tok ->
+//   scratch[B] u32: the ids of the piece starting at byte s at scratch[s ...] (ids <= bytes) ->
+//   tcnt[tile][j] ids of piece j, tile_tok scanned to each tile's first id ->
 //   ids[T] u32 + tok_off[D+1] u64 (output).
+// No array is indexed by a global piece number, so no pass has to wait for a global piece count.
 //
-// The regex of GPT2_PATTERN is evaluated as a per-code-point "piece starts here" predicate
-// over classes {White_Space, L, N, other} (derivation in DESIGN.md 3.2): one wavefront-parallel
-// pass, no backtracking, coalesced 16-byte loads.
+// The regex of GPT2_PATTERN is evaluated as a "piece starts here" predicate over code-point
+// classes {White_Space, L, N, other} (derivation in DESIGN.md), bit-parallel on 64-bit masks.
 #include <hip/hip_runtime.h>
 
 #include "ctok_internal.h"
+#include "seg_lane.h"
 
 namespace ctok_dev {
 
@@ -75,6 +77,11 @@ __device__ T block_excl_scan(T v, T* smem /*[17]*/, T* total) {
   __syncthreads();
   return r;
 }
+
+// Wave-uniform values are moved to SGPRs with readfirstlane: the loop exits and the chain walk
+// then branch on scalars, so the wave can never split around the cross-lane reductions (a split
+// wave reduces over inactive lanes and never terminates).
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
 __device__ __forceinline__ int u8len(uint8_t b) {
   return b < 0x80 ? 1 : (b >> 5) == 6 ? 2 : (b >> 4) == 14 ? 3 : 4;
@@ -145,28 +152,9 @@ hipError_t launch_docstart(const Work& w, hipStream_t s) {
 }
 
 // ------------------------------------------------------------------------------------------
-// pre-tokenizer: piece-start bitmap, bit-parallel.
-//
-// A wavefront owns 16 consecutive 64-byte words of a 4 KiB tile (4 waves per workgroup).  Lane l
-// classifies byte 64*g + l (continuation bytes take their lead's class); __ballot turns every
-// per-byte predicate into one 64-bit scalar mask, and the "piece starts here" predicate of
-// GPT2_PATTERN becomes a few dozen SALU ops per word over those
-// masks and their one-, two- and three-bit neighbours.  prev/next across word edges come from
-// the previous/next word's masks, carried in registers.  Positions >= n_bytes read as doc
-// starts (D), which closes every run at the end of the text.
-
-struct SegMasks {
-  uint64_t W, L, N;       // class White_Space / letter / number (other = none of them)
-  uint64_t S, Q;          // ' ' and '\''
-  uint64_t T1, R, Le, V, LL;  // 's','t','m','d' / 'r' / 'e' / 'v' / 'l'
-  uint64_t D;             // doc start (or past the end of the text)
-};
-
-__device__ __forceinline__ uint64_t p1(uint64_t c, uint64_t p) { return (c << 1) | (p >> 63); }
-__device__ __forceinline__ uint64_t p2(uint64_t c, uint64_t p) { return (c << 2) | (p >> 62); }
-__device__ __forceinline__ uint64_t p3(uint64_t c, uint64_t p) { return (c << 3) | (p >> 61); }
-__device__ __forceinline__ uint64_t n1(uint64_t c, uint64_t n) { return (c >> 1) | (n << 63); }
-__device__ __forceinline__ uint64_t n2(uint64_t c, uint64_t n) { return (c >> 2) | (n << 62); }
+// pre-tokenizer: piece-start bitmap, bit-parallel, one 64-byte word per lane (k_segment below;
+// the per-word logic is csrc/seg_lane.h).  Positions >= n_bytes read as doc starts (D), which
+// closes every run at the end of the text.
 
 // class of the code point byte x belongs to (x < B; non-ASCII slow path)
 __device__ __noinline__ int seg_cls_wide(const uint8_t* text, uint32_t B, uint32_t x, const Tables& t) {
@@ -185,173 +173,314 @@ __device__ __noinline__ int seg_cls_wide(const uint8_t* text, uint32_t B, uint32
   return cls_of(c, t);
 }
 
-// masks of 64-byte word g given this lane's byte b (already loaded; 0 past the end)
-__device__ __forceinline__ SegMasks seg_masks(const Work& w, const Tables& t, int64_t g, uint32_t b) {
-  SegMasks m;
-  const uint32_t B = w.n_bytes;
-  if (g < 0) {
-    m.W = m.L = m.N = m.S = m.Q = m.T1 = m.R = m.Le = m.V = m.LL = m.D = 0;
-    return m;
-  }
-  const uint64_t x0 = (uint64_t)g * 64;
-  if (x0 >= B) {
-    m.W = m.L = m.N = m.S = m.Q = m.T1 = m.R = m.Le = m.V = m.LL = 0;
-    m.D = ~0ull;
-    return m;
-  }
-  const uint32_t x = (uint32_t)x0 + (threadIdx.x & 63);
-  const bool in = x < B;
-  int c = cls_ascii(b);
-  if (__ballot(b >= 0x80)) {
-    if (b >= 0x80) c = seg_cls_wide(w.text, B, x, t);
-  }
-  m.W = __ballot(in && c == 0);
-  m.L = __ballot(in && c == 1);
-  m.N = __ballot(in && c == 2);
-  m.S = __ballot(b == ' ');
-  m.Q = __ballot(b == '\'');
-  m.T1 = __ballot(b == 's' || b == 't' || b == 'm' || b == 'd');
-  m.R = __ballot(b == 'r');
-  m.Le = __ballot(b == 'e');
-  m.V = __ballot(b == 'v');
-  m.LL = __ballot(b == 'l');
-  const uint32_t wi = (uint32_t)(x0 >> 5);
-  const uint64_t doc = (uint64_t)w.docbits[wi] | ((uint64_t)w.docbits[wi + 1] << 32);
-  m.D = doc | ~__ballot(in);
-  return m;
+__device__ __forceinline__ uint64_t shfl_up64(uint64_t v) {
+  const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)v, 1, 64);
+  const uint32_t hi = (uint32_t)__shfl_up((int)(uint32_t)(v >> 32), 1, 64);
+  return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+__device__ __forceinline__ uint64_t shfl_down64(uint64_t v) {
+  const uint32_t lo = (uint32_t)__shfl_down((int)(uint32_t)v, 1, 64);
+  const uint32_t hi = (uint32_t)__shfl_down((int)(uint32_t)(v >> 32), 1, 64);
+  return (uint64_t)lo | ((uint64_t)hi << 32);
 }
 
-struct SegDerived { uint64_t A, C1, C2; };  // attached space, 1- and 2-letter contraction at i
-
-// rp/rc/rn = masks of words g-1, g, g+1; A_prev = attached-space mask of word g-1
-__device__ __forceinline__ SegDerived seg_derive(const SegMasks& rp, const SegMasks& rc, const SegMasks& rn,
-                                                 uint64_t A_prev) {
-  SegDerived d;
-  const uint64_t P = ~(rc.W | rc.L | rc.N), Pp = ~(rp.W | rp.L | rp.N);
-  const uint64_t E = n1(rc.D, rn.D);  // run ends after i (next position starts a doc)
-  // ' ' that begins the following non-space run: next exists and is not White_Space, and
-  // the previous code point is absent or not White_Space
-  d.A = rc.S & ~E & ~n1(rc.W, rn.W) & (rc.D | ~p1(rc.W, rp.W));
-  // '\'' followed by a letter, previous absent or (not other and not an attached space)
-  const uint64_t Cb = rc.Q & ~E & n1(rc.L, rn.L) & (rc.D | (~p1(P, Pp) & ~p1(d.A, A_prev)));
-  const uint64_t t1 = n1(rc.T1, rn.T1);
-  d.C1 = Cb & t1;
-  d.C2 = Cb & ~t1 & ~n2(rc.D, rn.D) &
-         (((n1(rc.R, rn.R) | n1(rc.V, rn.V)) & n2(rc.Le, rn.Le)) | (n1(rc.LL, rn.LL) & n2(rc.LL, rn.LL)));
-  return d;
+// Bytes s .. s + 4*NW - 1 of the text as NW little-endian words, read with NW + 1 aligned dword
+// loads whose addresses are clamped into the buffer: every load is unconditional (a predicated
+// per-byte load makes hipcc branch and wait vmcnt(0) around each one); bytes past the piece or the
+// text are garbage and must be masked by the caller.
+template <int NW>
+__device__ __forceinline__ void load_words(const uint8_t* text, uint32_t s, uint32_t n_bytes, uint32_t (&wv)[NW]) {
+  const uint32_t a0 = s & ~3u;
+  const uint32_t last = (n_bytes - 1) & ~3u;
+  uint32_t d[NW + 1];
+#pragma unroll
+  for (int j = 0; j <= NW; j++) d[j] = *reinterpret_cast<const uint32_t*>(text + min(a0 + 4 * j, last));
+  const uint32_t sh = s & 3u;
+#pragma unroll
+  for (int j = 0; j < NW; j++) wv[j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh);
 }
 
-constexpr int kSegWordsPerWave = kTile / 64 / (kSegThreads / 64);  // 16
+__device__ __forceinline__ uint32_t byte_of(uint32_t w, int k) { return (w >> (8 * (k & 3))) & 255u; }
 
-__global__ __launch_bounds__(kSegThreads) void k_segment(Work w, Tables t) {
-  __shared__ uint32_t s_red[kSegThreads / 64];
+// position of the k-th (0-based) set bit of x (k < popcount(x))
+__device__ __forceinline__ uint32_t select_bit(uint64_t x, uint32_t k) {
+  uint32_t pos = 0;
+  uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  uint32_t c = __popc(lo);
+  uint32_t v = lo;
+  if (k >= c) { k -= c; v = hi; pos = 32; }
+#pragma unroll
+  for (int wdt = 16; wdt >= 1; wdt >>= 1) {
+    const uint32_t m = (1u << wdt) - 1u;
+    c = __popc(v & m);
+    if (k >= c) { k -= c; v >>= wdt; pos += wdt; }
+  }
+  return pos;
+}
+
+// wave-aggregated append to an LDS counter: returns this lane's slot (lanes with take == false
+// get garbage).  One ds_add per wave instead of one per lane.
+__device__ __forceinline__ uint32_t wave_append(uint32_t* counter, bool take) {
+  const uint64_t m = __ballot(take);
+  uint32_t base = 0;
+  if (m) {
+    const uint32_t leader = __ffsll((unsigned long long)m) - 1;
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t b = 0;
+    if (lane == leader) b = atomicAdd(counter, (uint32_t)__popcll(m));
+    base = (uint32_t)__shfl((int)b, (int)leader, 64);
+  }
+  return base + (uint32_t)__popcll(m & lanemask_lt());
+}
+
+
+// One wavefront per tile, kSegWaves tiles per workgroup, no workgroup barrier.  Lane l owns the
+// 64-byte word g0 - 1 + l: lane 0 is the previous tile's last word (context only), lanes 1..62
+// are the tile's words, lane 63 is the next tile's first word (look-ahead: where the tile's last
+// piece ends; its bits 62-63 depend on a word no lane holds and are not used).
+//  A. per lane: the word's class / byte masks by SWAR tests (csrc/seg_lane.h); non-ASCII code
+//     points classified per code point; doc starts from the doc bitmap;
+//  B. per lane: the piece-start predicate, the neighbouring words' masks by cross-lane shuffles;
+//  C. thread per piece (piece j = the j-th start of the tile): length from the next start, then
+//     routing: a piece of <= 8 bytes that is one self-encoding vocab token is finished here with
+//     one whole-piece probe; every other piece is appended to its tile's class list (<= 8 B,
+//     9..16 B, 17..32 B) or to the long list, so that the merge passes run dense, length-uniform
+//     waves.
+__global__ __launch_bounds__(64 * kSegWaves) void k_segment(Work w, Tables t) {
+  __shared__ uint64_t s_st_all[kSegWaves][64];
+  __shared__ uint32_t s_wpre_all[kSegWaves][64];
+  __shared__ uint32_t s_cnt_all[kSegWaves][4];
   const uint32_t lane = threadIdx.x & 63;
-  const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t g0 = (int64_t)blockIdx.x * (kTile / 64) + (int64_t)wid * kSegWordsPerWave;
+  const uint32_t wid = uni(threadIdx.x >> 6);
+  const uint32_t tile = uni(blockIdx.x * kSegWaves + wid);
+  if (tile >= w.n_tiles) return;
+  uint64_t* s_st = s_st_all[wid];
+  uint32_t* s_wpre = s_wpre_all[wid];
+  uint32_t* s_cnt = s_cnt_all[wid];
+  if (lane < 4) s_cnt[lane] = 0;
   const uint32_t B = w.n_bytes;
+  const uint32_t t0 = tile * kTile;
+  const int64_t g = (int64_t)tile * kTileWords - 1 + lane;  // this lane's word
+  const bool first = lane == 0, last = lane == 63;
 
-  // this lane's byte of words g0-1 .. g0+16, all loads issued up front
-  uint32_t by[kSegWordsPerWave + 2];
-#pragma unroll
-  for (int k = 0; k < kSegWordsPerWave + 2; k++) {
-    const int64_t x = (g0 - 1 + k) * 64 + lane;
-    const int64_t xc = x < 0 ? 0 : (x >= (int64_t)B ? (int64_t)B - 1 : x);
-    const uint32_t v = w.text[xc];
-    by[k] = (x >= 0 && x < (int64_t)B) ? v : 0u;
-  }
-
-  SegMasks rp, rc, rn;
+  // ---- A
+  uint32_t x[16];
+  uint64_t D, valid;
   {
-    SegMasks rz = seg_masks(w, t, -1, 0);
-    rc = seg_masks(w, t, g0 - 1, by[0]);
-    rn = seg_masks(w, t, g0, by[1]);
-    // word g0-1: only its top three bits are used below, and they do not depend on word g0-2
-    SegDerived d = seg_derive(rz, rc, rn, 0);
-    rp = rc;
-    rc = rn;
-    // carry
-    uint32_t out = 0, cnt = 0;
-    uint64_t A_p = d.A, C1_p = d.C1, C2_p = d.C2;
+    const int64_t x0 = g * 64;
+    if (x0 >= 0 && x0 + 64 <= (int64_t)B) {
+      const uint4* p = reinterpret_cast<const uint4*>(w.text + x0);
 #pragma unroll
-    for (int k = 0; k < kSegWordsPerWave; k++) {
-      const int64_t g = g0 + k;
-      rn = seg_masks(w, t, g + 1, by[k + 2]);
-      const SegDerived dc = seg_derive(rp, rc, rn, A_p);
-      const uint64_t chg = (rc.W ^ p1(rc.W, rp.W)) | (rc.L ^ p1(rc.L, rp.L)) | (rc.N ^ p1(rc.N, rp.N));
-      const uint64_t cc = dc.C1 | dc.C2, cc_p = C1_p | C2_p;
-      uint64_t st = rc.D | (chg & ~p1(dc.A, A_p) & ~p1(cc, cc_p)) |
-                    (~chg & rc.L & (p2(dc.C1, C1_p) | p3(dc.C2, C2_p)));
-      const uint64_t x0 = (uint64_t)g * 64;
-      st = x0 >= B ? 0ull : (B - x0 >= 64 ? st : st & ((1ull << (B - x0)) - 1));
-      cnt += __popcll(st);
-      if (lane == 2 * k) out = (uint32_t)st;
-      if (lane == 2 * k + 1) out = (uint32_t)(st >> 32);
-      rp = rc;
-      rc = rn;
-      A_p = dc.A;
-      C1_p = dc.C1;
-      C2_p = dc.C2;
+      for (int k = 0; k < 4; k++) {
+        const uint4 v = p[k];
+        x[4 * k] = v.x; x[4 * k + 1] = v.y; x[4 * k + 2] = v.z; x[4 * k + 3] = v.w;
+      }
+      valid = ~0ull;
+    } else {
+#pragma unroll
+      for (int k = 0; k < 16; k++) x[k] = 0;
+      valid = 0;
+      if (x0 >= 0 && x0 < (int64_t)B) {  // the text's last, partial word
+        const uint32_t n = B - (uint32_t)x0;
+        valid = (1ull << n) - 1;
+        for (uint32_t i = 0; i < n; i++) x[i >> 2] |= (uint32_t)w.text[x0 + i] << (8 * (i & 3));
+      }
     }
-    const uint64_t wi = (uint64_t)g0 * 2 + lane;
-    if (lane < 2 * kSegWordsPerWave && wi < w.n_words) w.pbits[wi] = out;
-    if (lane == 0) s_red[wid] = cnt;
+    if (x0 < 0) D = 0;
+    else if (x0 >= (int64_t)B) D = ~0ull;
+    else {
+      const uint32_t wi = (uint32_t)(x0 >> 5);
+      D = (uint64_t)w.docbits[wi] | ((uint64_t)w.docbits[wi + 1] << 32);
+      D |= ~valid;
+    }
   }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t s = 0;
+  seg::Masks m = seg::ascii_masks(x);
+  if (m.NA) {  // non-ASCII code points: one class lookup per code point
+    const uint32_t x0 = (uint32_t)(g * 64);
+    uint64_t todo = m.NA;
+    while (todo) {
+      const uint32_t i = __builtin_ctzll(todo);
+      const uint32_t b0 = w.text[x0 + i];
+      const int cl = seg_cls_wide(w.text, B, x0 + i, t);
+      // a lead byte covers its continuation bytes within the word; a continuation byte at the
+      // start of the word (lead in the previous word) is classified on its own
+      const uint32_t len = (b0 & 0xC0) == 0x80 ? 1u : (uint32_t)u8len((uint8_t)b0);
+      const uint64_t bits = (len >= 64 - i ? ~0ull : ((1ull << len) - 1)) << i;
+      if (cl == 0) m.W |= bits & m.NA;
+      else if (cl == 1) m.L |= bits & m.NA;
+      else if (cl == 2) m.N |= bits & m.NA;
+      todo &= ~bits;
+    }
+  }
+  // contraction letters only where an apostrophe could use them (this word's or the previous
+  // word's last two bytes)
+  // (every lane takes part in each shuffle: a lane that is inactive at a ds_bpermute hands its
+  // neighbour zeros)
+  uint64_t pQ = shfl_up64(m.Q);
+  if (first) pQ = 0;
+  seg::Letters lt{0, 0, 0, 0, 0};
+  if (m.Q | (pQ >> 62)) lt = seg::letter_masks(x, m.NA);
+
+  // ---- B
+  uint64_t st;
+  {
+    uint64_t pW = shfl_up64(m.W), pL = shfl_up64(m.L), pN = shfl_up64(m.N);
+    if (first) pW = pL = pN = 0;
+    uint64_t nW = shfl_down64(m.W), nL = shfl_down64(m.L), nD = shfl_down64(D);
+    seg::Letters nl{shfl_down64(lt.T1), shfl_down64(lt.R), shfl_down64(lt.Le), shfl_down64(lt.V), shfl_down64(lt.LL)};
+    if (last) {
+      nW = nL = nD = 0;
+      nl = seg::Letters{0, 0, 0, 0, 0};
+    }
+    const uint64_t A = seg::attached(m, D, pW, nW, nD);
+    uint64_t pA = shfl_up64(A);
+    if (first) pA = 0;
+    uint64_t C1, C2;
+    seg::contractions(m, lt, D, A, pA, ~(pW | pL | pN), nL, nD, nl, C1, C2);
+    uint64_t pC1 = shfl_up64(C1), pC2 = shfl_up64(C2);
+    if (first) pC1 = pC2 = 0;
+    st = seg::starts(m, D, pW, pL, pN, A, pA, C1, C2, pC1, pC2) & valid;
+    if (last) st &= (1ull << 62) - 1;
+    if (!first && !last) {  // piece-start bitmap
+      const uint64_t gw = (uint64_t)g * 2;
+      if (gw < w.n_words) w.pbits[gw] = (uint32_t)st;
+      if (gw + 1 < w.n_words) w.pbits[gw + 1] = (uint32_t)(st >> 32);
+    }
+  }
+  const uint32_t c = (!first && !last) ? (uint32_t)__popcll(st) : 0u;
+  const uint32_t inc = wave_incl_scan(c);
+  // tile word wi = lane - 1: s_st[wi], s_wpre[wi] = pieces before it; s_wpre[62] = s_wpre[63] = np
+  if (!first) {
+    s_st[lane - 1] = st;
+    s_wpre[lane - 1] = inc - c;
+    w.wpref[(size_t)tile * 64 + lane - 1] = (uint16_t)(inc - c);
+  } else {
+    s_st[63] = 0;
+  }
+  const uint32_t np = uni((uint32_t)__shfl((int)inc, 63, 64));
+  if (first) s_wpre[63] = np;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+  // ---- C: thread per piece
+  const bool generic = t.n_at != 0;  // added tokens can match inside pieces: no whole-piece shortcut
+  uint32_t* tcnt = w.tcnt + (size_t)tile * kTileSlots;
+  uint16_t* tpos = w.tpos + (size_t)tile * kTileSlots;
+  const uint64_t trusted_end = (uint64_t)t0 + kTile + 62;  // the look-ahead's bits 0..61
+  uint32_t hits = 0;
+  for (uint32_t j0 = 0; j0 < np; j0 += 64) {
+    const uint32_t j = j0 + lane;
+    const bool act = j < np;
+    uint32_t sl = 0, n = 0, cls = 4;  // 0..2 class lists, 3 long, 4 done (or inactive)
+    if (act) {
+      // word of piece j: the last wi with s_wpre[wi] <= j (s_wpre[62] = s_wpre[63] = np > j)
+      uint32_t lo = 0;
 #pragma unroll
-    for (int j = 0; j < kSegThreads / 64; j++) s += s_red[j];
-    w.tile_cnt[blockIdx.x] = s;
+      for (uint32_t step = 32; step >= 1; step >>= 1)
+        if (s_wpre[lo + step] <= j) lo += step;
+      const uint64_t xw = s_st[lo];
+      const uint32_t bit = select_bit(xw, j - s_wpre[lo]);
+      sl = lo * 64 + bit;
+      // end: the next start (this word, a later word, or the look-ahead word)
+      const uint64_t rest = bit == 63 ? 0ull : (xw >> (bit + 1));
+      int64_t el = -1;
+      if (rest) {
+        el = sl + 1 + __builtin_ctzll(rest);
+      } else {
+        for (uint32_t v = lo + 1; v <= kTileWords; v++) {
+          const uint64_t y = s_st[v];
+          if (y) { el = v * 64 + __builtin_ctzll(y); break; }
+        }
+        if (el < 0 && (uint64_t)B <= trusted_end) el = (int64_t)B - t0;
+      }
+      tpos[j] = (uint16_t)sl;
+      if (el < 0 || el - sl > kShortMax) {
+        cls = 3;
+      } else {
+        n = (uint32_t)(el - sl);
+        if (generic) cls = 0;
+        else if (n > 16) cls = 2;
+        else if (n > 8) cls = 1;
+        else {
+          // whole-piece probe: the piece's raw bytes as one self-encoding vocab token
+          uint32_t wv[2];
+          load_words<2>(w.text, t0 + sl, B, wv);
+          const uint32_t plo = n >= 4 ? wv[0] : wv[0] & ((1u << (8 * n)) - 1u);
+          const uint32_t phi = n >= 8 ? wv[1] : n <= 4 ? 0u : wv[1] & ((1u << (8 * (n - 4))) - 1u);
+          uint32_t h = piece_hash(plo, phi, n) & t.piece_mask;
+          uint32_t hit = kNone;
+          for (;;) {
+            const uint4 e = t.piece_tab[h];
+            if (e.z == 0) break;
+            if (e.x == plo && e.y == phi && e.z == n) { hit = e.w; break; }
+            h = (h + 1) & t.piece_mask;
+          }
+          if (hit != kNone) {
+            w.scratch[t0 + sl] = hit;
+            tcnt[j] = 1;
+            hits++;
+            cls = 4;
+          } else {
+            cls = 0;
+          }
+        }
+      }
+    }
+    const uint32_t e = list_entry(sl, j, n);
+    {
+      const uint32_t q = wave_append(&s_cnt[0], cls == 0);
+      if (cls == 0) w.list0[(size_t)tile * kCap0 + q] = e;
+    }
+    if (!generic) {
+      const uint32_t q1 = wave_append(&s_cnt[1], cls == 1);
+      if (cls == 1) w.list1[(size_t)tile * kCap1 + q1] = e;
+      const uint32_t q2 = wave_append(&s_cnt[2], cls == 2);
+      if (cls == 2) w.list2[(size_t)tile * kCap2 + q2] = e;
+    }
+    const uint64_t lm = __ballot(cls == 3);
+    if (lm) {  // rare: one global atomic per wave
+      const uint32_t leader = __ffsll((unsigned long long)lm) - 1;
+      uint32_t b = 0;
+      if (lane == leader) b = atomicAdd(&w.counters[0], (uint32_t)__popcll(lm));
+      b = (uint32_t)__shfl((int)b, (int)leader, 64);
+      if (cls == 3) w.long_list[b + __popcll(lm & lanemask_lt())] = (uint64_t)(t0 + sl) | ((uint64_t)j << 32);
+    }
   }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) hits += (uint32_t)__shfl_xor((int)hits, o, 64);
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  if (lane == 0) {
+    w.tile_tok[tile] = hits;  // initial token count (the merge passes add theirs atomically)
+    w.tile_np[tile] = np;
+  }
+  if (lane < 3) w.tcls[(size_t)lane * w.n_tiles + tile] = s_cnt[lane];
 }
 
 hipError_t launch_segment(const Work& w, const Tables& t, hipStream_t s) {
-  if (w.n_tiles) k_segment<<<w.n_tiles, kSegThreads, 0, s>>>(w, t);
+  if (w.n_tiles) k_segment<<<(w.n_tiles + kSegWaves - 1) / kSegWaves, 64 * kSegWaves, 0, s>>>(w, t);
   return hipGetLastError();
 }
 
-// ------------------------------------------------------------------------------------------
-// piece list from the bitmap (tile_cnt already exclusive-scanned: tile_cnt[n_tiles] = P)
-
-__global__ __launch_bounds__(128) void k_pieces(Work w) {
-  __shared__ uint32_t s_scan[17];
-  const uint32_t tile = blockIdx.x;
-  const uint32_t wi = tile * (kTile / 32) + threadIdx.x;
-  uint32_t word = wi < w.n_words ? w.pbits[wi] : 0u;
-  const uint32_t excl = block_excl_scan<uint32_t>(__popc(word), s_scan, nullptr);
-  const uint32_t base = w.tile_cnt[tile] + excl;
-  if (wi < w.n_words) w.word_prefix[wi] = base;
-  uint32_t k = 0;
-  while (word) {
-    const uint32_t bit = __ffs(word) - 1;
-    w.pstart[base + k++] = wi * 32 + bit;
-    word &= word - 1;
+// pieces in the batch (statistics only): one workgroup sums tile_np into counters[5]
+__global__ __launch_bounds__(1024) void k_count_pieces(Work w) {
+  __shared__ uint32_t s_red[16];
+  uint32_t c = 0;
+  for (uint32_t i = threadIdx.x; i < w.n_tiles; i += 1024) c += w.tile_np[i];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c += (uint32_t)__shfl_xor((int)c, o, 64);
+  if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t sum = 0;
+    for (int k = 0; k < 16; k++) sum += s_red[k];
+    w.counters[5] = sum;
   }
-  if (tile == 0 && threadIdx.x == 0) w.pstart[w.tile_cnt[w.n_tiles]] = w.n_bytes;
 }
 
-__global__ void k_docpiece(Work w) {
-  const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
-  if (d > w.n_docs) return;
-  const uint64_t x = w.doc_off[d];
-  uint32_t r;
-  if (x >= w.n_bytes) {
-    r = w.tile_cnt[w.n_tiles];
-  } else {
-    const uint32_t wi = (uint32_t)(x >> 5);
-    r = w.word_prefix[wi] + __popc(w.pbits[wi] & ((1u << (x & 31)) - 1u));
-  }
-  w.doc_piece[d] = r;
-}
-
-hipError_t launch_pieces(const Work& w, hipStream_t s) {
-  HIPCHK(scan_u32(w.tile_cnt, w.tile_cnt, w.n_tiles, nullptr, w.scan_tmp, w.scan_tmp_cap, s));
-  if (w.n_tiles) k_pieces<<<w.n_tiles, 128, 0, s>>>(w);
-  else {
-    const uint32_t zero = 0;
-    HIPCHK(hipMemcpyAsync(w.pstart, &zero, 4, hipMemcpyHostToDevice, s));
-  }
-  k_docpiece<<<(w.n_docs + 1 + 255) / 256, 256, 0, s>>>(w);
+hipError_t launch_count_pieces(const Work& w, hipStream_t s) {
+  k_count_pieces<<<1, 1024, 0, s>>>(w);
   return hipGetLastError();
 }
 
@@ -416,26 +545,85 @@ __device__ __forceinline__ uint32_t bpe_short(const Tables& t, const uint8_t* by
   return m;
 }
 
-// Generic thread-per-piece kernel (LDS working arrays, handles dropped bytes and added
-// tokens).  list == nullptr: every piece (used when the tokenizer has matchable added tokens),
-// routing pieces longer than kShortMax to the long list; else: the pieces named in list.
-__global__ __launch_bounds__(256) void k_bpe_generic(Work w, Tables t, const uint32_t* list, const uint32_t* list_n) {
+// ------------------------------------------------------------------------------------------
+// Merge passes over the per-tile class lists.  Workgroup b takes K consecutive tiles and treats
+// their lists as one concatenated list (prefix of the K counts in LDS); entry q -> its tile by a
+// binary search over those K offsets.  Token counts are summed per tile in LDS and added to
+// tile_tok with one atomic per (workgroup, tile); no two workgroups share a (class, tile).
+
+template <int K>
+__device__ __forceinline__ uint32_t tile_share_init(const uint32_t* counts, uint32_t n_tiles, uint32_t t0,
+                                                    uint32_t* s_pre, uint32_t* s_tsum) {
+  static_assert(K >= 1 && K <= 64 && (K & (K - 1)) == 0, "K: power of two <= 64");
+  if (threadIdx.x < 64) {
+    const uint32_t l = threadIdx.x;
+    const uint32_t c = (l < K && t0 + l < n_tiles) ? counts[t0 + l] : 0u;
+    const uint32_t inc = wave_incl_scan(c);
+    if (l < K) {
+      s_pre[l] = inc - c;
+      s_tsum[l] = 0;
+    }
+    if (l == 63) s_pre[K] = inc;
+  }
+  __syncthreads();
+  return s_pre[K];
+}
+
+template <int K>
+__device__ __forceinline__ uint32_t tile_of(const uint32_t* s_pre, uint32_t q) {
+  uint32_t lo = 0;
+#pragma unroll
+  for (uint32_t step = K / 2; step >= 1; step >>= 1)
+    if (s_pre[lo + step] <= q) lo += step;
+  return lo;
+}
+
+template <int K>
+__device__ __forceinline__ void tile_share_flush(const Work& w, uint32_t t0, const uint32_t* s_tsum) {
+  __syncthreads();
+  if (threadIdx.x < K && t0 + threadIdx.x < w.n_tiles && s_tsum[threadIdx.x])
+    atomicAdd(&w.tile_tok[t0 + threadIdx.x], s_tsum[threadIdx.x]);
+}
+
+constexpr int kTilesGeneric = 2;  // tiles per workgroup, generic pass over list0
+
+// Generic thread-per-piece kernel (LDS working arrays; handles dropped bytes and added tokens).
+// MID = false: every piece of list0 (launched instead of the register passes when the tokenizer
+// has added tokens that can match inside a piece); MID = true: the pieces the register passes
+// found to contain a byte whose char is not in the vocab (mid_list).
+template <bool MID>
+__global__ __launch_bounds__(256) void k_bpe_generic(Work w, Tables t) {
   __shared__ uint32_t s_tok[kShortMax * 256];
   __shared__ uint32_t s_rk[kShortMax * 256];
   __shared__ int32_t s_b2id[256];
+  __shared__ uint32_t s_pre[kTilesGeneric + 1], s_tsum[kTilesGeneric];
   const uint32_t tid = threadIdx.x;
   s_b2id[tid] = t.byte2id[tid];
-  __syncthreads();
   uint32_t* err = &w.counters[2];
-  const uint32_t P = list ? *list_n : w.tile_cnt[w.n_tiles];
-  for (uint32_t q = blockIdx.x * 256 + tid; q < P; q += gridDim.x * 256) {
-    const uint32_t p = list ? list[q] : q;
-    const uint32_t s = w.pstart[p];
-    const uint32_t n = w.pstart[p + 1] - s;
-    if (n > kShortMax) {
-      const uint32_t li = atomicAdd(&w.counters[0], 1u);
-      w.long_list[li] = p;
-      continue;
+  uint32_t E, t0 = 0;
+  if (MID) {
+    __syncthreads();
+    E = w.counters[4];
+  } else {
+    t0 = blockIdx.x * kTilesGeneric;
+    E = tile_share_init<kTilesGeneric>(w.tcls, w.n_tiles, t0, s_pre, s_tsum);
+  }
+  const uint32_t stride = MID ? gridDim.x * 256 : 256;
+  for (uint32_t q = (MID ? blockIdx.x * 256 : 0) + tid; q < E; q += stride) {
+    uint32_t s, j, n, tile, kt = 0;
+    if (MID) {
+      const uint64_t e = w.mid_list[q];
+      s = (uint32_t)e;
+      j = (uint32_t)(e >> 32) & 0xFFFFu;
+      n = (uint32_t)(e >> 48);
+      tile = s / kTile;
+    } else {
+      kt = tile_of<kTilesGeneric>(s_pre, q);
+      tile = t0 + kt;
+      const uint32_t e = w.list0[(size_t)tile * kCap0 + (q - s_pre[kt])];
+      s = tile * kTile + (e & 0xFFFu);
+      j = (e >> 12) & 0xFFFu;
+      n = e >> 24;
     }
     const uint8_t* bytes = w.text + s;
     uint32_t* out = w.scratch + s;
@@ -462,15 +650,17 @@ __global__ __launch_bounds__(256) void k_bpe_generic(Work w, Tables t, const uin
         pos += nxt;
       }
     }
-    w.pcnt[p] = cnt;
+    w.tcnt[(size_t)tile * kTileSlots + j] = cnt;
+    if (MID) atomicAdd(&w.tile_tok[tile], cnt);
+    else atomicAdd(&s_tsum[kt], cnt);
   }
+  if (!MID) tile_share_flush<kTilesGeneric>(w, t0, s_tsum);
 }
 
 // ------------------------------------------------------------------------------------------
-// BPE fast path: pieces of <= kRegMax bytes merged by one thread with the tokens and pair ranks
-// in registers (fully unrolled, compile-time slot indices; no LDS, so occupancy is set by
-// VGPRs alone).  All first-probe loads of the initial pairs issue back to back.  Longer pieces
-// go to the medium (LDS) or long (wavefront) lists.
+// BPE fast path: pieces of <= N bytes merged by one thread with the tokens and pair ranks in
+// registers (fully unrolled, compile-time slot indices; no LDS for the working set, so occupancy
+// is set by VGPRs alone).  All first-probe loads of the initial pairs issue back to back.
 
 __device__ __forceinline__ uint32_t resolve_rank(const Tables& t, uint64_t key, uint32_t h, uint64_t e, uint32_t* err) {
   for (;;) {
@@ -487,105 +677,36 @@ __device__ __forceinline__ uint32_t resolve_rank(const Tables& t, uint64_t key, 
 
 __device__ __forceinline__ uint64_t pair_key(uint32_t a, uint32_t b) { return ((uint64_t)a << kIdBits) | b; }
 
-// Pieces of at most N bytes.  FIRST: the pass over every piece, which routes longer pieces to
-// the 16-byte list / medium (LDS) list / long (wavefront) list; else: the pieces of list16.
-// Bytes s .. s + 4*NW - 1 of the text as NW little-endian words, read with NW + 1 aligned dword
-// loads whose addresses are clamped into the buffer: every load is unconditional (a predicated
-// per-byte load makes hipcc branch and wait vmcnt(0) around each one); bytes past the piece or the
-// text are garbage and must be masked by the caller.
-template <int NW>
-__device__ __forceinline__ void load_words(const uint8_t* text, uint32_t s, uint32_t n_bytes, uint32_t (&wv)[NW]) {
-  const uint32_t a0 = s & ~3u;
-  const uint32_t last = (n_bytes - 1) & ~3u;
-  uint32_t d[NW + 1];
-#pragma unroll
-  for (int j = 0; j <= NW; j++) d[j] = *reinterpret_cast<const uint32_t*>(text + min(a0 + 4 * j, last));
-  const uint32_t sh = s & 3u;
-#pragma unroll
-  for (int j = 0; j < NW; j++) wv[j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh);
+template <int N> struct RegClass;
+template <> struct RegClass<8> { static constexpr int cls = 0, K = 4; static constexpr uint32_t cap = kCap0; };
+template <> struct RegClass<16> { static constexpr int cls = 1, K = 16; static constexpr uint32_t cap = kCap1; };
+template <> struct RegClass<32> { static constexpr int cls = 2, K = 64; static constexpr uint32_t cap = kCap2; };
+
+template <int N>
+__device__ __forceinline__ const uint32_t* class_list(const Work& w) {
+  return N == 8 ? w.list0 : N == 16 ? w.list1 : w.list2;
 }
 
-__device__ __forceinline__ uint32_t byte_of(uint32_t w, int k) { return (w >> (8 * (k & 3))) & 255u; }
-
-// Routing pass: block b takes a contiguous range of pieces.  A piece of <= 8 bytes that is one
-// self-encoding vocab token is finished here with a single whole-piece probe; every other piece
-// is filed by length so that the merge passes run dense, length-uniform waves:
-//   class 0 (<= 8 B, probe missed) front of regionA[b], class 1 (9..16 B) back of regionA[b],
-//   class 2 (17..32 B) front of regionB[b], longer pieces in the long list (one global counter).
-__global__ __launch_bounds__(256) void k_route(Work w, Tables t) {
-  __shared__ uint32_t s_cnt[3];
-  const uint32_t tid = threadIdx.x;
-  if (tid < 3) s_cnt[tid] = 0;
-  __syncthreads();
-  const uint32_t P = w.tile_cnt[w.n_tiles];
-  const uint32_t per = (P + gridDim.x - 1) / gridDim.x;
-  const uint32_t q0 = blockIdx.x * per, q1 = min(P, q0 + per);
-  uint32_t* ra = w.region + (size_t)blockIdx.x * w.region_len;
-  uint32_t* rb = w.region2 + (size_t)blockIdx.x * w.region_len;
-  for (uint32_t p = q0 + tid; p < q1; p += 256) {
-    const uint32_t s = w.pstart[p];
-    const uint32_t n = w.pstart[p + 1] - s;
-    if (n > 8) {
-      if (n > kShortMax) w.long_list[atomicAdd(&w.counters[0], 1u)] = p;
-      else if (n > 16) rb[atomicAdd(&s_cnt[2], 1u)] = p;
-      else ra[w.region_len - 1 - atomicAdd(&s_cnt[1], 1u)] = p;
-      continue;
-    }
-    uint32_t wv[2];
-    load_words<2>(w.text, s, w.n_bytes, wv);
-    const uint32_t lo = n >= 4 ? wv[0] : wv[0] & ((1u << (8 * n)) - 1u);
-    const uint32_t hi = n >= 8 ? wv[1] : n <= 4 ? 0u : wv[1] & ((1u << (8 * (n - 4))) - 1u);
-    uint32_t h = piece_hash(lo, hi, n) & t.piece_mask;
-    uint32_t hit = kNone;
-    for (;;) {
-      const uint4 e = t.piece_tab[h];
-      if (e.z == 0) break;
-      if (e.x == lo && e.y == hi && e.z == n) { hit = e.w; break; }
-      h = (h + 1) & t.piece_mask;
-    }
-    if (hit != kNone) {
-      w.scratch[s] = hit;
-      w.pcnt[p] = 1;
-    } else {
-      ra[atomicAdd(&s_cnt[0], 1u)] = p;
-    }
-  }
-  __syncthreads();
-  if (tid < 3) w.ccnt[tid * (w.grid1 + 1) + blockIdx.x] = s_cnt[tid];
-}
-
-// Gather the routing pass's per-block class lists into one dense array: class 0 at
-// [0, T0), class 1 at [T0, T0 + T1), class 2 after (per-block counts already exclusive-scanned).
-__global__ __launch_bounds__(256) void k_compact(Work w) {
-  const uint32_t b = blockIdx.x, G1 = w.grid1 + 1;
-  const uint32_t* c0 = w.ccnt;
-  const uint32_t* c1 = w.ccnt + G1;
-  const uint32_t* c2 = w.ccnt + 2 * G1;
-  const uint32_t T0 = c0[w.grid1], T1 = c1[w.grid1];
-  const uint32_t* ra = w.region + (size_t)b * w.region_len;
-  const uint32_t* rb = w.region2 + (size_t)b * w.region_len;
-  const uint32_t n0 = c0[b + 1] - c0[b], n1 = c1[b + 1] - c1[b], n2 = c2[b + 1] - c2[b];
-  for (uint32_t j = threadIdx.x; j < n0; j += 256) w.dense[c0[b] + j] = ra[j];
-  for (uint32_t j = threadIdx.x; j < n1; j += 256) w.dense[T0 + c1[b] + j] = ra[w.region_len - 1 - j];
-  for (uint32_t j = threadIdx.x; j < n2; j += 256) w.dense[T0 + T1 + c2[b] + j] = rb[j];
-}
-
-// Merge pass over one length class (N = 8, 16, 32 slots) of the dense list.
+// Merge pass over one length class (N = 8, 16, 32 slots).
 template <int N, bool COMPACT>
 __global__ __launch_bounds__(256) void k_bpe_reg(Work w, Tables t) {
+  using RC = RegClass<N>;
+  constexpr int K = RC::K;
   __shared__ int32_t s_b2id[256];
+  __shared__ uint32_t s_pre[K + 1], s_tsum[K];
   const uint32_t tid = threadIdx.x;
   s_b2id[tid] = t.byte2id[tid];
-  __syncthreads();
   uint32_t* err = &w.counters[2];
-  const uint32_t G1 = w.grid1 + 1;
-  const uint32_t T0 = w.ccnt[w.grid1], T1 = w.ccnt[G1 + w.grid1], T2 = w.ccnt[2 * G1 + w.grid1];
-  const uint32_t base = N == 8 ? 0 : N == 16 ? T0 : T0 + T1;
-  const uint32_t P = N == 8 ? T0 : N == 16 ? T1 : T2;
-  for (uint32_t q = blockIdx.x * 256 + tid; q < P; q += gridDim.x * 256) {
-    const uint32_t p = w.dense[base + q];
-    const uint32_t s = w.pstart[p];
-    const uint32_t n = w.pstart[p + 1] - s;
+  const uint32_t t0 = blockIdx.x * K;
+  const uint32_t E = tile_share_init<K>(w.tcls + (size_t)RC::cls * w.n_tiles, w.n_tiles, t0, s_pre, s_tsum);
+  const uint32_t* list = class_list<N>(w);
+  for (uint32_t q = tid; q < E; q += 256) {
+    const uint32_t kt = tile_of<K>(s_pre, q);
+    const uint32_t tile = t0 + kt;
+    const uint32_t e = list[(size_t)tile * RC::cap + (q - s_pre[kt])];
+    const uint32_t s = tile * kTile + (e & 0xFFFu);
+    const uint32_t j = (e >> 12) & 0xFFFu;
+    const uint32_t n = e >> 24;
     uint32_t tk[N], rk[N];
     bool missing = false;
     {
@@ -599,7 +720,7 @@ __global__ __launch_bounds__(256) void k_bpe_reg(Work w, Tables t) {
       }
     }
     if (missing) {  // a byte char absent from the vocab is dropped: generic path
-      w.mid_list[atomicAdd(&w.counters[4], 1u)] = p;
+      w.mid_list[atomicAdd(&w.counters[4], 1u)] = (uint64_t)s | ((uint64_t)j << 32) | ((uint64_t)n << 48);
       continue;
     }
 #pragma unroll
@@ -607,17 +728,17 @@ __global__ __launch_bounds__(256) void k_bpe_reg(Work w, Tables t) {
       uint32_t hh[8];
       uint64_t ee[8];
 #pragma unroll
-      for (int j = 0; j < 8; j++) {
-        const int k = k0 + j;
+      for (int jj = 0; jj < 8; jj++) {
+        const int k = k0 + jj;
         if (k < N - 1) {
-          hh[j] = mhash(tk[k], tk[k + 1]) & t.merge_mask;
-          ee[j] = t.merge_tab[hh[j]];
+          hh[jj] = mhash(tk[k], tk[k + 1]) & t.merge_mask;
+          ee[jj] = t.merge_tab[hh[jj]];
         }
       }
 #pragma unroll
-      for (int j = 0; j < 8; j++) {
-        const int k = k0 + j;
-        if (k < N - 1) rk[k] = ((uint32_t)k + 1 < n) ? resolve_rank(t, pair_key(tk[k], tk[k + 1]), hh[j], ee[j], err) : kNoRank;
+      for (int jj = 0; jj < 8; jj++) {
+        const int k = k0 + jj;
+        if (k < N - 1) rk[k] = ((uint32_t)k + 1 < n) ? resolve_rank(t, pair_key(tk[k], tk[k + 1]), hh[jj], ee[jj], err) : kNoRank;
       }
     }
     rk[N - 1] = kNoRank;
@@ -661,34 +782,32 @@ __global__ __launch_bounds__(256) void k_bpe_reg(Work w, Tables t) {
 #pragma unroll
     for (int k = 0; k < N; k++)
       if ((uint32_t)k < m) out[k] = tk[k];
-    w.pcnt[p] = m;
+    w.tcnt[(size_t)tile * kTileSlots + j] = m;
+    atomicAdd(&s_tsum[kt], m);
   }
+  tile_share_flush<K>(w, t0, s_tsum);
 }
 
-template <bool C>
-static hipError_t launch_bpe_reg(const Work& w, const Tables& t, hipStream_t s) {
-  k_route<<<w.grid1, 256, 0, s>>>(w, t);
-  HIPCHK(hipGetLastError());
-  for (int c = 0; c < 3; c++) {  // per-block class counts -> dense offsets
-    uint32_t* cc = w.ccnt + c * (w.grid1 + 1);
-    HIPCHK(scan_u32(cc, cc, w.grid1, nullptr, w.scan_tmp, w.scan_tmp_cap, s));
-  }
-  k_compact<<<w.grid1, 256, 0, s>>>(w);
-  const uint32_t g2 = w.grid1 / 4 + 1;
-  k_bpe_reg<8, C><<<g2, 256, 0, s>>>(w, t);
-  k_bpe_reg<16, C><<<g2, 256, 0, s>>>(w, t);
-  k_bpe_reg<32, C><<<g2, 256, 0, s>>>(w, t);
+template <int N, bool C>
+static hipError_t launch_reg(const Work& w, const Tables& t, hipStream_t s) {
+  const uint32_t g = (w.n_tiles + RegClass<N>::K - 1) / RegClass<N>::K;
+  if (g) k_bpe_reg<N, C><<<g, 256, 0, s>>>(w, t);
   return hipGetLastError();
 }
 
-hipError_t launch_bpe(const Work& w, const Tables& t, hipStream_t s) {
-  if (t.n_at == 0) {
-    HIPCHK(t.compact ? launch_bpe_reg<true>(w, t, s) : launch_bpe_reg<false>(w, t, s));
-    k_bpe_generic<<<64, 256, 0, s>>>(w, t, w.mid_list, &w.counters[4]);  // pieces with dropped bytes
-  } else {
-    k_bpe_generic<<<w.grid1, 256, 0, s>>>(w, t, nullptr, nullptr);
+hipError_t launch_bpe_class(const Work& w, const Tables& t, int cls, hipStream_t s) {
+  if (t.n_at != 0) {  // every <= 32 B piece is in list0
+    if (cls == 0 && w.n_tiles) k_bpe_generic<false><<<(w.n_tiles + kTilesGeneric - 1) / kTilesGeneric, 256, 0, s>>>(w, t);
+    return hipGetLastError();
   }
-  return hipGetLastError();
+  switch (cls) {
+    case 0: return t.compact ? launch_reg<8, true>(w, t, s) : launch_reg<8, false>(w, t, s);
+    case 1: return t.compact ? launch_reg<16, true>(w, t, s) : launch_reg<16, false>(w, t, s);
+    case 2: return t.compact ? launch_reg<32, true>(w, t, s) : launch_reg<32, false>(w, t, s);
+    default:  // pieces with dropped bytes, found by the register passes
+      k_bpe_generic<true><<<64, 256, 0, s>>>(w, t);
+      return hipGetLastError();
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -769,10 +888,6 @@ __device__ __forceinline__ void merge_one(const Tables& t, const LongState<G>& L
   if (p != kNone) L.sRk(p, rank_of(t, L.Tok(p), nid, err));
 }
 
-// Wave-uniform values are moved to SGPRs with readfirstlane: the loop exits and the chain walk
-// then branch on scalars, so the wave can never split around the cross-lane reductions (a split
-// wave reduces over inactive lanes and never terminates).
-__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
 template <bool G>
 __device__ uint32_t bpe_wave(const Tables& t, const uint8_t* bytes, uint32_t n, const LongState<G>& L, uint32_t* out,
@@ -887,6 +1002,25 @@ __device__ uint32_t long_piece(const Tables& t, const uint8_t* bytes, uint32_t n
   return cnt;
 }
 
+// End of the piece starting at s: the next set bit of the piece-start bitmap, else n_bytes.
+// Wave-uniform (64 bitmap words per step).
+__device__ __forceinline__ uint32_t piece_end(const Work& w, uint32_t s) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t first = (s + 1) >> 5, sh = (s + 1) & 31;
+  for (uint32_t base = first; base < w.n_words; base += 64) {
+    const uint32_t idx = base + lane;
+    uint32_t v = idx < w.n_words ? w.pbits[idx] : 0u;
+    if (idx == first) v &= ~0u << sh;
+    const uint64_t m = __ballot(v != 0);
+    if (m) {
+      const uint32_t l = uni(__ffsll((unsigned long long)m) - 1);
+      const uint32_t vv = uni((uint32_t)__shfl((int)v, (int)l, 64));
+      return min(w.n_bytes, ((base + l) << 5) + (uint32_t)__builtin_ctz(vv));
+    }
+  }
+  return w.n_bytes;
+}
+
 // One wavefront per long piece, pieces dealt to waves by a static stride (no work-queue
 // atomics: every loop bound and index is a scalar, so the wave never splits).  GMEM selects the
 // tier: LDS for pieces up to kLdsPos positions, global memory beyond.
@@ -900,9 +1034,10 @@ __global__ __launch_bounds__(256) void k_bpe_long(Work w, Tables t) {
   uint32_t* err = &w.counters[2];
   const uint32_t B = w.n_bytes;
   for (uint32_t li = uni(blockIdx.x * (blockDim.x >> 6) + wid); li < n_long; li += n_waves) {
-    const uint32_t p = uni(w.long_list[li]);
-    const uint32_t s = uni(w.pstart[p]);
-    const uint32_t n = uni(w.pstart[p + 1]) - s;
+    const uint64_t e = w.long_list[li];
+    const uint32_t s = uni((uint32_t)e);
+    const uint32_t j = uni((uint32_t)(e >> 32));
+    const uint32_t n = uni(piece_end(w, s) - s);
     if (GMEM != (n > kLdsPos)) continue;
     const uint8_t* bytes = w.text + s;
     uint32_t* out = w.scratch + s;
@@ -915,7 +1050,11 @@ __global__ __launch_bounds__(256) void k_bpe_long(Work w, Tables t) {
       LongState<false> L{lds, lds + kLdsPos, lds + 2 * kLdsPos, lds + 3 * kLdsPos};
       cnt = long_piece<false>(t, bytes, n, L, out, err);
     }
-    if (lane == 0) w.pcnt[p] = cnt;
+    if (lane == 0) {
+      const uint32_t tile = s / kTile;
+      w.tcnt[(size_t)tile * kTileSlots + j] = cnt;
+      atomicAdd(&w.tile_tok[tile], cnt);
+    }
   }
 }
 
@@ -932,29 +1071,60 @@ hipError_t launch_bpe_long(const Work& w, const Tables& t, hipStream_t s) {
 }
 
 // ------------------------------------------------------------------------------------------
-// emission: ids[ptok[p] ...] = scratch[pstart[p] ...]; tok_off[d] = ptok[doc_piece[d]]
+// emission.  tile_tok is scanned to each tile's first id; one workgroup per tile scans its
+// pieces' counts in order (rounds of 256 pieces), copies each piece's ids from scratch to
+// ids[], and leaves each piece's first id (within the tile) in tcnt for k_tokoff.
 
-__global__ void k_emit(Work w, uint32_t* __restrict__ ids, uint64_t ids_cap) {
-  const uint32_t P = w.tile_cnt[w.n_tiles];
-  for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x) {
-    const uint32_t o = w.pcnt[p], c = w.pcnt[p + 1] - o;
-    const uint32_t* src = w.scratch + w.pstart[p];
-    for (uint32_t k = 0; k < c; k++)
-      if (o + k < ids_cap) ids[o + k] = src[k];  // the host reports CTOK_E_CAPACITY when short
+__global__ __launch_bounds__(256) void k_emit(Work w, uint32_t* __restrict__ ids, uint64_t ids_cap) {
+  __shared__ uint32_t s_scan[17];
+  const uint32_t tile = blockIdx.x, tid = threadIdx.x;
+  const uint32_t np = w.tile_np[tile];
+  const uint64_t base = w.tile_tok[tile];
+  uint32_t* tcnt = w.tcnt + (size_t)tile * kTileSlots;
+  const uint16_t* tpos = w.tpos + (size_t)tile * kTileSlots;
+  const uint32_t* src0 = w.scratch + (size_t)tile * kTile;
+  uint32_t carry = 0;
+  for (uint32_t j0 = 0; j0 < np; j0 += 256) {
+    const uint32_t j = j0 + tid;
+    const bool act = j < np;
+    const uint32_t c = act ? tcnt[j] : 0u;
+    const uint32_t sl = act ? tpos[j] : 0u;
+    uint32_t total;
+    const uint32_t o = carry + block_excl_scan<uint32_t>(c, s_scan, &total);
+    if (act) {
+      tcnt[j] = o;
+      const uint32_t* src = src0 + sl;
+      const uint64_t dst = base + o;
+      for (uint32_t k = 0; k < c; k++)
+        if (dst + k < ids_cap) ids[dst + k] = src[k];  // the host reports CTOK_E_CAPACITY when short
+    }
+    carry += total;
   }
 }
 
+// tok_off[d] = first id of the piece that starts at doc_off[d] (every non-empty doc starts a
+// piece; an empty doc shares the next doc's start, or the end of the text)
 __global__ void k_tokoff(Work w, uint64_t* __restrict__ tok_off) {
   const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
   if (d > w.n_docs) return;
-  tok_off[d] = w.pcnt[w.doc_piece[d]];
+  const uint64_t x = w.doc_off[d];
+  uint64_t r;
+  if (x >= w.n_bytes) {
+    r = w.tile_tok[w.n_tiles];
+  } else {
+    const uint32_t g = (uint32_t)(x >> 6), b = (uint32_t)(x & 63);
+    const uint32_t tile = (uint32_t)(x / kTile);
+    uint32_t below = __popc(w.pbits[2 * g] & (b >= 32 ? ~0u : ((1u << b) - 1u)));
+    if (b > 32) below += __popc(w.pbits[2 * g + 1] & ((1u << (b - 32)) - 1u));
+    const uint32_t j = w.wpref[(size_t)tile * 64 + (g - tile * kTileWords)] + below;
+    r = (uint64_t)w.tile_tok[tile] + w.tcnt[(size_t)tile * kTileSlots + j];
+  }
+  tok_off[d] = r;
 }
 
 hipError_t launch_emit(const Work& w, uint32_t* ids, uint64_t ids_cap, uint64_t* tok_off, hipStream_t s) {
-  HIPCHK(scan_u32(w.pcnt, w.pcnt, (uint64_t)w.n_bytes, &w.tile_cnt[w.n_tiles], w.scan_tmp, w.scan_tmp_cap, s));
-  uint32_t grid = (w.n_bytes / 4 + 255) / 256;
-  grid = grid < 1 ? 1 : grid > 8192 ? 8192 : grid;
-  k_emit<<<grid, 256, 0, s>>>(w, ids, ids_cap);
+  HIPCHK(scan_u32(w.tile_tok, w.tile_tok, (uint64_t)w.n_tiles, nullptr, w.scan_tmp, w.scan_tmp_cap, s));
+  if (w.n_tiles) k_emit<<<w.n_tiles, 256, 0, s>>>(w, ids, ids_cap);
   k_tokoff<<<(w.n_docs + 1 + 255) / 256, 256, 0, s>>>(w, tok_off);
   return hipGetLastError();
 }

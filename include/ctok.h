@@ -70,14 +70,17 @@ typedef struct ctok_exec {
 typedef struct ctok_stats {
   double ms_total;        /* wall time of the call (host clock)                        */
   double ms_device;       /* first kernel start -> last kernel end (HIP events)        */
-  double ms_pretok;       /* normalise check + pre-tokenizer + piece list              */
-  double ms_bpe_short;    /* BPE merge kernel, pieces <= 32 bytes (thread per piece)   */
+  double ms_pretok;       /* normalise check + doc bitmap + pre-tokenizer/routing      */
+  double ms_bpe_short;    /* BPE merge kernels, pieces <= 32 bytes (thread per piece)  */
   double ms_bpe_long;     /* BPE merge kernels, longer pieces (wavefront per piece)    */
-  double ms_emit;         /* token-count scan + compaction                             */
+  double ms_emit;         /* tile token scan + id emission + tok_off                   */
   double ms_h2d, ms_d2h;  /* host-buffer copies (ctok_encode_batch only)               */
   uint64_t bytes_in;      /* raw UTF-8 bytes of the batch                              */
   uint64_t bytes_norm;    /* bytes after normalisation / prefix space                  */
   uint64_t docs, pieces, long_pieces, tokens, nfc_docs;
+  double ms_segment;      /* k_segment alone: piece starts + whole-piece probes/routing */
+  double ms_bpe8, ms_bpe16, ms_bpe32;  /* k_bpe_reg per length class (ms_bpe32 includes the
+                                          dropped-byte generic pass, normally empty)  */
 } ctok_stats;
 
 /* Upper bound on the ids of a batch whose docs total `n_bytes` bytes (ids <= 3*bytes + docs:

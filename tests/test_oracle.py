@@ -301,6 +301,54 @@ def test_gpu_bitparallel_segmentation_equals_regex():
         assert bitparallel_starts(text, ds) == want, docs
 
 
+@pytest.fixture(scope="module")
+def seg_lane_lib(tmp_path_factory):
+    """tools/seg_lane_check.cpp (the kernel's per-lane SWAR logic, csrc/seg_lane.h) built with g++."""
+    import ctypes
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    src = os.path.join(root, "complexity-tokenizer_amd", "tools", "seg_lane_check.cpp")
+    so = str(tmp_path_factory.mktemp("seg") / "libseglane.so")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", src, "-o", so], check=True)
+    lib = ctypes.CDLL(so)
+    lib.seg_lane_starts.restype = ctypes.c_int
+    lib.seg_lane_starts.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p, ctypes.c_void_p]
+    return lib
+
+
+def _lane_starts(lib, docs):
+    text = b"".join(d.encode() for d in docs)
+    ds = bytearray(len(text) + 1)
+    want, o = [], 0
+    for d in docs:
+        e = d.encode()
+        if e:
+            ds[o] = 1
+        want += [o + len(d[:m.start()].encode()) for m in ref_py.GPT2_PATTERN.finditer(d)]
+        o += len(e)
+    words = np.zeros((len(text) + 63) // 64 + 1, dtype=np.uint64)
+    assert lib.seg_lane_starts(text, len(text), bytes(ds), words.ctypes.data) == 0, "look-ahead word disagrees"
+    bits = np.unpackbits(words.view(np.uint8), bitorder="little")[: len(text)]
+    return np.nonzero(bits)[0].tolist(), want
+
+
+def test_gpu_swar_lane_segmentation_equals_regex(seg_lane_lib):
+    rng = random.Random(13)
+    for trial in range(400):
+        if trial == 0:
+            docs = edge_cases.EDGE
+        elif trial % 5 == 0:  # several tiles of short docs
+            docs = edge_cases.random_unicode_docs(rng.randint(50, 400), seed=rng.randint(0, 10 ** 9), max_len=60)
+        else:
+            docs = edge_cases.random_unicode_docs(rng.randint(1, 40), seed=rng.randint(0, 10 ** 9), max_len=40)
+        got, want = _lane_starts(seg_lane_lib, docs)
+        assert got == want, docs
+    text, off = corpus.corpus_c1()
+    docs = [d.decode() for d in corpus.unpack(text, off)]
+    got, want = _lane_starts(seg_lane_lib, docs)
+    assert got == want
+
+
 # ----------------------------------------------------------------- independent BPE cross-check
 
 def test_hf_tokenizers_agree_on_shared_domain(gpt2_path, gpt2_obj):
