@@ -25,6 +25,7 @@ constexpr int kTileWords = 62;
 constexpr int kTile = kTileWords * 64;  // 3968 bytes per pre-tokenizer tile (piece starts are tile-local)
 constexpr int kTileSlots = 4096;        // per-tile stride of the piece-indexed arrays (pieces <= kTile)
 constexpr int kSegWaves = 4;            // tiles (wavefronts) per k_segment workgroup
+constexpr int kSegUnroll = 4;           // pieces per lane per routing round in k_segment
 constexpr int kShortMax = 32;      // pieces up to this many bytes are merged thread-per-piece
 // Per-tile piece lists by length class: <= 8 B (whole-piece probe missed), 9..16 B, 17..32 B.
 // Capacities are the most pieces of that class that can start in one tile.

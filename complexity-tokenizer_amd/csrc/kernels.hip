@@ -22,6 +22,8 @@
 // classes {White_Space, L, N, other} (derivation in DESIGN.md), bit-parallel on 64-bit masks.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "ctok_internal.h"
 #include "seg_lane.h"
 
@@ -234,6 +236,17 @@ __device__ __forceinline__ uint32_t wave_append(uint32_t* counter, bool take) {
 }
 
 
+// Whole-piece table lookup given the first probed slot e (at h): the vocab id, or kNone.
+__device__ __forceinline__ uint32_t piece_probe(const Tables& t, uint4 e, uint32_t h, uint32_t lo, uint32_t hi,
+                                                uint32_t n) {
+  while (e.z != 0) {  // linear probing past the first slot (rare)
+    if (e.x == lo && e.y == hi && e.z == n) return e.w;
+    h = (h + 1) & t.piece_mask;
+    e = t.piece_tab[h];
+  }
+  return kNone;
+}
+
 // One wavefront per tile, kSegWaves tiles per workgroup, no workgroup barrier.  Lane l owns the
 // 64-byte word g0 - 1 + l: lane 0 is the previous tile's last word (context only), lanes 1..62
 // are the tile's words, lane 63 is the next tile's first word (look-ahead: where the tile's last
@@ -250,6 +263,7 @@ __global__ __launch_bounds__(64 * kSegWaves) void k_segment(Work w, Tables t) {
   __shared__ uint64_t s_st_all[kSegWaves][64];
   __shared__ uint32_t s_wpre_all[kSegWaves][64];
   __shared__ uint32_t s_cnt_all[kSegWaves][4];
+  __shared__ uint32_t s_text_all[kSegWaves][(kTileWords + 1) * 16 + 4];  // the tile + look-ahead word
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wid = uni(threadIdx.x >> 6);
   const uint32_t tile = uni(blockIdx.x * kSegWaves + wid);
@@ -295,6 +309,14 @@ __global__ __launch_bounds__(64 * kSegWaves) void k_segment(Work w, Tables t) {
     }
   }
   seg::Masks m = seg::ascii_masks(x);
+  uint32_t* s_text = s_text_all[wid];
+  if (!first) {  // the tile's bytes (and the look-ahead word) for the whole-piece probes
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+      *reinterpret_cast<uint4*>(s_text + (lane - 1) * 16 + 4 * k) = make_uint4(x[4 * k], x[4 * k + 1], x[4 * k + 2], x[4 * k + 3]);
+  } else {
+    s_text[(kTileWords + 1) * 16] = 0;
+  }
   if (m.NA) {  // non-ASCII code points: one class lookup per code point
     const uint32_t x0 = (uint32_t)(g * 64);
     uint64_t todo = m.NA;
@@ -363,88 +385,102 @@ __global__ __launch_bounds__(64 * kSegWaves) void k_segment(Work w, Tables t) {
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
-  // ---- C: thread per piece
+  // ---- C: thread per piece, kSegUnroll pieces per lane per round with their LDS lookups and
+  // table probes issued together (each round is one dependent global round trip)
   const bool generic = t.n_at != 0;  // added tokens can match inside pieces: no whole-piece shortcut
   uint32_t* tcnt = w.tcnt + (size_t)tile * kTileSlots;
   uint16_t* tpos = w.tpos + (size_t)tile * kTileSlots;
   const uint64_t trusted_end = (uint64_t)t0 + kTile + 62;  // the look-ahead's bits 0..61
   uint32_t hits = 0;
-  for (uint32_t j0 = 0; j0 < np; j0 += 64) {
-    const uint32_t j = j0 + lane;
-    const bool act = j < np;
-    uint32_t sl = 0, n = 0, cls = 4;  // 0..2 class lists, 3 long, 4 done (or inactive)
-    if (act) {
-      // word of piece j: the last wi with s_wpre[wi] <= j (s_wpre[62] = s_wpre[63] = np > j)
-      uint32_t lo = 0;
+  constexpr int U = kSegUnroll;
+  for (uint32_t j0 = 0; j0 < np; j0 += 64 * U) {
+    uint32_t sl[U], n[U], cls[U], plo[U], phi[U], h[U];
 #pragma unroll
-      for (uint32_t step = 32; step >= 1; step >>= 1)
-        if (s_wpre[lo + step] <= j) lo += step;
-      const uint64_t xw = s_st[lo];
-      const uint32_t bit = select_bit(xw, j - s_wpre[lo]);
-      sl = lo * 64 + bit;
-      // end: the next start (this word, a later word, or the look-ahead word)
-      const uint64_t rest = bit == 63 ? 0ull : (xw >> (bit + 1));
-      int64_t el = -1;
-      if (rest) {
-        el = sl + 1 + __builtin_ctzll(rest);
-      } else {
-        for (uint32_t v = lo + 1; v <= kTileWords; v++) {
-          const uint64_t y = s_st[v];
-          if (y) { el = v * 64 + __builtin_ctzll(y); break; }
+    for (int u = 0; u < U; u++) {
+      const uint32_t j = j0 + 64 * u + lane;
+      sl[u] = 0;
+      n[u] = 0;
+      cls[u] = 4;  // 0..2 class lists, 3 long, 4 done (or inactive), 5 probe
+      if (j < np) {
+        // word of piece j: the last wi with s_wpre[wi] <= j (s_wpre[62] = s_wpre[63] = np > j)
+        uint32_t lo = 0;
+#pragma unroll
+        for (uint32_t step = 32; step >= 1; step >>= 1)
+          if (s_wpre[lo + step] <= j) lo += step;
+        const uint64_t xw = s_st[lo];
+        const uint32_t bit = select_bit(xw, j - s_wpre[lo]);
+        sl[u] = lo * 64 + bit;
+        // end: the next start (this word, a later word, or the look-ahead word)
+        const uint64_t rest = bit == 63 ? 0ull : (xw >> (bit + 1));
+        int64_t el = -1;
+        if (rest) {
+          el = sl[u] + 1 + __builtin_ctzll(rest);
+        } else {
+          for (uint32_t v = lo + 1; v <= kTileWords; v++) {
+            const uint64_t y = s_st[v];
+            if (y) { el = v * 64 + __builtin_ctzll(y); break; }
+          }
+          if (el < 0 && (uint64_t)B <= trusted_end) el = (int64_t)B - t0;
         }
-        if (el < 0 && (uint64_t)B <= trusted_end) el = (int64_t)B - t0;
-      }
-      tpos[j] = (uint16_t)sl;
-      if (el < 0 || el - sl > kShortMax) {
-        cls = 3;
-      } else {
-        n = (uint32_t)(el - sl);
-        if (generic) cls = 0;
-        else if (n > 16) cls = 2;
-        else if (n > 8) cls = 1;
-        else {
-          // whole-piece probe: the piece's raw bytes as one self-encoding vocab token
-          uint32_t wv[2];
-          load_words<2>(w.text, t0 + sl, B, wv);
-          const uint32_t plo = n >= 4 ? wv[0] : wv[0] & ((1u << (8 * n)) - 1u);
-          const uint32_t phi = n >= 8 ? wv[1] : n <= 4 ? 0u : wv[1] & ((1u << (8 * (n - 4))) - 1u);
-          uint32_t h = piece_hash(plo, phi, n) & t.piece_mask;
-          uint32_t hit = kNone;
-          for (;;) {
-            const uint4 e = t.piece_tab[h];
-            if (e.z == 0) break;
-            if (e.x == plo && e.y == phi && e.z == n) { hit = e.w; break; }
-            h = (h + 1) & t.piece_mask;
-          }
-          if (hit != kNone) {
-            w.scratch[t0 + sl] = hit;
-            tcnt[j] = 1;
-            hits++;
-            cls = 4;
-          } else {
-            cls = 0;
-          }
+        tpos[j] = (uint16_t)sl[u];
+        if (el < 0 || el - sl[u] > kShortMax) {
+          cls[u] = 3;
+        } else {
+          n[u] = (uint32_t)(el - sl[u]);
+          cls[u] = generic ? 0 : n[u] > 16 ? 2 : n[u] > 8 ? 1 : 5;
         }
       }
+      // whole-piece probe key: the piece's raw bytes (from LDS), zero-padded to 8
+      const uint32_t a = sl[u] >> 2, sh = sl[u] & 3;
+      const uint32_t d0 = s_text[a], d1 = s_text[a + 1], d2 = s_text[a + 2];
+      const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh), w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+      const uint32_t nn = n[u];
+      plo[u] = nn >= 4 ? w0 : w0 & ((1u << (8 * nn)) - 1u);
+      phi[u] = nn >= 8 ? w1 : nn <= 4 ? 0u : w1 & ((1u << (8 * (nn - 4))) - 1u);
+      h[u] = piece_hash(plo[u], phi[u], nn) & t.piece_mask;
     }
-    const uint32_t e = list_entry(sl, j, n);
-    {
-      const uint32_t q = wave_append(&s_cnt[0], cls == 0);
-      if (cls == 0) w.list0[(size_t)tile * kCap0 + q] = e;
+    static_assert(U == 4, "the probes below are unrolled by hand");
+    // all first probes in flight together
+    const uint4 e0 = t.piece_tab[h[0]], e1 = t.piece_tab[h[1]], e2 = t.piece_tab[h[2]], e3 = t.piece_tab[h[3]];
+    const uint32_t hit0 = piece_probe(t, e0, h[0], plo[0], phi[0], n[0]);
+    const uint32_t hit1 = piece_probe(t, e1, h[1], plo[1], phi[1], n[1]);
+    const uint32_t hit2 = piece_probe(t, e2, h[2], plo[2], phi[2], n[2]);
+    const uint32_t hit3 = piece_probe(t, e3, h[3], plo[3], phi[3], n[3]);
+    const uint32_t hitv[U] = {hit0, hit1, hit2, hit3};
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      if (cls[u] != 5) continue;
+      if (hitv[u] != kNone) {
+        w.scratch[t0 + sl[u]] = hitv[u];
+        tcnt[j0 + 64 * u + lane] = 1;
+        hits++;
+        cls[u] = 4;
+      } else {
+        cls[u] = 0;
+      }
     }
-    if (!generic) {
-      const uint32_t q1 = wave_append(&s_cnt[1], cls == 1);
-      if (cls == 1) w.list1[(size_t)tile * kCap1 + q1] = e;
-      const uint32_t q2 = wave_append(&s_cnt[2], cls == 2);
-      if (cls == 2) w.list2[(size_t)tile * kCap2 + q2] = e;
-    }
-    const uint64_t lm = __ballot(cls == 3);
-    if (lm) {  // rare: one global atomic per wave
-      const uint32_t leader = __ffsll((unsigned long long)lm) - 1;
-      uint32_t b = 0;
-      if (lane == leader) b = atomicAdd(&w.counters[0], (uint32_t)__popcll(lm));
-      b = (uint32_t)__shfl((int)b, (int)leader, 64);
-      if (cls == 3) w.long_list[b + __popcll(lm & lanemask_lt())] = (uint64_t)(t0 + sl) | ((uint64_t)j << 32);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint32_t j = j0 + 64 * u + lane;
+      const uint32_t e = list_entry(sl[u], j, n[u]);
+      {
+        const uint32_t q = wave_append(&s_cnt[0], cls[u] == 0);
+        if (cls[u] == 0) w.list0[(size_t)tile * kCap0 + q] = e;
+      }
+      if (!generic) {
+        const uint32_t q1 = wave_append(&s_cnt[1], cls[u] == 1);
+        if (cls[u] == 1) w.list1[(size_t)tile * kCap1 + q1] = e;
+        const uint32_t q2 = wave_append(&s_cnt[2], cls[u] == 2);
+        if (cls[u] == 2) w.list2[(size_t)tile * kCap2 + q2] = e;
+      }
+      const uint64_t lm = __ballot(cls[u] == 3);
+      if (lm) {  // rare: one global atomic per wave
+        const uint32_t leader = __ffsll((unsigned long long)lm) - 1;
+        uint32_t b = 0;
+        if (lane == leader) b = atomicAdd(&w.counters[0], (uint32_t)__popcll(lm));
+        b = (uint32_t)__shfl((int)b, (int)leader, 64);
+        if (cls[u] == 3) w.long_list[b + __popcll(lm & lanemask_lt())] = (uint64_t)(t0 + sl[u]) | ((uint64_t)j << 32);
+      }
     }
   }
 #pragma unroll
@@ -743,40 +779,39 @@ __global__ __launch_bounds__(256) void k_bpe_reg(Work w, Tables t) {
     }
     rk[N - 1] = kNoRank;
     uint32_t m = n;
+    // Branch-free over the N slots (selects only): the lowest (rank, position) pair is merged,
+    // the slots right of it shift left by one, the two new pairs' ranks are probed.
     for (;;) {
-      uint32_t best = kNoRank, bi = 0;
+      uint32_t key = ~0u;  // rank << 5 | position: one v_min per slot (ranks < 2^22)
 #pragma unroll
-      for (int k = 0; k < N - 1; k++)
-        if (rk[k] < best) { best = rk[k]; bi = (uint32_t)k; }
+      for (int k = 0; k < N - 1; k++) key = min(key, (rk[k] << 5) | (uint32_t)k);
+      const uint32_t best = key >> 5, bi = key & 31u;
       if (best == kNoRank) break;
       const uint32_t nid = COMPACT ? best : t.rank_newid[best];
       uint32_t L = 0, R = 0;
 #pragma unroll
       for (int k = 0; k < N; k++) {
-        if ((uint32_t)k + 1 == bi) L = tk[k];
-        if ((uint32_t)k == bi + 2) R = tk[k];
+        L = ((uint32_t)k + 1 == bi) ? tk[k] : L;
+        R = ((uint32_t)k == bi + 2) ? tk[k] : R;
       }
       const bool has_l = bi > 0, has_r = bi + 2 < m;
       const uint32_t hl = mhash(L, nid) & t.merge_mask, hr = mhash(nid, R) & t.merge_mask;
       const uint64_t el0 = t.merge_tab[hl];  // both new pairs probe in parallel, unconditionally
       const uint64_t er0 = t.merge_tab[hr];
-      const uint64_t el = has_l ? el0 : kEmpty;
-      const uint64_t er = has_r ? er0 : kEmpty;
 #pragma unroll
       for (int k = 0; k < N; k++) {  // ascending: tk[k+1] is read before it is overwritten
         const uint32_t nxt_t = k + 1 < N ? tk[k + 1] : kDead;
         const uint32_t nxt_r = k + 1 < N ? rk[k + 1] : kNoRank;
-        if ((uint32_t)k == bi) tk[k] = nid;
-        else if ((uint32_t)k > bi) { tk[k] = nxt_t; rk[k] = nxt_r; }
+        const bool gt = (uint32_t)k > bi;
+        tk[k] = gt ? nxt_t : ((uint32_t)k == bi ? nid : tk[k]);
+        rk[k] = gt ? nxt_r : rk[k];
       }
       m--;
-      const uint32_t rl = has_l ? resolve_rank(t, pair_key(L, nid), hl, el, err) : kNoRank;
-      const uint32_t rr = has_r ? resolve_rank(t, pair_key(nid, R), hr, er, err) : kNoRank;
+      const uint32_t rl = has_l ? resolve_rank(t, pair_key(L, nid), hl, el0, err) : kNoRank;
+      const uint32_t rr = has_r ? resolve_rank(t, pair_key(nid, R), hr, er0, err) : kNoRank;
 #pragma unroll
-      for (int k = 0; k < N; k++) {
-        if ((uint32_t)k + 1 == bi) rk[k] = rl;
-        if ((uint32_t)k == bi) rk[k] = rr;
-      }
+      for (int k = 0; k < N - 1; k++)
+        rk[k] = ((uint32_t)k + 1 == bi) ? rl : (((uint32_t)k == bi) ? rr : rk[k]);
     }
     uint32_t* out = w.scratch + s;
 #pragma unroll
@@ -1072,33 +1107,61 @@ hipError_t launch_bpe_long(const Work& w, const Tables& t, hipStream_t s) {
 
 // ------------------------------------------------------------------------------------------
 // emission.  tile_tok is scanned to each tile's first id; one workgroup per tile scans its
-// pieces' counts in order (rounds of 256 pieces), copies each piece's ids from scratch to
-// ids[], and leaves each piece's first id (within the tile) in tcnt for k_tokoff.
+// pieces' counts (blocked: 16 consecutive pieces per thread), copies each piece's ids from
+// scratch to ids[] (interleaved: coalesced writes), and leaves each piece's first id (within
+// the tile) in tcnt for k_tokoff.
 
 __global__ __launch_bounds__(256) void k_emit(Work w, uint32_t* __restrict__ ids, uint64_t ids_cap) {
   __shared__ uint32_t s_scan[17];
+  __shared__ uint32_t s_off[kTileSlots + 1];
   const uint32_t tile = blockIdx.x, tid = threadIdx.x;
   const uint32_t np = w.tile_np[tile];
   const uint64_t base = w.tile_tok[tile];
   uint32_t* tcnt = w.tcnt + (size_t)tile * kTileSlots;
   const uint16_t* tpos = w.tpos + (size_t)tile * kTileSlots;
   const uint32_t* src0 = w.scratch + (size_t)tile * kTile;
-  uint32_t carry = 0;
-  for (uint32_t j0 = 0; j0 < np; j0 += 256) {
-    const uint32_t j = j0 + tid;
-    const bool act = j < np;
-    const uint32_t c = act ? tcnt[j] : 0u;
-    const uint32_t sl = act ? tpos[j] : 0u;
-    uint32_t total;
-    const uint32_t o = carry + block_excl_scan<uint32_t>(c, s_scan, &total);
-    if (act) {
-      tcnt[j] = o;
-      const uint32_t* src = src0 + sl;
-      const uint64_t dst = base + o;
-      for (uint32_t k = 0; k < c; k++)
-        if (dst + k < ids_cap) ids[dst + k] = src[k];  // the host reports CTOK_E_CAPACITY when short
+  // 1. thread tid scans pieces [16 tid, 16 tid + 16): four 16-byte loads, one workgroup scan
+  constexpr int PER = kTileSlots / 256;
+  const uint32_t jb = tid * PER;
+  uint32_t c[PER];
+  if (jb < np) {
+#pragma unroll
+    for (int k = 0; k < PER / 4; k++) {
+      const uint4 v = reinterpret_cast<const uint4*>(tcnt + jb)[k];
+      c[4 * k] = v.x; c[4 * k + 1] = v.y; c[4 * k + 2] = v.z; c[4 * k + 3] = v.w;
     }
-    carry += total;
+  }
+  uint32_t sum = 0;
+#pragma unroll
+  for (int k = 0; k < PER; k++) {
+    c[k] = jb + k < np ? c[k] : 0u;
+    sum += c[k];
+  }
+  uint32_t total;
+  uint32_t o = block_excl_scan<uint32_t>(sum, s_scan, &total);
+  uint32_t pre[PER];
+#pragma unroll
+  for (int k = 0; k < PER; k++) {
+    pre[k] = o;
+    s_off[jb + k] = o;
+    o += c[k];
+  }
+  if (tid == 0) s_off[np] = total;
+  if (jb < np) {  // each piece's first id within the tile, for k_tokoff
+#pragma unroll
+    for (int k = 0; k < PER / 4; k++)
+      reinterpret_cast<uint4*>(tcnt + jb)[k] = make_uint4(pre[4 * k], pre[4 * k + 1], pre[4 * k + 2], pre[4 * k + 3]);
+  }
+  __syncthreads();
+  // 2. copy, piece j = tid + 256 k: consecutive lanes write consecutive ids
+  for (uint32_t j = tid; j < np; j += 256) {
+    const uint32_t oj = s_off[j], cj = s_off[j + 1] - oj;
+    const uint32_t* src = src0 + tpos[j];
+    const uint64_t dst = base + oj;
+    const uint32_t v0 = src[0];  // every piece has >= 1 id unless all its bytes were dropped
+    if (cj > 0 && dst < ids_cap) ids[dst] = v0;
+    for (uint32_t k = 1; k < cj; k++)
+      if (dst + k < ids_cap) ids[dst + k] = src[k];  // the host reports CTOK_E_CAPACITY when short
   }
 }
 
