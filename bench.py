@@ -5,8 +5,8 @@ Metric (BASELINE.json): "MB/s raw UTF-8 encoded (encode_batch), 50k ByteLevel BP
 Workload per GPU = config C2 (BASELINE.json configs[1]): 1,000,000 synthetic English-like ASCII
 docs of 96-160 bytes (~128 MB), GPT-2-shaped 50,257-token ByteLevel BPE (synthetic merges, no
 network).  A step = one `ctok_encode_batch_device` call over the whole batch, inputs already
-resident in HBM (pre-tokenize + BPE + compaction + token offsets, ending with the host reading
-the token count).  N > 1: one process per GPU (torch.distributed.run), every rank encodes its own
+resident in HBM (pre-tokenize + routing, BPE merge passes, id emission + token offsets, ending
+with the host reading the token count).  N > 1: one process per GPU (torch.distributed.run), every rank encodes its own
 1M-doc shard (seed 2 + 1000*rank): weak scaling, no data-path collective (gloo only for the
 barrier and the max-over-ranks timing).
 
@@ -148,11 +148,20 @@ def main():
 
     st = stats[-1]
     P, T, B, D = st["pieces"], st["tokens"], st["bytes_norm"], st["docs"]
-    # dominant kernel: k_bpe (thread-per-piece merge).  Algorithmic bytes per launch:
-    # text bytes it reads (B) + pstart reads (4(P+1)) + pcnt writes (4P) + id writes (4T).
-    ms_bpe = avg("ms_bpe_short")
-    alg_bpe = B + 4 * (P + 1) + 4 * P + 4 * T
-    ach = alg_bpe / (ms_bpe * 1e-3) / 1e9
+    # Per-kernel rooflines (HIP events on the encode stream, averaged over the timed steps).
+    # Algorithmic bytes per launch (DESIGN.md "Measurement"):
+    #   k_segment:      text read (B) + doc-start bitmap read (B/8) + piece-start bitmap written (B/8)
+    #   k_bpe_lds<N>:   text bytes of the pieces of its length class + 4 B per id it writes
+    cb, ci = st["class_bytes"], st["class_ids"]
+    kernels = {
+        "k_segment": (avg("ms_segment"), 1.25 * B),
+        "k_bpe_lds<8>": (avg("ms_bpe8"), cb[0] + 4 * ci[0]),
+        "k_bpe_lds<16>": (avg("ms_bpe16"), cb[1] + 4 * ci[1]),
+        "k_bpe_lds<32>": (avg("ms_bpe32"), cb[2] + 4 * ci[2]),
+    }
+    dom = max(kernels, key=lambda k: kernels[k][0])
+    ms_dom, alg_dom = kernels[dom]
+    ach = alg_dom / (ms_dom * 1e-3) / 1e9
     # whole pipeline: B_alg = sum L + 4 sum T + 16 (D+1)
     b_alg = B + 4 * T + 16 * (D + 1)
     ms_dev = avg("ms_device")
@@ -162,10 +171,10 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             threads = min(16, os.cpu_count() or 1)
             cpu = cpu_baseline(tok_path, text, off, args.cpu_seconds, threads)
-        traffic = None
-        tr_path = os.path.join(ROOT, "profiles", "r01_pmc_k_bpe.json")
+        traffic = None  # HBM bytes per launch of the dominant kernel from the committed PMC passes
+        tr_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(tr_path):
-            traffic = json.load(open(tr_path)).get("hbm_bytes_per_launch")
+            traffic = json.load(open(tr_path)).get("hbm_bytes_per_launch", {}).get(dom)
         ms_step = elapsed_max / args.steps * 1e3
         out = {
             "metric": METRIC,
@@ -184,11 +193,13 @@ def main():
                                    "ByteLevel BPE" % (n_docs, n_bytes / 1e6),
                        "docs_per_gpu": n_docs, "bytes_per_gpu": n_bytes, "tokens_per_gpu": int(T),
                        "parallelism": "doc-sharded x%d, no collectives" % world},
-            "roofline": {"bound": "hbm", "kernel": "k_bpe", "achieved": round(ach, 2), "peak": HBM_PEAK_GBPS,
+            "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(ach, 2), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 5), "traffic": traffic,
-                         "alg_bytes_per_launch": int(alg_bpe), "ms_per_launch": round(ms_bpe, 4)},
+                         "alg_bytes_per_launch": int(alg_dom), "ms_per_launch": round(ms_dom, 4),
+                         "kernels": {k: {"ms": round(v[0], 4), "alg_bytes": int(v[1]),
+                                         "GBps": round(v[1] / (v[0] * 1e-3) / 1e9, 2)} for k, v in kernels.items()}},
             "pipeline": {"ms_device": round(ms_dev, 4), "ms_pretok": round(avg("ms_pretok"), 4),
-                         "ms_bpe_short": round(ms_bpe, 4), "ms_bpe_long": round(avg("ms_bpe_long"), 4),
+                         "ms_bpe_short": round(avg("ms_bpe_short"), 4), "ms_bpe_long": round(avg("ms_bpe_long"), 4),
                          "ms_emit": round(avg("ms_emit"), 4), "ms_call": round(avg("ms_total"), 4),
                          "B_alg": int(b_alg), "achieved_GBps": round(b_alg / (ms_dev * 1e-3) / 1e9, 2),
                          "pieces": int(P), "long_pieces": int(st["long_pieces"]),

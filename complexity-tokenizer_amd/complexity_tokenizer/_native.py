@@ -41,10 +41,15 @@ class Stats(ctypes.Structure):
                 ("ms_d2h", ctypes.c_double), ("bytes_in", ctypes.c_uint64), ("bytes_norm", ctypes.c_uint64),
                 ("docs", ctypes.c_uint64), ("pieces", ctypes.c_uint64), ("long_pieces", ctypes.c_uint64),
                 ("tokens", ctypes.c_uint64), ("nfc_docs", ctypes.c_uint64), ("ms_segment", ctypes.c_double),
-                ("ms_bpe8", ctypes.c_double), ("ms_bpe16", ctypes.c_double), ("ms_bpe32", ctypes.c_double)]
+                ("ms_bpe8", ctypes.c_double), ("ms_bpe16", ctypes.c_double), ("ms_bpe32", ctypes.c_double),
+                ("class_bytes", ctypes.c_uint64 * 3), ("class_ids", ctypes.c_uint64 * 3)]
 
     def as_dict(self):
-        return {k: getattr(self, k) for k, _ in self._fields_}
+        d = {}
+        for k, _ in self._fields_:
+            v = getattr(self, k)
+            d[k] = list(v) if isinstance(v, ctypes.Array) else v
+        return d
 
 
 _p = ctypes.c_void_p

@@ -156,13 +156,14 @@ struct DevBuf {
 
 struct DeviceState {
   int device = -1;
+  uint32_t n_cus = 1;
   std::mutex mu;
   hipStream_t stream = nullptr;
   hipEvent_t ev[10] = {};
   hipEvent_t ev_sync = nullptr;   // spin-waited completion marker (no blocking-wait wakeup latency)
   uint64_t* host = nullptr;       // pinned host words for small device->host readbacks
   // tables
-  DevBuf<uint64_t> merge_tab;
+  DevBuf<uint64_t> merge_tab, lds_image;
   DevBuf<uint32_t> piece_tab;
   DevBuf<uint32_t> rank_newid;
   DevBuf<int32_t> byte2id;
@@ -207,6 +208,8 @@ struct ctok {
   // compiled tables
   std::vector<uint64_t> merge_tab;
   uint32_t merge_mask = 0;
+  std::vector<uint64_t> lds_image;  // kLdsImageBytes: hot table + Bloom filter
+  size_t hot_entries = 0;
   std::vector<uint32_t> piece_tab;  // 4 u32 per slot (see ctok_internal.h piece_hash)
   uint32_t piece_mask = 0;
   std::vector<uint32_t> rank_newid;
@@ -295,10 +298,6 @@ void parse_pre_tokenizer(const ctj::Value* v, std::vector<std::pair<char, bool>>
   }
 }
 
-uint32_t mhash_host(uint32_t a, uint32_t b) {
-  uint32_t h = a * 0x9E3779B1u ^ (b + 0x7F4A7C15u) * 0x85EBCA77u;
-  return h ^ (h >> 15);
-}
 
 void load(ctok* t, const char* buf, size_t len) {
   ctj::Value root;
@@ -374,12 +373,47 @@ void load(ctok* t, const char* buf, size_t len) {
     uint64_t val = kv.second;
     if (t->compact) val = kv.second < valid_new.size() ? valid_new[kv.second] : kPanicVal;
     uint64_t e = (val << 42) | ((uint64_t)a << kIdBits) | b;
-    uint32_t h = mhash_host(a, b) & t->merge_mask;
+    uint32_t h = mhash(a, b) & t->merge_mask;
     while (t->merge_tab[h] != kEmpty) h = (h + 1) & t->merge_mask;
     t->merge_tab[h] = e;
   }
   for (uint32_t id : valid_new)
     if (id > kMaxId) throw_err(CTOK_E_UNSUPPORTED, "token ids above 2^21-2 are not supported by the device merge table");
+  // LDS image: hot table filled greedily in rank order (a pair whose two buckets are full stays
+  // global-only), Bloom filter over every entry (including the ones whose lookup panics)
+  {
+    t->lds_image.assign(kLdsImageBytes / 8, 0);
+    uint64_t* hot = t->lds_image.data();
+    std::fill(hot, hot + kHotU64, kEmpty);
+    uint32_t* bloom = reinterpret_cast<uint32_t*>(hot + kHotU64);
+    std::vector<std::pair<uint32_t, uint64_t>> by_rank;  // (rank, entry)
+    by_rank.reserve(ranks.size());
+    for (uint64_t e : t->merge_tab) {
+      if (e == kEmpty) continue;
+      const uint32_t a = (uint32_t)((e >> kIdBits) & ((1u << kIdBits) - 1)), b = (uint32_t)(e & ((1u << kIdBits) - 1));
+      const uint32_t h1 = mhash(a, b), h2 = mhash2(a, b);
+      const uint32_t b1 = (h1 >> 12) & (kBloomBits - 1), b2 = (h2 >> 12) & (kBloomBits - 1);
+      bloom[b1 >> 5] |= 1u << (b1 & 31);
+      bloom[b2 >> 5] |= 1u << (b2 & 31);
+      const uint32_t r = ranks.at(((uint64_t)a << 32) | b);
+      if (r < valid_new.size()) by_rank.push_back({r, e});  // never cache an entry that panics
+    }
+    std::sort(by_rank.begin(), by_rank.end());
+    size_t placed = 0;
+    if (!getenv("CTOK_NO_HOT_TABLE")) {
+      for (const auto& re : by_rank) {
+        const uint64_t e = re.second;
+        const uint32_t a = (uint32_t)((e >> kIdBits) & ((1u << kIdBits) - 1)), b = (uint32_t)(e & ((1u << kIdBits) - 1));
+        const uint32_t c1 = mhash(a, b) & (kHotBuckets - 1), c2 = mhash2(a, b) & (kHotBuckets - 1);
+        uint64_t* slot = nullptr;
+        for (uint32_t c : {c1, c2})
+          for (int k = 0; k < 2 && !slot; k++)
+            if (hot[2 * c + k] == kEmpty) slot = &hot[2 * c + k];
+        if (slot) { *slot = e; placed++; }
+      }
+    }
+    t->hot_entries = placed;
+  }
   // rank monotonicity ("proper"): every merge consuming z ranks after every merge producing z
   {
     std::unordered_map<uint32_t, uint32_t> maxprod, mincons;
@@ -542,11 +576,17 @@ DeviceState* device_state(ctok* t, int device) {
   auto ds = std::make_unique<DeviceState>();
   ds->device = device;
   HIPTRY(hipStreamCreateWithFlags(&ds->stream, hipStreamNonBlocking));
+  {
+    int cus = 0;
+    HIPTRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+    ds->n_cus = cus > 0 ? (uint32_t)cus : 1u;
+  }
   for (auto& e : ds->ev) HIPTRY(hipEventCreate(&e));
   HIPTRY(hipEventCreateWithFlags(&ds->ev_sync, hipEventDisableTiming));
   HIPTRY(hipHostMalloc((void**)&ds->host, 4096, hipHostMallocDefault));
   hipStream_t s = ds->stream;
   upload(ds->merge_tab, t->merge_tab.data(), t->merge_tab.size(), s);
+  upload(ds->lds_image, t->lds_image.data(), t->lds_image.size(), s);
   upload(ds->rank_newid, t->rank_newid.data(), t->rank_newid.size(), s);
   upload(ds->piece_tab, t->piece_tab.data(), t->piece_tab.size(), s);
   upload(ds->byte2id, t->byte2id, 256, s);
@@ -568,6 +608,7 @@ DeviceState* device_state(ctok* t, int device) {
   Tables& tb = ds->t;
   tb.merge_tab = ds->merge_tab.p;
   tb.merge_mask = t->merge_mask;
+  tb.lds_image = (const uint4*)ds->lds_image.p;
   tb.piece_tab = (const uint4*)ds->piece_tab.p;
   tb.piece_mask = t->piece_mask;
   tb.rank_newid = ds->rank_newid.p;
@@ -638,8 +679,8 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   const Tables& tb = ds->t;
   if (timing) HIPTRY(hipEventRecord(ds->ev[0], s));
 
-  ds->counters.ensure(8);
-  HIPTRY(hipMemsetAsync(ds->counters.p, 0, 8 * 4, s));
+  ds->counters.ensure(16);
+  HIPTRY(hipMemsetAsync(ds->counters.p, 0, 16 * 4, s));
   const uint8_t* text = d_text;
   const uint64_t* off = d_off;
   uint64_t B = n_bytes;
@@ -685,6 +726,7 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   w.n_docs = (uint32_t)n_docs;
   w.n_words = (uint32_t)((B + 31) / 32);
   w.n_tiles = (uint32_t)((B + kTile - 1) / kTile);
+  w.n_cus = ds->n_cus;
   const size_t nt = w.n_tiles;
   ds->docbits.ensure(w.n_words + 8);
   ds->pbits.ensure(w.n_words + 8);
@@ -742,11 +784,11 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   if (timing) HIPTRY(hipEventRecord(ds->ev[6], s));
   if (st && w.n_tiles) STEP("count", launch_count_pieces(w, s));
   HIPTRY(hipMemcpyAsync(ds->host, d_tok_off + n_docs, 8, hipMemcpyDeviceToHost, s));
-  HIPTRY(hipMemcpyAsync(ds->host + 1, ds->counters.p, 24, hipMemcpyDeviceToHost, s));
+  HIPTRY(hipMemcpyAsync(ds->host + 1, ds->counters.p, 48, hipMemcpyDeviceToHost, s));
   spin_sync(ds, s);
   const uint64_t ntok = ((volatile uint64_t*)ds->host)[0];
-  uint32_t cnt[6];
-  for (int i = 0; i < 6; i++) cnt[i] = ((volatile uint32_t*)(ds->host + 1))[i];
+  uint32_t cnt[12];
+  for (int i = 0; i < 12; i++) cnt[i] = ((volatile uint32_t*)(ds->host + 1))[i];
   const uint32_t P = cnt[5];
   if (cnt[2] & kErrPanic)
     throw_err(CTOK_E_PANIC, "index out of bounds: a merge rank points past the list of valid merges (reference src/bpe.rs:141 panics)");
@@ -759,6 +801,10 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
     st->long_pieces = cnt[0];
     st->tokens = ntok;
     st->nfc_docs = nfc_docs;
+    for (int c = 0; c < 3; c++) {
+      st->class_bytes[c] = cnt[6 + 2 * c];
+      st->class_ids[c] = cnt[7 + 2 * c];
+    }
     if (timing) {
       auto el = [&](int i, int j) {
         float v = 0;

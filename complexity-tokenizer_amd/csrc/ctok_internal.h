@@ -33,6 +33,30 @@ constexpr uint32_t kCap0 = kTile, kCap1 = (kTile + 8) / 9, kCap2 = (kTile + 16) 
 // List entry (u32): start within the tile [0,12), piece index within the tile [12,24), length [24,30).
 __host__ __device__ inline uint32_t list_entry(uint32_t sl, uint32_t j, uint32_t n) { return sl | (j << 12) | (n << 24); }
 
+// Merge-table hashes of a pair (a, b): mhash picks the global table slot (open addressing) and,
+// with mhash2, the two candidate buckets of the LDS hot table and the two Bloom-filter bits.
+__host__ __device__ inline uint32_t mhash(uint32_t a, uint32_t b) {
+  const uint32_t h = a * 0x9E3779B1u ^ (b + 0x7F4A7C15u) * 0x85EBCA77u;
+  return h ^ (h >> 15);
+}
+__host__ __device__ inline uint32_t mhash2(uint32_t a, uint32_t b) {
+  uint32_t h = (a + 0x632BE5ABu) * 0xC2B2AE3Du ^ b * 0x27D4EB2Fu;
+  h ^= h >> 13;
+  h *= 0x165667B1u;
+  return h ^ (h >> 16);
+}
+
+// LDS image for the merge passes (loaded once per workgroup): a hot table of the lowest-rank
+// mergeable pairs, kHotBuckets buckets of two merge-table entries, a pair in bucket
+// mhash & mask or mhash2 & mask; and a Bloom filter over every merge-table entry (bits
+// (mhash >> 12) and (mhash2 >> 12) mod kBloomBits).  A pair found in neither LDS structure goes
+// to the global table only when both Bloom bits are set.
+constexpr uint32_t kHotBuckets = 4096;                 // 64 KiB
+constexpr uint32_t kBloomBits = 1u << 18;              // 32 KiB
+constexpr uint32_t kHotU64 = 2 * kHotBuckets;
+constexpr uint32_t kBloomWords = kBloomBits / 32;
+constexpr uint32_t kLdsImageBytes = kHotU64 * 8 + kBloomWords * 4;
+
 // Whole-piece table: raw byte strings of <= 8 bytes whose BPE is exactly one token (checked at
 // load time by running the merge loop on every vocab entry).  Entry = {lo32, hi32, len, id} of
 // the zero-padded bytes; len == 0 marks an empty slot.
@@ -44,6 +68,7 @@ __host__ __device__ inline uint32_t piece_hash(uint32_t lo, uint32_t hi, uint32_
 struct Tables {            // device pointers, owned by the host runtime
   const uint64_t* merge_tab;
   uint32_t merge_mask;     // capacity - 1 (power of two)
+  const uint4* lds_image;  // hot table + Bloom filter (kLdsImageBytes), copied to LDS by the merge passes
   const uint4* piece_tab;  // whole-piece table (see piece_hash)
   uint32_t piece_mask;
   const uint32_t* rank_newid;
@@ -81,6 +106,7 @@ struct Work {              // device pointers, sized by the host for one call
   uint32_t* pbits;         // piece-start bitmap (u32 words), n_words + 8
   uint32_t n_words;
   uint32_t n_tiles;
+  uint32_t n_cus;          // compute units of the device (persistent merge-pass grid)
   uint16_t* wpref;         // [n_tiles * 64] pieces of the tile before each 64-byte word
   uint32_t* tile_np;       // [n_tiles] pieces starting in the tile
   uint32_t* tile_tok;      // [n_tiles + 1] tokens per tile, scanned in place to the tile's first id
@@ -93,7 +119,8 @@ struct Work {              // device pointers, sized by the host for one call
   uint32_t* scratch;       // [n_bytes] ids of the piece starting at byte s at scratch[s ..]
   uint64_t* long_list;     // pieces > kShortMax B (or of unknown length at a tile end): s | j << 32
   uint64_t* mid_list;      // pieces with dropped bytes for the generic kernel: s | j << 32 | n << 48
-  uint32_t* counters;      // [0] long count, [2] err, [3] nfc docs, [4] mid count, [5] pieces (stats)
+  uint32_t* counters;      // [0] long count, [2] err, [3] nfc docs, [4] mid count, [5] pieces (stats),
+                           // [6 + 2c], [7 + 2c]: bytes merged / ids produced by class pass c (stats)
   uint32_t* lw;            // long-piece workspace: 4 * n_bytes u32
   uint32_t* scan_tmp;      // scan partials
   uint64_t scan_tmp_cap;

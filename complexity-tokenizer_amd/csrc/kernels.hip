@@ -105,10 +105,6 @@ __device__ __forceinline__ int cls_of(uint32_t cp, const Tables& t) {
   return (w >> ((cp & 3) * 2)) & 3;
 }
 
-__device__ __forceinline__ uint32_t mhash(uint32_t a, uint32_t b) {
-  uint32_t h = a * 0x9E3779B1u ^ (b + 0x7F4A7C15u) * 0x85EBCA77u;
-  return h ^ (h >> 15);
-}
 
 // Merge-table value of an entry: the merge priority.  Compact tables (new ids strictly increasing
 // in rank, the usual layout) store the merged token id itself, so the minimum value is both the
@@ -713,120 +709,212 @@ __device__ __forceinline__ uint32_t resolve_rank(const Tables& t, uint64_t key, 
 
 __device__ __forceinline__ uint64_t pair_key(uint32_t a, uint32_t b) { return ((uint64_t)a << kIdBits) | b; }
 
-template <int N> struct RegClass;
-template <> struct RegClass<8> { static constexpr int cls = 0, K = 4; static constexpr uint32_t cap = kCap0; };
-template <> struct RegClass<16> { static constexpr int cls = 1, K = 16; static constexpr uint32_t cap = kCap1; };
-template <> struct RegClass<32> { static constexpr int cls = 2, K = 64; static constexpr uint32_t cap = kCap2; };
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(3))) uint64_t lds_u64;
+
+// The LDS image of the merge passes: hot table + Bloom filter (ctok_internal.h).
+struct PairLds {
+  const lds_u64* hot;  // bucket c = hot[2c], hot[2c + 1]
+  const lds_u32* bloom;
+};
+
+// Rank lookup, LDS stage: the pair's value from the hot table, else kNoRank; `global` is set
+// when the hot table missed and the Bloom filter cannot rule the pair out.
+__device__ __forceinline__ uint32_t rank_lds(const PairLds& P, uint32_t a, uint32_t b, uint32_t h1, uint32_t h2,
+                                             bool& global) {
+  const uint32_t c1 = 2 * (h1 & (kHotBuckets - 1)), c2 = 2 * (h2 & (kHotBuckets - 1));
+  const uint64_t x0 = P.hot[c1], x1 = P.hot[c1 + 1], y0 = P.hot[c2], y1 = P.hot[c2 + 1];
+  const uint32_t b1 = (h1 >> 12) & (kBloomBits - 1), b2 = (h2 >> 12) & (kBloomBits - 1);
+  const uint32_t f = (P.bloom[b1 >> 5] >> (b1 & 31)) & (P.bloom[b2 >> 5] >> (b2 & 31)) & 1u;
+  // entry = value << 42 | a << 21 | b: compare the 42-bit key as (lo 32, hi 10)
+  const uint32_t klo = (a << kIdBits) | b, khi = a >> (32 - kIdBits);
+  uint32_t v = kNoRank;
+  bool hit = false;
+  auto chk = [&](uint64_t e) {
+    const uint32_t lo = (uint32_t)e, hi = (uint32_t)(e >> 32);
+    const bool m = lo == klo && (hi & 0x3FFu) == khi;
+    v = m ? (hi >> 10) : v;
+    hit |= m;
+  };
+  chk(x0);
+  chk(x1);
+  chk(y0);
+  chk(y1);
+  global = !hit && f;
+  return v;
+}
+
+template <int N> struct LdsClass;
+template <> struct LdsClass<8> { static constexpr int cls = 0, threads = 1024; static constexpr uint32_t cap = kCap0; };
+template <> struct LdsClass<16> { static constexpr int cls = 1, threads = 1024; static constexpr uint32_t cap = kCap1; };
+template <> struct LdsClass<32> { static constexpr int cls = 2, threads = 512; static constexpr uint32_t cap = kCap2; };
 
 template <int N>
 __device__ __forceinline__ const uint32_t* class_list(const Work& w) {
   return N == 8 ? w.list0 : N == 16 ? w.list1 : w.list2;
 }
 
-// Merge pass over one length class (N = 8, 16, 32 slots).
+// Merge pass over one length class (N = 8, 16, 32 slots): a persistent grid, one workgroup per
+// CU holding the merge LDS image; workgroup b takes a contiguous range of tiles and walks its
+// class lists 64 tiles at a time (one concatenated list per chunk, see tile_share_init).
+// Thread per piece, tokens and pair ranks in registers (fully unrolled, compile-time slots).
 template <int N, bool COMPACT>
-__global__ __launch_bounds__(256) void k_bpe_reg(Work w, Tables t) {
-  using RC = RegClass<N>;
-  constexpr int K = RC::K;
+__global__ __launch_bounds__(LdsClass<N>::threads) void k_bpe_lds(Work w, Tables t, uint32_t tiles_per_block) {
+  using LC = LdsClass<N>;
+  constexpr uint32_t NT = LC::threads;
+  constexpr int K = 64;
+  extern __shared__ __attribute__((aligned(16))) uint4 s_img[];
   __shared__ int32_t s_b2id[256];
-  __shared__ uint32_t s_pre[K + 1], s_tsum[K];
+  __shared__ uint32_t s_pre[K + 1], s_tsum[K], s_stat[2];
   const uint32_t tid = threadIdx.x;
-  s_b2id[tid] = t.byte2id[tid];
+  if (tid < 2) s_stat[tid] = 0;
+  for (uint32_t i = tid; i < kLdsImageBytes / 16; i += NT) s_img[i] = t.lds_image[i];
+  for (uint32_t i = tid; i < 256; i += NT) s_b2id[i] = t.byte2id[i];
+  const PairLds P{(const lds_u64*)s_img, (const lds_u32*)(s_img + kHotBuckets)};
   uint32_t* err = &w.counters[2];
-  const uint32_t t0 = blockIdx.x * K;
-  const uint32_t E = tile_share_init<K>(w.tcls + (size_t)RC::cls * w.n_tiles, w.n_tiles, t0, s_pre, s_tsum);
   const uint32_t* list = class_list<N>(w);
-  for (uint32_t q = tid; q < E; q += 256) {
-    const uint32_t kt = tile_of<K>(s_pre, q);
-    const uint32_t tile = t0 + kt;
-    const uint32_t e = list[(size_t)tile * RC::cap + (q - s_pre[kt])];
-    const uint32_t s = tile * kTile + (e & 0xFFFu);
-    const uint32_t j = (e >> 12) & 0xFFFu;
-    const uint32_t n = e >> 24;
-    uint32_t tk[N], rk[N];
-    bool missing = false;
-    {
-      uint32_t wv[N / 4];
-      load_words<N / 4>(w.text, s, w.n_bytes, wv);
+  const uint32_t* counts = w.tcls + (size_t)LC::cls * w.n_tiles;
+  const uint32_t tb0 = blockIdx.x * tiles_per_block, tb1 = min(w.n_tiles, tb0 + tiles_per_block);
+  uint32_t st_bytes = 0, st_ids = 0;
+  __syncthreads();
+  for (uint32_t c0 = tb0; c0 < tb1; c0 += K) {
+    const uint32_t E = tile_share_init<K>(counts, tb1, c0, s_pre, s_tsum);
+    for (uint32_t q = tid; q < E; q += NT) {
+      const uint32_t kt = tile_of<K>(s_pre, q);
+      const uint32_t tile = c0 + kt;
+      const uint32_t e = list[(size_t)tile * LC::cap + (q - s_pre[kt])];
+      const uint32_t s = tile * kTile + (e & 0xFFFu);
+      const uint32_t j = (e >> 12) & 0xFFFu;
+      const uint32_t n = e >> 24;
+      uint32_t tk[N], rk[N];
+      bool missing = false;
+      {
+        uint32_t wv[N / 4];
+        load_words<N / 4>(w.text, s, w.n_bytes, wv);
 #pragma unroll
-      for (int k = 0; k < N; k++) {
-        const int32_t id = s_b2id[byte_of(wv[k >> 2], k)];
-        missing |= ((uint32_t)k < n) & (id < 0);
-        tk[k] = (uint32_t)id;
-      }
-    }
-    if (missing) {  // a byte char absent from the vocab is dropped: generic path
-      w.mid_list[atomicAdd(&w.counters[4], 1u)] = (uint64_t)s | ((uint64_t)j << 32) | ((uint64_t)n << 48);
-      continue;
-    }
-#pragma unroll
-    for (int k0 = 0; k0 < N - 1; k0 += 8) {  // first probes of 8 pairs in flight together (unconditional)
-      uint32_t hh[8];
-      uint64_t ee[8];
-#pragma unroll
-      for (int jj = 0; jj < 8; jj++) {
-        const int k = k0 + jj;
-        if (k < N - 1) {
-          hh[jj] = mhash(tk[k], tk[k + 1]) & t.merge_mask;
-          ee[jj] = t.merge_tab[hh[jj]];
+        for (int k = 0; k < N; k++) {
+          const int32_t id = s_b2id[byte_of(wv[k >> 2], k)];
+          missing |= ((uint32_t)k < n) & (id < 0);
+          tk[k] = (uint32_t)id;
         }
       }
-#pragma unroll
-      for (int jj = 0; jj < 8; jj++) {
-        const int k = k0 + jj;
-        if (k < N - 1) rk[k] = ((uint32_t)k + 1 < n) ? resolve_rank(t, pair_key(tk[k], tk[k + 1]), hh[jj], ee[jj], err) : kNoRank;
+      if (missing) {  // a byte char absent from the vocab is dropped: generic path
+        w.mid_list[atomicAdd(&w.counters[4], 1u)] = (uint64_t)s | ((uint64_t)j << 32) | ((uint64_t)n << 48);
+        continue;
       }
+      // initial pair ranks, four pairs at a time: LDS stage, then the global probes that remain
+      // (issued together before any is consumed)
+#pragma unroll
+      for (int k0 = 0; k0 < N - 1; k0 += 4) {
+        uint32_t h1[4];
+        bool g[4];
+        uint64_t ee[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          const int k = k0 + i;
+          if (k < N - 1) {
+            h1[i] = mhash(tk[k], tk[k + 1]);
+            rk[k] = rank_lds(P, tk[k], tk[k + 1], h1[i], mhash2(tk[k], tk[k + 1]), g[i]);
+            g[i] = g[i] && (uint32_t)k + 1 < n;
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+          if (k0 + i < N - 1 && g[i]) ee[i] = t.merge_tab[h1[i] & t.merge_mask];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          const int k = k0 + i;
+          if (k < N - 1) {
+            if (g[i]) rk[k] = resolve_rank(t, pair_key(tk[k], tk[k + 1]), h1[i] & t.merge_mask, ee[i], err);
+            rk[k] = (uint32_t)k + 1 < n ? rk[k] : kNoRank;
+          }
+        }
+      }
+      rk[N - 1] = kNoRank;
+      uint32_t m = n;
+      // Branch-free over the N slots (selects only): the lowest (rank, position) pair is merged,
+      // the slots right of it shift left by one, the two new pairs' ranks are looked up.
+      for (;;) {
+        uint32_t key = ~0u;  // rank << 5 | position: one v_min per slot (ranks < 2^22)
+#pragma unroll
+        for (int k = 0; k < N - 1; k++) key = min(key, (rk[k] << 5) | (uint32_t)k);
+        const uint32_t best = key >> 5, bi = key & 31u;
+        if (best == kNoRank) break;
+        const uint32_t nid = COMPACT ? best : t.rank_newid[best];
+        uint32_t L = 0, R = 0;
+#pragma unroll
+        for (int k = 0; k < N; k++) {
+          L = ((uint32_t)k + 1 == bi) ? tk[k] : L;
+          R = ((uint32_t)k == bi + 2) ? tk[k] : R;
+        }
+        const bool has_l = bi > 0, has_r = bi + 2 < m;
+        const uint32_t hl1 = mhash(L, nid), hr1 = mhash(nid, R);
+        bool gl, gr;
+        uint32_t rl = rank_lds(P, L, nid, hl1, mhash2(L, nid), gl);
+        uint32_t rr = rank_lds(P, nid, R, hr1, mhash2(nid, R), gr);
+        gl = gl && has_l;
+        gr = gr && has_r;
+        uint64_t el = 0, er = 0;
+        if (gl) el = t.merge_tab[hl1 & t.merge_mask];
+        if (gr) er = t.merge_tab[hr1 & t.merge_mask];
+#pragma unroll
+        for (int k = 0; k < N; k++) {  // ascending: tk[k+1] is read before it is overwritten
+          const uint32_t nxt_t = k + 1 < N ? tk[k + 1] : kDead;
+          const uint32_t nxt_r = k + 1 < N ? rk[k + 1] : kNoRank;
+          const bool gt = (uint32_t)k > bi;
+          tk[k] = gt ? nxt_t : ((uint32_t)k == bi ? nid : tk[k]);
+          rk[k] = gt ? nxt_r : rk[k];
+        }
+        m--;
+        if (gl) rl = resolve_rank(t, pair_key(L, nid), hl1 & t.merge_mask, el, err);
+        if (gr) rr = resolve_rank(t, pair_key(nid, R), hr1 & t.merge_mask, er, err);
+        rl = has_l ? rl : kNoRank;
+        rr = has_r ? rr : kNoRank;
+#pragma unroll
+        for (int k = 0; k < N - 1; k++)
+          rk[k] = ((uint32_t)k + 1 == bi) ? rl : (((uint32_t)k == bi) ? rr : rk[k]);
+      }
+      uint32_t* out = w.scratch + s;
+#pragma unroll
+      for (int k = 0; k < N; k++)
+        if ((uint32_t)k < m) out[k] = tk[k];
+      w.tcnt[(size_t)tile * kTileSlots + j] = m;
+      atomicAdd(&s_tsum[kt], m);
+      st_bytes += n;
+      st_ids += m;
     }
-    rk[N - 1] = kNoRank;
-    uint32_t m = n;
-    // Branch-free over the N slots (selects only): the lowest (rank, position) pair is merged,
-    // the slots right of it shift left by one, the two new pairs' ranks are probed.
-    for (;;) {
-      uint32_t key = ~0u;  // rank << 5 | position: one v_min per slot (ranks < 2^22)
-#pragma unroll
-      for (int k = 0; k < N - 1; k++) key = min(key, (rk[k] << 5) | (uint32_t)k);
-      const uint32_t best = key >> 5, bi = key & 31u;
-      if (best == kNoRank) break;
-      const uint32_t nid = COMPACT ? best : t.rank_newid[best];
-      uint32_t L = 0, R = 0;
-#pragma unroll
-      for (int k = 0; k < N; k++) {
-        L = ((uint32_t)k + 1 == bi) ? tk[k] : L;
-        R = ((uint32_t)k == bi + 2) ? tk[k] : R;
-      }
-      const bool has_l = bi > 0, has_r = bi + 2 < m;
-      const uint32_t hl = mhash(L, nid) & t.merge_mask, hr = mhash(nid, R) & t.merge_mask;
-      const uint64_t el0 = t.merge_tab[hl];  // both new pairs probe in parallel, unconditionally
-      const uint64_t er0 = t.merge_tab[hr];
-#pragma unroll
-      for (int k = 0; k < N; k++) {  // ascending: tk[k+1] is read before it is overwritten
-        const uint32_t nxt_t = k + 1 < N ? tk[k + 1] : kDead;
-        const uint32_t nxt_r = k + 1 < N ? rk[k + 1] : kNoRank;
-        const bool gt = (uint32_t)k > bi;
-        tk[k] = gt ? nxt_t : ((uint32_t)k == bi ? nid : tk[k]);
-        rk[k] = gt ? nxt_r : rk[k];
-      }
-      m--;
-      const uint32_t rl = has_l ? resolve_rank(t, pair_key(L, nid), hl, el0, err) : kNoRank;
-      const uint32_t rr = has_r ? resolve_rank(t, pair_key(nid, R), hr, er0, err) : kNoRank;
-#pragma unroll
-      for (int k = 0; k < N - 1; k++)
-        rk[k] = ((uint32_t)k + 1 == bi) ? rl : (((uint32_t)k == bi) ? rr : rk[k]);
-    }
-    uint32_t* out = w.scratch + s;
-#pragma unroll
-    for (int k = 0; k < N; k++)
-      if ((uint32_t)k < m) out[k] = tk[k];
-    w.tcnt[(size_t)tile * kTileSlots + j] = m;
-    atomicAdd(&s_tsum[kt], m);
+    tile_share_flush<K>(w, c0, s_tsum);
+    __syncthreads();
   }
-  tile_share_flush<K>(w, t0, s_tsum);
+  // statistics: bytes merged and ids produced by this pass (algorithmic bytes for the roofline)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    st_bytes += (uint32_t)__shfl_xor((int)st_bytes, o, 64);
+    st_ids += (uint32_t)__shfl_xor((int)st_ids, o, 64);
+  }
+  if ((tid & 63) == 0) {
+    atomicAdd(&s_stat[0], st_bytes);
+    atomicAdd(&s_stat[1], st_ids);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    atomicAdd(&w.counters[6 + 2 * LC::cls], s_stat[0]);
+    atomicAdd(&w.counters[7 + 2 * LC::cls], s_stat[1]);
+  }
 }
 
 template <int N, bool C>
-static hipError_t launch_reg(const Work& w, const Tables& t, hipStream_t s) {
-  const uint32_t g = (w.n_tiles + RegClass<N>::K - 1) / RegClass<N>::K;
-  if (g) k_bpe_reg<N, C><<<g, 256, 0, s>>>(w, t);
+static hipError_t launch_lds(const Work& w, const Tables& t, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    HIPCHK(hipFuncSetAttribute((const void*)k_bpe_lds<N, C>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)kLdsImageBytes));
+    attr = true;
+  }
+  if (!w.n_tiles) return hipSuccess;
+  const uint32_t grid = min(w.n_tiles, w.n_cus);
+  const uint32_t per = (w.n_tiles + grid - 1) / grid;
+  k_bpe_lds<N, C><<<(w.n_tiles + per - 1) / per, LdsClass<N>::threads, kLdsImageBytes, s>>>(w, t, per);
   return hipGetLastError();
 }
 
@@ -836,10 +924,10 @@ hipError_t launch_bpe_class(const Work& w, const Tables& t, int cls, hipStream_t
     return hipGetLastError();
   }
   switch (cls) {
-    case 0: return t.compact ? launch_reg<8, true>(w, t, s) : launch_reg<8, false>(w, t, s);
-    case 1: return t.compact ? launch_reg<16, true>(w, t, s) : launch_reg<16, false>(w, t, s);
-    case 2: return t.compact ? launch_reg<32, true>(w, t, s) : launch_reg<32, false>(w, t, s);
-    default:  // pieces with dropped bytes, found by the register passes
+    case 0: return t.compact ? launch_lds<8, true>(w, t, s) : launch_lds<8, false>(w, t, s);
+    case 1: return t.compact ? launch_lds<16, true>(w, t, s) : launch_lds<16, false>(w, t, s);
+    case 2: return t.compact ? launch_lds<32, true>(w, t, s) : launch_lds<32, false>(w, t, s);
+    default:  // pieces with dropped bytes, found by the merge passes
       k_bpe_generic<true><<<64, 256, 0, s>>>(w, t);
       return hipGetLastError();
   }
@@ -858,8 +946,6 @@ hipError_t launch_bpe_class(const Work& w, const Tables& t, int cls, hipStream_t
 // wave see each other's stores between rounds (the vector L1 does not).  LDS = arrays in the
 // wave's slice of LDS (pieces up to kLdsPos), accessed through address-space-3 pointers so the
 // compiler emits in-order ds_read/ds_write (never flat).
-typedef __attribute__((address_space(3))) uint32_t lds_u32;
-
 template <bool GMEM>
 struct LongState;
 

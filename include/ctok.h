@@ -79,8 +79,10 @@ typedef struct ctok_stats {
   uint64_t bytes_norm;    /* bytes after normalisation / prefix space                  */
   uint64_t docs, pieces, long_pieces, tokens, nfc_docs;
   double ms_segment;      /* k_segment alone: piece starts + whole-piece probes/routing */
-  double ms_bpe8, ms_bpe16, ms_bpe32;  /* k_bpe_reg per length class (ms_bpe32 includes the
-                                          dropped-byte generic pass, normally empty)  */
+  double ms_bpe8, ms_bpe16, ms_bpe32;  /* merge pass per length class (<= 8, 9..16, 17..32 B;
+                                          ms_bpe32 includes the dropped-byte generic pass) */
+  uint64_t class_bytes[3];  /* text bytes merged by each length-class pass                 */
+  uint64_t class_ids[3];    /* ids produced by each length-class pass                      */
 } ctok_stats;
 
 /* Upper bound on the ids of a batch whose docs total `n_bytes` bytes (ids <= 3*bytes + docs:
