@@ -391,7 +391,7 @@ void load(ctok* t, const char* buf, size_t len) {
     for (uint64_t e : t->merge_tab) {
       if (e == kEmpty) continue;
       const uint32_t a = (uint32_t)((e >> kIdBits) & ((1u << kIdBits) - 1)), b = (uint32_t)(e & ((1u << kIdBits) - 1));
-      const uint32_t h1 = mhash(a, b), h2 = mhash2(a, b);
+      const uint32_t h1 = mhash(a, b), h2 = mhash2(h1);
       const uint32_t b1 = (h1 >> 12) & (kBloomBits - 1), b2 = (h2 >> 12) & (kBloomBits - 1);
       bloom[b1 >> 5] |= 1u << (b1 & 31);
       bloom[b2 >> 5] |= 1u << (b2 & 31);
@@ -404,7 +404,7 @@ void load(ctok* t, const char* buf, size_t len) {
       for (const auto& re : by_rank) {
         const uint64_t e = re.second;
         const uint32_t a = (uint32_t)((e >> kIdBits) & ((1u << kIdBits) - 1)), b = (uint32_t)(e & ((1u << kIdBits) - 1));
-        const uint32_t c1 = mhash(a, b) & (kHotBuckets - 1), c2 = mhash2(a, b) & (kHotBuckets - 1);
+        const uint32_t c1 = mhash(a, b) & (kHotBuckets - 1), c2 = mhash2(mhash(a, b)) & (kHotBuckets - 1);
         uint64_t* slot = nullptr;
         for (uint32_t c : {c1, c2})
           for (int k = 0; k < 2 && !slot; k++)

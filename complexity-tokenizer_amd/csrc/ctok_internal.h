@@ -33,16 +33,28 @@ constexpr uint32_t kCap0 = kTile, kCap1 = (kTile + 8) / 9, kCap2 = (kTile + 16) 
 // List entry (u32): start within the tile [0,12), piece index within the tile [12,24), length [24,30).
 __host__ __device__ inline uint32_t list_entry(uint32_t sl, uint32_t j, uint32_t n) { return sl | (j << 12) | (n << 24); }
 
-// Merge-table hashes of a pair (a, b): mhash picks the global table slot (open addressing) and,
-// with mhash2, the two candidate buckets of the LDS hot table and the two Bloom-filter bits.
-__host__ __device__ inline uint32_t mhash(uint32_t a, uint32_t b) {
-  const uint32_t h = a * 0x9E3779B1u ^ (b + 0x7F4A7C15u) * 0x85EBCA77u;
-  return h ^ (h >> 15);
+// 24-bit multiply (v_mul_u32_u24: full rate; a 32-bit v_mul_lo_u32 is quarter rate on CDNA)
+__host__ __device__ inline uint32_t mul24(uint32_t a, uint32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __umul24(a, b);
+#else
+  return (a & 0xFFFFFFu) * (b & 0xFFFFFFu);
+#endif
 }
-__host__ __device__ inline uint32_t mhash2(uint32_t a, uint32_t b) {
-  uint32_t h = (a + 0x632BE5ABu) * 0xC2B2AE3Du ^ b * 0x27D4EB2Fu;
+
+// Merge-table hashes of a pair (a, b) of token ids (< 2^21): mhash picks the global table slot
+// (open addressing) and, with mhash2, the two candidate buckets of the LDS hot table and the two
+// Bloom-filter bits.  Built from 24-bit multiplies and shift-xors only.
+__host__ __device__ inline uint32_t mhash(uint32_t a, uint32_t b) {
+  uint32_t h = mul24(a, 0x9E3779u) + mul24(b ^ 0x5A5A5Au, 0x85EBCBu);
+  h ^= h >> 15;
+  h = mul24(h, 0xC2B2AFu) ^ (h >> 9);
+  return h ^ (h >> 16);
+}
+__host__ __device__ inline uint32_t mhash2(uint32_t h1) {
+  uint32_t h = mul24(h1 ^ (h1 >> 24), 0x27D4EBu) + (h1 >> 11);
   h ^= h >> 13;
-  h *= 0x165667B1u;
+  h = mul24(h, 0x165667u) ^ (h >> 8);
   return h ^ (h >> 16);
 }
 
@@ -61,7 +73,9 @@ constexpr uint32_t kLdsImageBytes = kHotU64 * 8 + kBloomWords * 4;
 // load time by running the merge loop on every vocab entry).  Entry = {lo32, hi32, len, id} of
 // the zero-padded bytes; len == 0 marks an empty slot.
 __host__ __device__ inline uint32_t piece_hash(uint32_t lo, uint32_t hi, uint32_t len) {
-  uint32_t h = lo * 0x9E3779B1u ^ (hi + 0x632BE5ABu) * 0x85EBCA77u ^ len * 0xC2B2AE3Du;
+  uint32_t h = mul24(lo, 0x9E3779u) + mul24((lo >> 24) | (hi << 8), 0x85EBCBu) + mul24((hi >> 16) | (len << 16), 0xC2B2AFu);
+  h ^= h >> 15;
+  h = mul24(h, 0x27D4EBu) ^ (h >> 9);
   return h ^ (h >> 16);
 }
 

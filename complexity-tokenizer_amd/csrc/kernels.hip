@@ -216,20 +216,6 @@ __device__ __forceinline__ uint32_t select_bit(uint64_t x, uint32_t k) {
   return pos;
 }
 
-// wave-aggregated append to an LDS counter: returns this lane's slot (lanes with take == false
-// get garbage).  One ds_add per wave instead of one per lane.
-__device__ __forceinline__ uint32_t wave_append(uint32_t* counter, bool take) {
-  const uint64_t m = __ballot(take);
-  uint32_t base = 0;
-  if (m) {
-    const uint32_t leader = __ffsll((unsigned long long)m) - 1;
-    const uint32_t lane = threadIdx.x & 63;
-    uint32_t b = 0;
-    if (lane == leader) b = atomicAdd(counter, (uint32_t)__popcll(m));
-    base = (uint32_t)__shfl((int)b, (int)leader, 64);
-  }
-  return base + (uint32_t)__popcll(m & lanemask_lt());
-}
 
 
 // Whole-piece table lookup given the first probed slot e (at h): the vocab id, or kNone.
@@ -258,7 +244,6 @@ __device__ __forceinline__ uint32_t piece_probe(const Tables& t, uint4 e, uint32
 __global__ __launch_bounds__(64 * kSegWaves) void k_segment(Work w, Tables t) {
   __shared__ uint64_t s_st_all[kSegWaves][64];
   __shared__ uint32_t s_wpre_all[kSegWaves][64];
-  __shared__ uint32_t s_cnt_all[kSegWaves][4];
   __shared__ uint32_t s_text_all[kSegWaves][(kTileWords + 1) * 16 + 4];  // the tile + look-ahead word
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wid = uni(threadIdx.x >> 6);
@@ -266,8 +251,6 @@ __global__ __launch_bounds__(64 * kSegWaves) void k_segment(Work w, Tables t) {
   if (tile >= w.n_tiles) return;
   uint64_t* s_st = s_st_all[wid];
   uint32_t* s_wpre = s_wpre_all[wid];
-  uint32_t* s_cnt = s_cnt_all[wid];
-  if (lane < 4) s_cnt[lane] = 0;
   const uint32_t B = w.n_bytes;
   const uint32_t t0 = tile * kTile;
   const int64_t g = (int64_t)tile * kTileWords - 1 + lane;  // this lane's word
@@ -388,6 +371,7 @@ __global__ __launch_bounds__(64 * kSegWaves) void k_segment(Work w, Tables t) {
   uint16_t* tpos = w.tpos + (size_t)tile * kTileSlots;
   const uint64_t trusted_end = (uint64_t)t0 + kTile + 62;  // the look-ahead's bits 0..61
   uint32_t hits = 0;
+  uint32_t n0 = 0, n1 = 0, n2 = 0;  // class-list lengths (wave-uniform)
   constexpr int U = kSegUnroll;
   for (uint32_t j0 = 0; j0 < np; j0 += 64 * U) {
     uint32_t sl[U], n[U], cls[U], plo[U], phi[U], h[U];
@@ -459,15 +443,15 @@ __global__ __launch_bounds__(64 * kSegWaves) void k_segment(Work w, Tables t) {
     for (int u = 0; u < U; u++) {
       const uint32_t j = j0 + 64 * u + lane;
       const uint32_t e = list_entry(sl[u], j, n[u]);
-      {
-        const uint32_t q = wave_append(&s_cnt[0], cls[u] == 0);
-        if (cls[u] == 0) w.list0[(size_t)tile * kCap0 + q] = e;
-      }
-      if (!generic) {
-        const uint32_t q1 = wave_append(&s_cnt[1], cls[u] == 1);
-        if (cls[u] == 1) w.list1[(size_t)tile * kCap1 + q1] = e;
-        const uint32_t q2 = wave_append(&s_cnt[2], cls[u] == 2);
-        if (cls[u] == 2) w.list2[(size_t)tile * kCap2 + q2] = e;
+      {  // the wave owns its tile's lists: running counts in scalar registers, no atomics
+        const uint64_t m0 = __ballot(cls[u] == 0), m1 = __ballot(cls[u] == 1), m2 = __ballot(cls[u] == 2);
+        const uint64_t below = lanemask_lt();
+        if (cls[u] == 0) w.list0[(size_t)tile * kCap0 + n0 + __popcll(m0 & below)] = e;
+        if (cls[u] == 1) w.list1[(size_t)tile * kCap1 + n1 + __popcll(m1 & below)] = e;
+        if (cls[u] == 2) w.list2[(size_t)tile * kCap2 + n2 + __popcll(m2 & below)] = e;
+        n0 += __popcll(m0);
+        n1 += __popcll(m1);
+        n2 += __popcll(m2);
       }
       const uint64_t lm = __ballot(cls[u] == 3);
       if (lm) {  // rare: one global atomic per wave
@@ -487,7 +471,7 @@ __global__ __launch_bounds__(64 * kSegWaves) void k_segment(Work w, Tables t) {
     w.tile_tok[tile] = hits;  // initial token count (the merge passes add theirs atomically)
     w.tile_np[tile] = np;
   }
-  if (lane < 3) w.tcls[(size_t)lane * w.n_tiles + tile] = s_cnt[lane];
+  if (lane < 3) w.tcls[(size_t)lane * w.n_tiles + tile] = lane == 0 ? n0 : lane == 1 ? n1 : n2;
 }
 
 hipError_t launch_segment(const Work& w, const Tables& t, hipStream_t s) {
@@ -754,6 +738,57 @@ __device__ __forceinline__ const uint32_t* class_list(const Work& w) {
   return N == 8 ? w.list0 : N == 16 ? w.list1 : w.list2;
 }
 
+// The merge loop on the first N register slots of tk / rk (compile-time indices only, so the
+// arrays stay in registers): branch-free over the slots, the lowest (rank, position) pair is
+// merged, the slots right of it shift left by one, the two new pairs' ranks are looked up.
+// Returns true when it stopped because the piece shrank to <= stop tokens (the caller continues
+// on fewer slots), false when no pair can merge.  Slots >= m hold kDead / kNoRank.
+template <int N, bool COMPACT>
+__device__ __forceinline__ bool merge_slots(const Tables& t, const PairLds& P, uint32_t* tk, uint32_t* rk,
+                                            uint32_t& m, uint32_t stop, uint32_t* err) {
+  for (;;) {
+    if (m <= stop) return true;
+    uint32_t key = ~0u;  // rank << 5 | position: one v_min per slot (ranks < 2^22)
+#pragma unroll
+    for (int k = 0; k < N - 1; k++) key = min(key, (rk[k] << 5) | (uint32_t)k);
+    const uint32_t best = key >> 5, bi = key & 31u;
+    if (best == kNoRank) return false;
+    const uint32_t nid = COMPACT ? best : t.rank_newid[best];
+    uint32_t L = 0, R = 0;
+#pragma unroll
+    for (int k = 0; k < N; k++) {
+      L = ((uint32_t)k + 1 == bi) ? tk[k] : L;
+      R = ((uint32_t)k == bi + 2) ? tk[k] : R;
+    }
+    const bool has_l = bi > 0, has_r = bi + 2 < m;
+    const uint32_t hl1 = mhash(L, nid), hr1 = mhash(nid, R);
+    bool gl, gr;
+    uint32_t rl = rank_lds(P, L, nid, hl1, mhash2(hl1), gl);
+    uint32_t rr = rank_lds(P, nid, R, hr1, mhash2(hr1), gr);
+    gl = gl && has_l;
+    gr = gr && has_r;
+    uint64_t el = 0, er = 0;
+    if (gl) el = t.merge_tab[hl1 & t.merge_mask];
+    if (gr) er = t.merge_tab[hr1 & t.merge_mask];
+#pragma unroll
+    for (int k = 0; k < N; k++) {  // ascending: tk[k+1] is read before it is overwritten
+      const uint32_t nxt_t = k + 1 < N ? tk[k + 1] : kDead;
+      const uint32_t nxt_r = k + 1 < N ? rk[k + 1] : kNoRank;
+      const bool gt = (uint32_t)k > bi;
+      tk[k] = gt ? nxt_t : ((uint32_t)k == bi ? nid : tk[k]);
+      rk[k] = gt ? nxt_r : rk[k];
+    }
+    m--;
+    if (gl) rl = resolve_rank(t, pair_key(L, nid), hl1 & t.merge_mask, el, err);
+    if (gr) rr = resolve_rank(t, pair_key(nid, R), hr1 & t.merge_mask, er, err);
+    rl = has_l ? rl : kNoRank;
+    rr = has_r ? rr : kNoRank;
+#pragma unroll
+    for (int k = 0; k < N - 1; k++)
+      rk[k] = ((uint32_t)k + 1 == bi) ? rl : (((uint32_t)k == bi) ? rr : rk[k]);
+  }
+}
+
 // Merge pass over one length class (N = 8, 16, 32 slots): a persistent grid, one workgroup per
 // CU holding the merge LDS image; workgroup b takes a contiguous range of tiles and walks its
 // class lists 64 tiles at a time (one concatenated list per chunk, see tile_share_init).
@@ -814,7 +849,7 @@ __global__ __launch_bounds__(LdsClass<N>::threads) void k_bpe_lds(Work w, Tables
           const int k = k0 + i;
           if (k < N - 1) {
             h1[i] = mhash(tk[k], tk[k + 1]);
-            rk[k] = rank_lds(P, tk[k], tk[k + 1], h1[i], mhash2(tk[k], tk[k + 1]), g[i]);
+            rk[k] = rank_lds(P, tk[k], tk[k + 1], h1[i], mhash2(h1[i]), g[i]);
             g[i] = g[i] && (uint32_t)k + 1 < n;
           }
         }
@@ -832,48 +867,13 @@ __global__ __launch_bounds__(LdsClass<N>::threads) void k_bpe_lds(Work w, Tables
       }
       rk[N - 1] = kNoRank;
       uint32_t m = n;
-      // Branch-free over the N slots (selects only): the lowest (rank, position) pair is merged,
-      // the slots right of it shift left by one, the two new pairs' ranks are looked up.
-      for (;;) {
-        uint32_t key = ~0u;  // rank << 5 | position: one v_min per slot (ranks < 2^22)
-#pragma unroll
-        for (int k = 0; k < N - 1; k++) key = min(key, (rk[k] << 5) | (uint32_t)k);
-        const uint32_t best = key >> 5, bi = key & 31u;
-        if (best == kNoRank) break;
-        const uint32_t nid = COMPACT ? best : t.rank_newid[best];
-        uint32_t L = 0, R = 0;
-#pragma unroll
-        for (int k = 0; k < N; k++) {
-          L = ((uint32_t)k + 1 == bi) ? tk[k] : L;
-          R = ((uint32_t)k == bi + 2) ? tk[k] : R;
-        }
-        const bool has_l = bi > 0, has_r = bi + 2 < m;
-        const uint32_t hl1 = mhash(L, nid), hr1 = mhash(nid, R);
-        bool gl, gr;
-        uint32_t rl = rank_lds(P, L, nid, hl1, mhash2(L, nid), gl);
-        uint32_t rr = rank_lds(P, nid, R, hr1, mhash2(nid, R), gr);
-        gl = gl && has_l;
-        gr = gr && has_r;
-        uint64_t el = 0, er = 0;
-        if (gl) el = t.merge_tab[hl1 & t.merge_mask];
-        if (gr) er = t.merge_tab[hr1 & t.merge_mask];
-#pragma unroll
-        for (int k = 0; k < N; k++) {  // ascending: tk[k+1] is read before it is overwritten
-          const uint32_t nxt_t = k + 1 < N ? tk[k + 1] : kDead;
-          const uint32_t nxt_r = k + 1 < N ? rk[k + 1] : kNoRank;
-          const bool gt = (uint32_t)k > bi;
-          tk[k] = gt ? nxt_t : ((uint32_t)k == bi ? nid : tk[k]);
-          rk[k] = gt ? nxt_r : rk[k];
-        }
-        m--;
-        if (gl) rl = resolve_rank(t, pair_key(L, nid), hl1 & t.merge_mask, el, err);
-        if (gr) rr = resolve_rank(t, pair_key(nid, R), hr1 & t.merge_mask, er, err);
-        rl = has_l ? rl : kNoRank;
-        rr = has_r ? rr : kNoRank;
-#pragma unroll
-        for (int k = 0; k < N - 1; k++)
-          rk[k] = ((uint32_t)k + 1 == bi) ? rl : (((uint32_t)k == bi) ? rr : rk[k]);
+      // tiers: N slots while the piece has more than N/2 tokens, then N/2, ... down to 8 slots
+      bool more = true;
+      if constexpr (N >= 32) more = merge_slots<32, COMPACT>(t, P, tk, rk, m, 16, err);
+      if constexpr (N >= 16) {
+        if (more) more = merge_slots<16, COMPACT>(t, P, tk, rk, m, 8, err);
       }
+      if (more) merge_slots<8, COMPACT>(t, P, tk, rk, m, 0, err);
       uint32_t* out = w.scratch + s;
 #pragma unroll
       for (int k = 0; k < N; k++)
@@ -1239,15 +1239,33 @@ __global__ __launch_bounds__(256) void k_emit(Work w, uint32_t* __restrict__ ids
       reinterpret_cast<uint4*>(tcnt + jb)[k] = make_uint4(pre[4 * k], pre[4 * k + 1], pre[4 * k + 2], pre[4 * k + 3]);
   }
   __syncthreads();
-  // 2. copy, piece j = tid + 256 k: consecutive lanes write consecutive ids
-  for (uint32_t j = tid; j < np; j += 256) {
+  // 2. copy, piece j = tid + 256 k: consecutive lanes write consecutive ids.  All first-id
+  // loads of a thread's pieces are in flight together; a multi-id piece (rare) then reads its
+  // remaining ids four at a time.
+  uint32_t pos[PER], v[PER];
+#pragma unroll
+  for (int k = 0; k < PER; k++) {
+    const uint32_t j = tid + 256 * k;
+    pos[k] = j < np ? (uint32_t)tpos[j] : 0u;
+  }
+#pragma unroll
+  for (int k = 0; k < PER; k++) v[k] = src0[pos[k]];
+#pragma unroll
+  for (int k = 0; k < PER; k++) {
+    const uint32_t j = tid + 256 * k;
+    if (j >= np) break;
     const uint32_t oj = s_off[j], cj = s_off[j + 1] - oj;
-    const uint32_t* src = src0 + tpos[j];
     const uint64_t dst = base + oj;
-    const uint32_t v0 = src[0];  // every piece has >= 1 id unless all its bytes were dropped
-    if (cj > 0 && dst < ids_cap) ids[dst] = v0;
-    for (uint32_t k = 1; k < cj; k++)
-      if (dst + k < ids_cap) ids[dst + k] = src[k];  // the host reports CTOK_E_CAPACITY when short
+    if (cj > 0 && dst < ids_cap) ids[dst] = v[k];
+    for (uint32_t m = 1; m < cj; m += 4) {
+      const uint32_t* src = src0 + pos[k] + m;
+      uint32_t x[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) x[i] = m + i < cj ? src[i] : 0u;
+#pragma unroll
+      for (int i = 0; i < 4; i++)
+        if (m + i < cj && dst + m + i < ids_cap) ids[dst + m + i] = x[i];  // the host reports CTOK_E_CAPACITY when short
+    }
   }
 }
 
