@@ -164,6 +164,7 @@ struct DeviceState {
   uint64_t* host = nullptr;       // pinned host words for small device->host readbacks
   // tables
   DevBuf<uint64_t> merge_tab, lds_image;
+  DevBuf<uint32_t> pair0;
   DevBuf<uint32_t> piece_tab;
   DevBuf<uint32_t> rank_newid;
   DevBuf<int32_t> byte2id;
@@ -209,6 +210,7 @@ struct ctok {
   std::vector<uint64_t> merge_tab;
   uint32_t merge_mask = 0;
   std::vector<uint64_t> lds_image;  // kLdsImageBytes: hot table + Bloom filter
+  std::vector<uint32_t> pair0;      // 256 x 256 byte-pair merge values
   size_t hot_entries = 0;
   std::vector<uint32_t> piece_tab;  // 4 u32 per slot (see ctok_internal.h piece_hash)
   uint32_t piece_mask = 0;
@@ -379,9 +381,21 @@ void load(ctok* t, const char* buf, size_t len) {
   }
   for (uint32_t id : valid_new)
     if (id > kMaxId) throw_err(CTOK_E_UNSUPPORTED, "token ids above 2^21-2 are not supported by the device merge table");
+  // byte-level initial ids: vocab[bytes_to_unicode[b]] (src/bpe.rs:94-97), -1 = dropped
+  std::vector<uint32_t> bm = byte_map();
+  for (int b = 0; b < 256; b++) {
+    auto it = t->vocab.find(utf8(bm[b]));
+    t->byte2id[b] = it == t->vocab.end() ? -1 : (int32_t)it->second;
+  }
+
   // LDS image: hot table filled greedily in rank order (a pair whose two buckets are full stays
-  // global-only), Bloom filter over every entry (including the ones whose lookup panics)
+  // global-only), Bloom filter over every entry (including the ones whose lookup panics).
+  // Byte-pair merges are left out of both: the merge passes look a pair up in LDS only after a
+  // merge, when one side is a merged (multi-byte) token; initial byte pairs use pair0.
   {
+    std::vector<uint8_t> is_byte_tok(kMaxId + 2, 0);
+    for (int b = 0; b < 256; b++)
+      if (t->byte2id[b] >= 0 && (uint32_t)t->byte2id[b] <= kMaxId) is_byte_tok[t->byte2id[b]] = 1;
     t->lds_image.assign(kLdsImageBytes / 8, 0);
     uint64_t* hot = t->lds_image.data();
     std::fill(hot, hot + kHotU64, kEmpty);
@@ -391,6 +405,7 @@ void load(ctok* t, const char* buf, size_t len) {
     for (uint64_t e : t->merge_tab) {
       if (e == kEmpty) continue;
       const uint32_t a = (uint32_t)((e >> kIdBits) & ((1u << kIdBits) - 1)), b = (uint32_t)(e & ((1u << kIdBits) - 1));
+      if (is_byte_tok[a] && is_byte_tok[b]) continue;
       const uint32_t h1 = mhash(a, b), h2 = mhash2(h1);
       const uint32_t b1 = (h1 >> 12) & (kBloomBits - 1), b2 = (h2 >> 12) & (kBloomBits - 1);
       bloom[b1 >> 5] |= 1u << (b1 & 31);
@@ -435,12 +450,18 @@ void load(ctok* t, const char* buf, size_t len) {
     }
   }
 
-  // byte-level initial ids: vocab[bytes_to_unicode[b]] (src/bpe.rs:94-97), -1 = dropped
-  std::vector<uint32_t> bm = byte_map();
-  for (int b = 0; b < 256; b++) {
-    auto it = t->vocab.find(utf8(bm[b]));
-    t->byte2id[b] = it == t->vocab.end() ? -1 : (int32_t)it->second;
-  }
+
+  // byte-pair table: the merge-table value of (byte2id[a], byte2id[b]) for every byte pair a, b
+  // (the initial pairs of every piece are byte pairs), kNoRank where the pair has no merge
+  t->pair0.assign(65536, kNoRank);
+  for (uint32_t a = 0; a < 256; a++)
+    for (uint32_t b = 0; b < 256; b++) {
+      if (t->byte2id[a] < 0 || t->byte2id[b] < 0) continue;
+      auto it = ranks.find(((uint64_t)(uint32_t)t->byte2id[a] << 32) | (uint32_t)t->byte2id[b]);
+      if (it == ranks.end()) continue;
+      const uint32_t r = it->second;
+      t->pair0[a * 256 + b] = t->compact ? (r < valid_new.size() ? valid_new[r] : kPanicVal) : r;
+    }
 
   // whole-piece table: every vocab entry of <= 8 raw bytes whose own BPE is that single token
   {
@@ -587,6 +608,7 @@ DeviceState* device_state(ctok* t, int device) {
   hipStream_t s = ds->stream;
   upload(ds->merge_tab, t->merge_tab.data(), t->merge_tab.size(), s);
   upload(ds->lds_image, t->lds_image.data(), t->lds_image.size(), s);
+  upload(ds->pair0, t->pair0.data(), t->pair0.size(), s);
   upload(ds->rank_newid, t->rank_newid.data(), t->rank_newid.size(), s);
   upload(ds->piece_tab, t->piece_tab.data(), t->piece_tab.size(), s);
   upload(ds->byte2id, t->byte2id, 256, s);
@@ -609,6 +631,7 @@ DeviceState* device_state(ctok* t, int device) {
   tb.merge_tab = ds->merge_tab.p;
   tb.merge_mask = t->merge_mask;
   tb.lds_image = (const uint4*)ds->lds_image.p;
+  tb.pair0 = ds->pair0.p;
   tb.piece_tab = (const uint4*)ds->piece_tab.p;
   tb.piece_mask = t->piece_mask;
   tb.rank_newid = ds->rank_newid.p;

@@ -200,6 +200,20 @@ __device__ __forceinline__ void load_words(const uint8_t* text, uint32_t s, uint
 
 __device__ __forceinline__ uint32_t byte_of(uint32_t w, int k) { return (w >> (8 * (k & 3))) & 255u; }
 
+
+
+
+// Whole-piece table lookup given the first probed slot e (at h): the vocab id, or kNone.
+__device__ __forceinline__ uint32_t piece_probe(const Tables& t, uint4 e, uint32_t h, uint32_t lo, uint32_t hi,
+                                                uint32_t n) {
+  while (e.z != 0) {  // linear probing past the first slot (rare)
+    if (e.x == lo && e.y == hi && e.z == n) return e.w;
+    h = (h + 1) & t.piece_mask;
+    e = t.piece_tab[h];
+  }
+  return kNone;
+}
+
 // position of the k-th (0-based) set bit of x (k < popcount(x))
 __device__ __forceinline__ uint32_t select_bit(uint64_t x, uint32_t k) {
   uint32_t pos = 0;
@@ -218,16 +232,6 @@ __device__ __forceinline__ uint32_t select_bit(uint64_t x, uint32_t k) {
 
 
 
-// Whole-piece table lookup given the first probed slot e (at h): the vocab id, or kNone.
-__device__ __forceinline__ uint32_t piece_probe(const Tables& t, uint4 e, uint32_t h, uint32_t lo, uint32_t hi,
-                                                uint32_t n) {
-  while (e.z != 0) {  // linear probing past the first slot (rare)
-    if (e.x == lo && e.y == hi && e.z == n) return e.w;
-    h = (h + 1) & t.piece_mask;
-    e = t.piece_tab[h];
-  }
-  return kNone;
-}
 
 // One wavefront per tile, kSegWaves tiles per workgroup, no workgroup barrier.  Lane l owns the
 // 64-byte word g0 - 1 + l: lane 0 is the previous tile's last word (context only), lanes 1..62
@@ -823,8 +827,8 @@ __global__ __launch_bounds__(LdsClass<N>::threads) void k_bpe_lds(Work w, Tables
       const uint32_t n = e >> 24;
       uint32_t tk[N], rk[N];
       bool missing = false;
+      uint32_t wv[N / 4];
       {
-        uint32_t wv[N / 4];
         load_words<N / 4>(w.text, s, w.n_bytes, wv);
 #pragma unroll
         for (int k = 0; k < N; k++) {
@@ -837,32 +841,19 @@ __global__ __launch_bounds__(LdsClass<N>::threads) void k_bpe_lds(Work w, Tables
         w.mid_list[atomicAdd(&w.counters[4], 1u)] = (uint64_t)s | ((uint64_t)j << 32) | ((uint64_t)n << 48);
         continue;
       }
-      // initial pair ranks, four pairs at a time: LDS stage, then the global probes that remain
-      // (issued together before any is consumed)
+      // initial pair ranks: every initial pair is a byte pair, one load each from the 256 x 256
+      // byte-pair table (L2-resident), all in flight together
+      {
+        uint32_t bytes[N];
 #pragma unroll
-      for (int k0 = 0; k0 < N - 1; k0 += 4) {
-        uint32_t h1[4];
-        bool g[4];
-        uint64_t ee[4];
+        for (int k = 0; k < N; k++) bytes[k] = byte_of(wv[k >> 2], k);
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
-          const int k = k0 + i;
-          if (k < N - 1) {
-            h1[i] = mhash(tk[k], tk[k + 1]);
-            rk[k] = rank_lds(P, tk[k], tk[k + 1], h1[i], mhash2(h1[i]), g[i]);
-            g[i] = g[i] && (uint32_t)k + 1 < n;
-          }
-        }
+        for (int k = 0; k < N - 1; k++) rk[k] = t.pair0[(bytes[k] << 8) | bytes[k + 1]];
 #pragma unroll
-        for (int i = 0; i < 4; i++)
-          if (k0 + i < N - 1 && g[i]) ee[i] = t.merge_tab[h1[i] & t.merge_mask];
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-          const int k = k0 + i;
-          if (k < N - 1) {
-            if (g[i]) rk[k] = resolve_rank(t, pair_key(tk[k], tk[k + 1]), h1[i] & t.merge_mask, ee[i], err);
-            rk[k] = (uint32_t)k + 1 < n ? rk[k] : kNoRank;
-          }
+        for (int k = 0; k < N - 1; k++) {
+          const bool live = (uint32_t)k + 1 < n;
+          if (live && rk[k] != kNoRank && value_panics(t, rk[k])) atomicOr(err, kErrPanic);
+          rk[k] = (live && !(rk[k] != kNoRank && value_panics(t, rk[k]))) ? rk[k] : kNoRank;
         }
       }
       rk[N - 1] = kNoRank;
