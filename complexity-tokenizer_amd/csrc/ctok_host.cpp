@@ -700,6 +700,12 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   if (n_bytes >= 0xF0000000ull) throw_err(CTOK_E_ARG, "a single call is limited to < 3.75 GiB of text; split the batch");
   if (n_docs >= 0xF0000000ull) throw_err(CTOK_E_ARG, "too many documents in one call");
   const Tables& tb = ds->t;
+  // NFC speculation: when NFC is the only normalisation, run the pipeline on the raw text and
+  // let k_segment flag any code point that NFC might change (NFC_QC != Yes or a non-zero
+  // combining class; ASCII never is).  Only a flagged batch pays for the check + normalise
+  // passes and a second run.
+  bool speculate = t->nfc && !t->add_prefix_space && n_bytes && !getenv("CTOK_NO_NFC_SPECULATION");
+  for (;;) {
   if (timing) HIPTRY(hipEventRecord(ds->ev[0], s));
 
   ds->counters.ensure(16);
@@ -709,7 +715,7 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   uint64_t B = n_bytes;
   uint64_t nfc_docs = 0;
   bool norm = t->add_prefix_space;
-  if (t->nfc && n_bytes) {
+  if (t->nfc && n_bytes && !speculate) {
     ds->doc_flag.ensure(n_docs + 1);
     HIPTRY(hipMemsetAsync(ds->doc_flag.p, 0, (n_docs + 1) * 4, s));
     STEP("nfc_check", launch_nfc_check(d_text, n_bytes, d_off, (uint32_t)n_docs, tb, ds->doc_flag.p, ds->counters.p + 3, s));
@@ -750,6 +756,7 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   w.n_words = (uint32_t)((B + 31) / 32);
   w.n_tiles = (uint32_t)((B + kTile - 1) / kTile);
   w.n_cus = ds->n_cus;
+  w.nfc_watch = speculate ? 1u : 0u;
   const size_t nt = w.n_tiles;
   ds->docbits.ensure(w.n_words + 8);
   ds->pbits.ensure(w.n_words + 8);
@@ -764,7 +771,7 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   }
   ds->tpos.ensure(nt * kTileSlots + 8);
   ds->tcnt.ensure(nt * kTileSlots + 8);
-  ds->scratch.ensure(B + 8);
+  ds->scratch.ensure(nt * kTile + 8);  // whole tiles: k_emit gathers unconditionally
   ds->long_list.ensure(B / kShortMax + nt + 8);
   ds->mid_list.ensure(B / 2 + 8);
   ds->lw.ensure(4 * B + 64);
@@ -807,11 +814,15 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   if (timing) HIPTRY(hipEventRecord(ds->ev[6], s));
   if (st && w.n_tiles) STEP("count", launch_count_pieces(w, s));
   HIPTRY(hipMemcpyAsync(ds->host, d_tok_off + n_docs, 8, hipMemcpyDeviceToHost, s));
-  HIPTRY(hipMemcpyAsync(ds->host + 1, ds->counters.p, 48, hipMemcpyDeviceToHost, s));
+  HIPTRY(hipMemcpyAsync(ds->host + 1, ds->counters.p, 64, hipMemcpyDeviceToHost, s));
   spin_sync(ds, s);
   const uint64_t ntok = ((volatile uint64_t*)ds->host)[0];
-  uint32_t cnt[12];
-  for (int i = 0; i < 12; i++) cnt[i] = ((volatile uint32_t*)(ds->host + 1))[i];
+  uint32_t cnt[16];
+  for (int i = 0; i < 16; i++) cnt[i] = ((volatile uint32_t*)(ds->host + 1))[i];
+  if (speculate && cnt[12]) {  // a code point NFC may change: check, normalise, run again
+    speculate = false;
+    continue;
+  }
   const uint32_t P = cnt[5];
   if (cnt[2] & kErrPanic)
     throw_err(CTOK_E_PANIC, "index out of bounds: a merge rank points past the list of valid merges (reference src/bpe.rs:141 panics)");
@@ -846,6 +857,7 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
     }
   }
   return ntok;
+  }
 }
 
 }  // namespace

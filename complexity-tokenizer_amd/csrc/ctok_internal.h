@@ -68,6 +68,7 @@ constexpr uint32_t kBloomBits = 1u << 18;              // 32 KiB
 constexpr uint32_t kHotU64 = 2 * kHotBuckets;
 constexpr uint32_t kBloomWords = kBloomBits / 32;
 constexpr uint32_t kLdsImageBytes = kHotU64 * 8 + kBloomWords * 4;
+constexpr uint32_t kSortCap = 8192;  // merge-pass chunk entries sorted by length bucket (u16 in LDS)
 
 // Whole-piece table: raw byte strings of <= 8 bytes whose BPE is exactly one token (checked at
 // load time by running the merge loop on every vocab entry).  Entry = {lo32, hi32, len, id} of
@@ -122,6 +123,8 @@ struct Work {              // device pointers, sized by the host for one call
   uint32_t n_words;
   uint32_t n_tiles;
   uint32_t n_cus;          // compute units of the device (persistent merge-pass grid)
+  uint32_t nfc_watch;      // 1: the text was not NFC-checked; k_segment sets counters[12] on a
+                           // code point NFC might change
   uint16_t* wpref;         // [n_tiles * 64] pieces of the tile before each 64-byte word
   uint32_t* tile_np;       // [n_tiles] pieces starting in the tile
   uint32_t* tile_tok;      // [n_tiles + 1] tokens per tile, scanned in place to the tile's first id
@@ -135,7 +138,8 @@ struct Work {              // device pointers, sized by the host for one call
   uint64_t* long_list;     // pieces > kShortMax B (or of unknown length at a tile end): s | j << 32
   uint64_t* mid_list;      // pieces with dropped bytes for the generic kernel: s | j << 32 | n << 48
   uint32_t* counters;      // [0] long count, [2] err, [3] nfc docs, [4] mid count, [5] pieces (stats),
-                           // [6 + 2c], [7 + 2c]: bytes merged / ids produced by class pass c (stats)
+                           // [6 + 2c], [7 + 2c]: bytes merged / ids produced by class pass c (stats),
+                           // [12] NFC speculation failed
   uint32_t* lw;            // long-piece workspace: 4 * n_bytes u32
   uint32_t* scan_tmp;      // scan partials
   uint64_t scan_tmp_cap;

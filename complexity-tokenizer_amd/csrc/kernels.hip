@@ -85,6 +85,21 @@ __device__ T block_excl_scan(T v, T* smem /*[17]*/, T* total) {
 // wave reduces over inactive lanes and never terminates).
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// wave-aggregated append to an LDS counter: returns this lane's slot (lanes with take == false
+// get garbage).  One ds_add per wave instead of one per lane.
+__device__ __forceinline__ uint32_t wave_append(uint32_t* counter, bool take) {
+  const uint64_t m = __ballot(take);
+  uint32_t base = 0;
+  if (m) {
+    const uint32_t leader = __ffsll((unsigned long long)m) - 1;
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t b = 0;
+    if (lane == leader) b = atomicAdd(counter, (uint32_t)__popcll(m));
+    base = (uint32_t)__shfl((int)b, (int)leader, 64);
+  }
+  return base + (uint32_t)__popcll(m & lanemask_lt());
+}
+
 __device__ __forceinline__ int u8len(uint8_t b) {
   return b < 0x80 ? 1 : (b >> 5) == 6 ? 2 : (b >> 4) == 14 ? 3 : 4;
 }
@@ -154,8 +169,14 @@ hipError_t launch_docstart(const Work& w, hipStream_t s) {
 // the per-word logic is csrc/seg_lane.h).  Positions >= n_bytes read as doc starts (D), which
 // closes every run at the end of the text.
 
-// class of the code point byte x belongs to (x < B; non-ASCII slow path)
-__device__ __noinline__ int seg_cls_wide(const uint8_t* text, uint32_t B, uint32_t x, const Tables& t) {
+__device__ __forceinline__ uint16_t nfc16(const Tables& t, uint32_t cp) {
+  if (cp >= 0x110000) return 0;
+  return t.nfc_s2[t.nfc_s1[cp >> 8] * 256 + (cp & 255)];
+}
+
+// class of the code point byte x belongs to (x < B; non-ASCII slow path), | 4 when NFC might
+// change that code point (NFC_QC != Yes or non-zero combining class)
+__device__ __forceinline__ int seg_cls_wide(const uint8_t* text, uint32_t B, uint32_t x, const Tables& t) {
   uint32_t j = x;
 #pragma unroll
   for (int k = 0; k < 3; k++)
@@ -168,7 +189,7 @@ __device__ __noinline__ int seg_cls_wide(const uint8_t* text, uint32_t B, uint32
   else if (len == 2) c = ((b0 & 0x1Fu) << 6) | at(j + 1);
   else if (len == 3) c = ((b0 & 0x0Fu) << 12) | (at(j + 1) << 6) | at(j + 2);
   else c = ((b0 & 0x07u) << 18) | (at(j + 1) << 12) | (at(j + 2) << 6) | at(j + 3);
-  return cls_of(c, t);
+  return cls_of(c, t) | (nfc16(t, c) != 0 ? 4 : 0);
 }
 
 __device__ __forceinline__ uint64_t shfl_up64(uint64_t v) {
@@ -303,10 +324,13 @@ __global__ __launch_bounds__(64 * kSegWaves) void k_segment(Work w, Tables t) {
   if (m.NA) {  // non-ASCII code points: one class lookup per code point
     const uint32_t x0 = (uint32_t)(g * 64);
     uint64_t todo = m.NA;
+    bool nfc_bad = false;
     while (todo) {
       const uint32_t i = __builtin_ctzll(todo);
       const uint32_t b0 = w.text[x0 + i];
-      const int cl = seg_cls_wide(w.text, B, x0 + i, t);
+      const int cw = seg_cls_wide(w.text, B, x0 + i, t);
+      const int cl = cw & 3;
+      nfc_bad |= (cw & 4) != 0;
       // a lead byte covers its continuation bytes within the word; a continuation byte at the
       // start of the word (lead in the previous word) is classified on its own
       const uint32_t len = (b0 & 0xC0) == 0x80 ? 1u : (uint32_t)u8len((uint8_t)b0);
@@ -316,6 +340,7 @@ __global__ __launch_bounds__(64 * kSegWaves) void k_segment(Work w, Tables t) {
       else if (cl == 2) m.N |= bits & m.NA;
       todo &= ~bits;
     }
+    if (nfc_bad && w.nfc_watch) atomicOr(&w.counters[12], 1u);
   }
   // contraction letters only where an apostrophe could use them (this word's or the previous
   // word's last two bytes)
@@ -805,6 +830,8 @@ __global__ __launch_bounds__(LdsClass<N>::threads) void k_bpe_lds(Work w, Tables
   extern __shared__ __attribute__((aligned(16))) uint4 s_img[];
   __shared__ int32_t s_b2id[256];
   __shared__ uint32_t s_pre[K + 1], s_tsum[K], s_stat[2];
+  __shared__ uint32_t s_bcnt[4], s_bfill[4];
+  __shared__ uint16_t s_perm[kSortCap];  // the chunk's entries ordered by length bucket
   const uint32_t tid = threadIdx.x;
   if (tid < 2) s_stat[tid] = 0;
   for (uint32_t i = tid; i < kLdsImageBytes / 16; i += NT) s_img[i] = t.lds_image[i];
@@ -816,9 +843,48 @@ __global__ __launch_bounds__(LdsClass<N>::threads) void k_bpe_lds(Work w, Tables
   const uint32_t tb0 = blockIdx.x * tiles_per_block, tb1 = min(w.n_tiles, tb0 + tiles_per_block);
   uint32_t st_bytes = 0, st_ids = 0;
   __syncthreads();
+  // length buckets (4 per class): a wavefront's pieces then have similar lengths, hence
+  // similar merge counts, and fewer of its lanes idle while the longest piece finishes
+  constexpr uint32_t blo = N == 8 ? 1 : N / 2 + 1, bw = N == 32 ? 4 : 2;
+  auto bucket = [&](uint32_t n) { return min(3u, (n - blo) / bw); };
   for (uint32_t c0 = tb0; c0 < tb1; c0 += K) {
     const uint32_t E = tile_share_init<K>(counts, tb1, c0, s_pre, s_tsum);
-    for (uint32_t q = tid; q < E; q += NT) {
+    const bool sorted = N > 8 && E <= kSortCap;  // <= 8 B pieces: few merges, sorting does not pay
+    if (sorted) {
+      if (tid < 4) { s_bcnt[tid] = 0; s_bfill[tid] = 0; }
+      __syncthreads();
+      for (uint32_t q = tid; q < E; q += NT) {  // bucket sizes (one LDS add per wave and bucket)
+        const uint32_t kt = tile_of<K>(s_pre, q);
+        const uint32_t b = bucket(list[(size_t)(c0 + kt) * LC::cap + (q - s_pre[kt])] >> 24);
+#pragma unroll
+        for (uint32_t bb = 0; bb < 4; bb++) {
+          const uint64_t m = __ballot(b == bb);
+          if (m && (threadIdx.x & 63) == __ffsll((unsigned long long)m) - 1) atomicAdd(&s_bcnt[bb], (uint32_t)__popcll(m));
+        }
+      }
+      __syncthreads();
+      if (tid == 0) {
+        uint32_t acc = 0;
+        for (int bb = 0; bb < 4; bb++) {
+          const uint32_t c = s_bcnt[bb];
+          s_bfill[bb] = acc;
+          acc += c;
+        }
+      }
+      __syncthreads();
+      for (uint32_t q = tid; q < E; q += NT) {  // scatter entry numbers into bucket order
+        const uint32_t kt = tile_of<K>(s_pre, q);
+        const uint32_t b = bucket(list[(size_t)(c0 + kt) * LC::cap + (q - s_pre[kt])] >> 24);
+#pragma unroll
+        for (uint32_t bb = 0; bb < 4; bb++) {
+          const uint32_t slot = wave_append(&s_bfill[bb], b == bb);
+          if (b == bb) s_perm[slot] = (uint16_t)q;
+        }
+      }
+      __syncthreads();
+    }
+    for (uint32_t i = tid; i < E; i += NT) {
+      const uint32_t q = sorted ? (uint32_t)s_perm[i] : i;
       const uint32_t kt = tile_of<K>(s_pre, q);
       const uint32_t tile = c0 + kt;
       const uint32_t e = list[(size_t)tile * LC::cap + (q - s_pre[kt])];
@@ -1387,10 +1453,6 @@ hipError_t scan_u64(uint64_t* inout, uint64_t n, uint64_t* tmp, uint64_t tmp_cap
 // ------------------------------------------------------------------------------------------
 // NFC (src/normalizers.rs:47): quick check per chunk, exact normalisation per flagged doc.
 
-__device__ __forceinline__ uint16_t nfc16(const Tables& t, uint32_t cp) {
-  if (cp >= 0x110000) return 0;
-  return t.nfc_s2[t.nfc_s1[cp >> 8] * 256 + (cp & 255)];
-}
 
 __device__ __forceinline__ int dev_decode(const uint8_t* s, uint32_t n, uint32_t i, uint32_t* cp) {
   const uint8_t b = s[i];

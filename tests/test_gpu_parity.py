@@ -190,3 +190,18 @@ def test_without_piece_table(gpt2, monkeypatch):
     monkeypatch.delenv("CTOK_NO_PIECE_TABLE")
     text, off = corpus.corpus_c2(30_000, seed=22)
     assert_same(*tok.encode_packed(text, off), *rc.encode_packed(text, off))
+
+
+def test_nfc_speculation_redo(gpt2):
+    """NFC is speculated away for text without NFC-unstable code points; one such code point
+    anywhere in the batch (here: only in the last doc, far from the first tile) makes the
+    library check, normalise and run again.  Both batches must match the oracle exactly."""
+    obj, tok, rc = gpt2
+    text, off = corpus.corpus_c2(20_000, seed=77)
+    ascii_docs = [d.decode() for d in corpus.unpack(text, off)]
+    for tail in ("", "café Å"):
+        docs = ascii_docs + ([tail] if tail else [])
+        got = tok.encode_batch(docs)
+        want = rc.encode_batch(docs)
+        assert got == want, "batch with tail %r differs" % tail
+        assert tok.last_stats is None or tok.last_stats.get("nfc_docs", 0) == (1 if tail else 0)
