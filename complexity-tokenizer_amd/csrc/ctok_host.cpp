@@ -175,7 +175,8 @@ struct DeviceState {
   Tables t{};
   // workspace
   DevBuf<uint32_t> docbits, pbits, tile_np, tile_tok, tcls, list0, list1, list2, tcnt, scratch, counters, lw;
-  DevBuf<uint16_t> wpref, tpos;
+  DevBuf<uint16_t> wpref;
+  DevBuf<uint32_t> long_cnt;
   DevBuf<uint64_t> long_list, mid_list, scan_tmp;
   DevBuf<uint32_t> doc_flag, ncp;
   DevBuf<uint64_t> norm_off;
@@ -769,10 +770,10 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
     ds->list1.ensure(nt * kCap1 + 8);
     ds->list2.ensure(nt * kCap2 + 8);
   }
-  ds->tpos.ensure(nt * kTileSlots + 8);
   ds->tcnt.ensure(nt * kTileSlots + 8);
   ds->scratch.ensure(nt * kTile + 8);  // whole tiles: k_emit gathers unconditionally
   ds->long_list.ensure(B / kShortMax + nt + 8);
+  ds->long_cnt.ensure(B / kShortMax + nt + 8);
   ds->mid_list.ensure(B / 2 + 8);
   ds->lw.ensure(4 * B + 64);
   ds->scan_tmp.ensure(scan_tmp_elems(std::max<uint64_t>(nt + 1, n_docs + 1)) + 64);
@@ -785,7 +786,7 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   w.list0 = ds->list0.p;
   w.list1 = ds->list1.p;
   w.list2 = ds->list2.p;
-  w.tpos = ds->tpos.p;
+  w.long_cnt = ds->long_cnt.p;
   w.tcnt = ds->tcnt.p;
   w.scratch = ds->scratch.p;
   w.long_list = ds->long_list.p;

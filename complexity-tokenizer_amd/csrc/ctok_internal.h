@@ -33,6 +33,14 @@ constexpr uint32_t kCap0 = kTile, kCap1 = (kTile + 8) / 9, kCap2 = (kTile + 16) 
 // List entry (u32): start within the tile [0,12), piece index within the tile [12,24), length [24,30).
 __host__ __device__ inline uint32_t list_entry(uint32_t sl, uint32_t j, uint32_t n) { return sl | (j << 12) | (n << 24); }
 
+// Piece record (tcnt[tile][j], u32), written by whichever pass finishes piece j:
+//   kRecHit | id            one id, the whole-piece probe's (no scratch entry)
+//   kRecLong | li           long piece li: count long_cnt[li], ids at scratch[(u32)long_list[li] ..]
+//   count | start << 16     merged piece (<= 32 B): ids at scratch[tile start + start ..]
+// k_emit turns the records into each piece's first id within the tile (for k_tokoff).
+constexpr uint32_t kRecHit = 0x80000000u, kRecLong = 0x40000000u;
+__host__ __device__ inline uint32_t rec_short(uint32_t count, uint32_t sl) { return count | (sl << 16); }
+
 // 24-bit multiply (v_mul_u32_u24: full rate; a 32-bit v_mul_lo_u32 is quarter rate on CDNA)
 __host__ __device__ inline uint32_t mul24(uint32_t a, uint32_t b) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -132,8 +140,9 @@ struct Work {              // device pointers, sized by the host for one call
   uint32_t* list0;         // [n_tiles * kCap0] (also every <= 32 B piece when added tokens can match)
   uint32_t* list1;         // [n_tiles * kCap1]
   uint32_t* list2;         // [n_tiles * kCap2]
-  uint16_t* tpos;          // [n_tiles * kTileSlots] start (within the tile) of piece j
-  uint32_t* tcnt;          // [n_tiles * kTileSlots] ids of piece j, then (k_emit) its first id within the tile
+  uint32_t* tcnt;          // [n_tiles * kTileSlots] record of piece j (see kRecHit), then (k_emit) its
+                           // first id within the tile
+  uint32_t* long_cnt;      // ids of long piece li
   uint32_t* scratch;       // [n_bytes] ids of the piece starting at byte s at scratch[s ..]
   uint64_t* long_list;     // pieces > kShortMax B (or of unknown length at a tile end): s | j << 32
   uint64_t* mid_list;      // pieces with dropped bytes for the generic kernel: s | j << 32 | n << 48

@@ -11,10 +11,11 @@
 // Data layout in HBM (all offsets u32: one call covers < 4 GiB of text):
 //   text[B] u8, doc_off[D+1] u64 (input) ->
 //   docbits / pbits: 1 bit per byte (doc start / piece start), 4 KiB tiles of 64 64-byte words ->
-//   per tile: wpref (pieces before each word), tpos[j] (start of piece j in the tile), three
-//   class lists of pieces still to merge, tile_np, tile_tok ->
-//   scratch[B] u32: the ids of the piece starting at byte s at scratch[s ...] (ids <= bytes) ->
-//   tcnt[tile][j] ids of piece j, tile_tok scanned to each tile's first id ->
+//   per tile: wpref (pieces before each word), three class lists of pieces still to merge,
+//   tile_np, tile_tok ->
+//   scratch[B] u32: the ids of a merged piece starting at byte s at scratch[s ...] ->
+//   tcnt[tile][j] record of piece j (a whole-piece hit carries its id), tile_tok scanned to each
+//   tile's first id ->
 //   ids[T] u32 + tok_off[D+1] u64 (output).
 // No array is indexed by a global piece number, so no pass has to wait for a global piece count.
 //
@@ -397,7 +398,6 @@ __global__ __launch_bounds__(64 * kSegWaves) void k_segment(Work w, Tables t) {
   // table probes issued together (each round is one dependent global round trip)
   const bool generic = t.n_at != 0;  // added tokens can match inside pieces: no whole-piece shortcut
   uint32_t* tcnt = w.tcnt + (size_t)tile * kTileSlots;
-  uint16_t* tpos = w.tpos + (size_t)tile * kTileSlots;
   const uint64_t trusted_end = (uint64_t)t0 + kTile + 62;  // the look-ahead's bits 0..61
   uint32_t hits = 0;
   uint32_t n0 = 0, n1 = 0, n2 = 0;  // class-list lengths (wave-uniform)
@@ -431,7 +431,6 @@ __global__ __launch_bounds__(64 * kSegWaves) void k_segment(Work w, Tables t) {
           }
           if (el < 0 && (uint64_t)B <= trusted_end) el = (int64_t)B - t0;
         }
-        tpos[j] = (uint16_t)sl[u];
         if (el < 0 || el - sl[u] > kShortMax) {
           cls[u] = 3;
         } else {
@@ -458,15 +457,18 @@ __global__ __launch_bounds__(64 * kSegWaves) void k_segment(Work w, Tables t) {
     const uint32_t hitv[U] = {hit0, hit1, hit2, hit3};
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      if (cls[u] != 5) continue;
-      if (hitv[u] != kNone) {
-        w.scratch[t0 + sl[u]] = hitv[u];
-        tcnt[j0 + 64 * u + lane] = 1;
-        hits++;
-        cls[u] = 4;
-      } else {
-        cls[u] = 0;
+      const uint32_t j = j0 + 64 * u + lane;
+      uint32_t rec = 0;  // placeholder, rewritten by the pass that merges the piece
+      if (cls[u] == 5) {
+        if (hitv[u] != kNone) {
+          rec = kRecHit | hitv[u];
+          hits++;
+          cls[u] = 4;
+        } else {
+          cls[u] = 0;
+        }
       }
+      if (j < np) tcnt[j] = rec;  // every piece's slot: whole coalesced lines
     }
 #pragma unroll
     for (int u = 0; u < U; u++) {
@@ -695,7 +697,7 @@ __global__ __launch_bounds__(256) void k_bpe_generic(Work w, Tables t) {
         pos += nxt;
       }
     }
-    w.tcnt[(size_t)tile * kTileSlots + j] = cnt;
+    w.tcnt[(size_t)tile * kTileSlots + j] = rec_short(cnt, s - tile * kTile);
     if (MID) atomicAdd(&w.tile_tok[tile], cnt);
     else atomicAdd(&s_tsum[kt], cnt);
   }
@@ -935,7 +937,7 @@ __global__ __launch_bounds__(LdsClass<N>::threads) void k_bpe_lds(Work w, Tables
 #pragma unroll
       for (int k = 0; k < N; k++)
         if ((uint32_t)k < m) out[k] = tk[k];
-      w.tcnt[(size_t)tile * kTileSlots + j] = m;
+      w.tcnt[(size_t)tile * kTileSlots + j] = rec_short(m, e & 0xFFFu);
       atomicAdd(&s_tsum[kt], m);
       st_bytes += n;
       st_ids += m;
@@ -1230,7 +1232,8 @@ __global__ __launch_bounds__(256) void k_bpe_long(Work w, Tables t) {
     }
     if (lane == 0) {
       const uint32_t tile = s / kTile;
-      w.tcnt[(size_t)tile * kTileSlots + j] = cnt;
+      w.long_cnt[li] = cnt;
+      w.tcnt[(size_t)tile * kTileSlots + j] = kRecLong | li;
       atomicAdd(&w.tile_tok[tile], cnt);
     }
   }
@@ -1254,6 +1257,10 @@ hipError_t launch_bpe_long(const Work& w, const Tables& t, hipStream_t s) {
 // scratch to ids[] (interleaved: coalesced writes), and leaves each piece's first id (within
 // the tile) in tcnt for k_tokoff.
 
+__device__ __forceinline__ uint32_t rec_count(const Work& w, uint32_t v) {
+  return (v & kRecHit) ? 1u : (v & kRecLong) ? w.long_cnt[v & ~kRecLong] : (v & 0xFFFFu);
+}
+
 __global__ __launch_bounds__(256) void k_emit(Work w, uint32_t* __restrict__ ids, uint64_t ids_cap) {
   __shared__ uint32_t s_scan[17];
   __shared__ uint32_t s_off[kTileSlots + 1];
@@ -1261,7 +1268,6 @@ __global__ __launch_bounds__(256) void k_emit(Work w, uint32_t* __restrict__ ids
   const uint32_t np = w.tile_np[tile];
   const uint64_t base = w.tile_tok[tile];
   uint32_t* tcnt = w.tcnt + (size_t)tile * kTileSlots;
-  const uint16_t* tpos = w.tpos + (size_t)tile * kTileSlots;
   const uint32_t* src0 = w.scratch + (size_t)tile * kTile;
   // 1. thread tid scans pieces [16 tid, 16 tid + 16): four 16-byte loads, one workgroup scan
   constexpr int PER = kTileSlots / 256;
@@ -1277,7 +1283,7 @@ __global__ __launch_bounds__(256) void k_emit(Work w, uint32_t* __restrict__ ids
   uint32_t sum = 0;
 #pragma unroll
   for (int k = 0; k < PER; k++) {
-    c[k] = jb + k < np ? c[k] : 0u;
+    c[k] = jb + k < np ? rec_count(w, c[k]) : 0u;
     sum += c[k];
   }
   uint32_t total;
@@ -1290,39 +1296,47 @@ __global__ __launch_bounds__(256) void k_emit(Work w, uint32_t* __restrict__ ids
     o += c[k];
   }
   if (tid == 0) s_off[np] = total;
-  if (jb < np) {  // each piece's first id within the tile, for k_tokoff
-#pragma unroll
-    for (int k = 0; k < PER / 4; k++)
-      reinterpret_cast<uint4*>(tcnt + jb)[k] = make_uint4(pre[4 * k], pre[4 * k + 1], pre[4 * k + 2], pre[4 * k + 3]);
-  }
   __syncthreads();
-  // 2. copy, piece j = tid + 256 k: consecutive lanes write consecutive ids.  All first-id
-  // loads of a thread's pieces are in flight together; a multi-id piece (rare) then reads its
-  // remaining ids four at a time.
-  uint32_t pos[PER], v[PER];
+  // 2. copy, piece j = tid + 256 k: consecutive lanes write consecutive ids.  A whole-piece hit
+  // carries its id in the record; other pieces read theirs from scratch, all first reads of a
+  // thread's pieces in flight together, the rest (multi-id pieces) four at a time.
+  uint32_t rec[PER];
 #pragma unroll
   for (int k = 0; k < PER; k++) {
     const uint32_t j = tid + 256 * k;
-    pos[k] = j < np ? (uint32_t)tpos[j] : 0u;
+    rec[k] = j < np ? tcnt[j] : kRecHit;
   }
+  auto src_of = [&](uint32_t r) -> const uint32_t* {
+    return (r & kRecLong) ? w.scratch + (uint32_t)w.long_list[r & ~kRecLong] : src0 + ((r >> 16) & 0xFFFu);
+  };
+  uint32_t v0[PER];
 #pragma unroll
-  for (int k = 0; k < PER; k++) v[k] = src0[pos[k]];
+  for (int k = 0; k < PER; k++) {
+    const uint32_t r = rec[k];
+    v0[k] = (r & kRecHit) ? (r & ~kRecHit) : src_of(r)[0];
+  }
 #pragma unroll
   for (int k = 0; k < PER; k++) {
     const uint32_t j = tid + 256 * k;
     if (j >= np) break;
     const uint32_t oj = s_off[j], cj = s_off[j + 1] - oj;
     const uint64_t dst = base + oj;
-    if (cj > 0 && dst < ids_cap) ids[dst] = v[k];
+    if (cj > 0 && dst < ids_cap) ids[dst] = v0[k];
     for (uint32_t m = 1; m < cj; m += 4) {
-      const uint32_t* src = src0 + pos[k] + m;
+      const uint32_t* sp = src_of(rec[k]);
       uint32_t x[4];
 #pragma unroll
-      for (int i = 0; i < 4; i++) x[i] = m + i < cj ? src[i] : 0u;
+      for (int i = 0; i < 4; i++) x[i] = m + i < cj ? sp[m + i] : 0u;
 #pragma unroll
       for (int i = 0; i < 4; i++)
         if (m + i < cj && dst + m + i < ids_cap) ids[dst + m + i] = x[i];  // the host reports CTOK_E_CAPACITY when short
     }
+  }
+  __syncthreads();  // every record has been read: overwrite them with first ids
+  if (jb < np) {  // each piece's first id within the tile, for k_tokoff
+#pragma unroll
+    for (int k = 0; k < PER / 4; k++)
+      reinterpret_cast<uint4*>(tcnt + jb)[k] = make_uint4(pre[4 * k], pre[4 * k + 1], pre[4 * k + 2], pre[4 * k + 3]);
   }
 }
 
