@@ -161,6 +161,8 @@ struct DeviceState {
   hipStream_t stream = nullptr;
   hipEvent_t ev[10] = {};
   hipEvent_t ev_sync = nullptr;   // spin-waited completion marker (no blocking-wait wakeup latency)
+  hipStream_t side = nullptr;     // long-piece pass, overlapped with the short merge passes
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   uint64_t* host = nullptr;       // pinned host words for small device->host readbacks
   // tables
   DevBuf<uint64_t> merge_tab, lds_image;
@@ -190,6 +192,9 @@ struct DeviceState {
       (void)hipSetDevice(device);
       for (auto& e : ev) if (e) (void)hipEventDestroy(e);
       if (ev_sync) (void)hipEventDestroy(ev_sync);
+      if (ev_fork) (void)hipEventDestroy(ev_fork);
+      if (ev_join) (void)hipEventDestroy(ev_join);
+      if (side) (void)hipStreamDestroy(side);
       if (host) (void)hipHostFree(host);
       if (stream) (void)hipStreamDestroy(stream);
     }
@@ -605,6 +610,9 @@ DeviceState* device_state(ctok* t, int device) {
   }
   for (auto& e : ds->ev) HIPTRY(hipEventCreate(&e));
   HIPTRY(hipEventCreateWithFlags(&ds->ev_sync, hipEventDisableTiming));
+  HIPTRY(hipEventCreateWithFlags(&ds->ev_fork, hipEventDisableTiming));
+  HIPTRY(hipEventCreateWithFlags(&ds->ev_join, hipEventDisableTiming));
+  HIPTRY(hipStreamCreateWithFlags(&ds->side, hipStreamNonBlocking));
   HIPTRY(hipHostMalloc((void**)&ds->host, 4096, hipHostMallocDefault));
   hipStream_t s = ds->stream;
   upload(ds->merge_tab, t->merge_tab.data(), t->merge_tab.size(), s);
@@ -797,11 +805,16 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   w.scan_tmp_cap = ds->scan_tmp.cap * 2;
 
   // events: 0 start | 1 segment | 2 class 0 | 3 class 1 | 4 class 2 + dropped-byte pieces |
-  //         5 long pieces | 6 emit
+  //         5 long pieces joined | 6 emit.  The long-piece pass runs on a side stream, forked
+  //         after k_segment and joined before k_emit (it only reads k_segment's output).
   STEP("docstart", launch_docstart(w, s));
   if (timing) HIPTRY(hipEventRecord(ds->ev[7], s));
   STEP("segment", launch_segment(w, tb, s));
   if (timing) HIPTRY(hipEventRecord(ds->ev[1], s));
+  HIPTRY(hipEventRecord(ds->ev_fork, s));
+  HIPTRY(hipStreamWaitEvent(ds->side, ds->ev_fork, 0));
+  STEP("bpe_long", launch_bpe_long(w, tb, ds->side));
+  HIPTRY(hipEventRecord(ds->ev_join, ds->side));
   STEP("bpe0", launch_bpe_class(w, tb, 0, s));
   if (timing) HIPTRY(hipEventRecord(ds->ev[2], s));
   STEP("bpe1", launch_bpe_class(w, tb, 1, s));
@@ -809,7 +822,7 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   STEP("bpe2", launch_bpe_class(w, tb, 2, s));
   STEP("bpe_mid", launch_bpe_class(w, tb, 3, s));
   if (timing) HIPTRY(hipEventRecord(ds->ev[4], s));
-  STEP("bpe_long", launch_bpe_long(w, tb, s));
+  HIPTRY(hipStreamWaitEvent(s, ds->ev_join, 0));
   if (timing) HIPTRY(hipEventRecord(ds->ev[5], s));
   STEP("emit", launch_emit(w, d_ids, ids_cap, d_tok_off, s));
   if (timing) HIPTRY(hipEventRecord(ds->ev[6], s));

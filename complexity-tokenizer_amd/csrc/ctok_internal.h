@@ -148,7 +148,7 @@ struct Work {              // device pointers, sized by the host for one call
   uint64_t* mid_list;      // pieces with dropped bytes for the generic kernel: s | j << 32 | n << 48
   uint32_t* counters;      // [0] long count, [2] err, [3] nfc docs, [4] mid count, [5] pieces (stats),
                            // [6 + 2c], [7 + 2c]: bytes merged / ids produced by class pass c (stats),
-                           // [12] NFC speculation failed
+                           // [12] NFC speculation failed, [13 + c] next chunk of class pass c
   uint32_t* lw;            // long-piece workspace: 4 * n_bytes u32
   uint32_t* scan_tmp;      // scan partials
   uint64_t scan_tmp_cap;

@@ -821,11 +821,11 @@ __device__ __forceinline__ bool merge_slots(const Tables& t, const PairLds& P, u
 }
 
 // Merge pass over one length class (N = 8, 16, 32 slots): a persistent grid, one workgroup per
-// CU holding the merge LDS image; workgroup b takes a contiguous range of tiles and walks its
-// class lists 64 tiles at a time (one concatenated list per chunk, see tile_share_init).
+// CU holding the merge LDS image; workgroups take chunks of 64 tiles from a counter and walk the
+// chunk's class lists as one concatenated list (see tile_share_init).
 // Thread per piece, tokens and pair ranks in registers (fully unrolled, compile-time slots).
 template <int N, bool COMPACT>
-__global__ __launch_bounds__(LdsClass<N>::threads) void k_bpe_lds(Work w, Tables t, uint32_t tiles_per_block) {
+__global__ __launch_bounds__(LdsClass<N>::threads) void k_bpe_lds(Work w, Tables t) {
   using LC = LdsClass<N>;
   constexpr uint32_t NT = LC::threads;
   constexpr int K = 64;
@@ -842,14 +842,21 @@ __global__ __launch_bounds__(LdsClass<N>::threads) void k_bpe_lds(Work w, Tables
   uint32_t* err = &w.counters[2];
   const uint32_t* list = class_list<N>(w);
   const uint32_t* counts = w.tcls + (size_t)LC::cls * w.n_tiles;
-  const uint32_t tb0 = blockIdx.x * tiles_per_block, tb1 = min(w.n_tiles, tb0 + tiles_per_block);
   uint32_t st_bytes = 0, st_ids = 0;
+  __shared__ uint32_t s_chunk;
   __syncthreads();
   // length buckets (4 per class): a wavefront's pieces then have similar lengths, hence
   // similar merge counts, and fewer of its lanes idle while the longest piece finishes
   constexpr uint32_t blo = N == 8 ? 1 : N / 2 + 1, bw = N == 32 ? 4 : 2;
   auto bucket = [&](uint32_t n) { return min(3u, (n - blo) / bw); };
-  for (uint32_t c0 = tb0; c0 < tb1; c0 += K) {
+  // chunks of K tiles dealt dynamically (one atomic per chunk, taken by thread 0 and broadcast
+  // through LDS): workgroups that start late, or whose CU is shared, take fewer chunks
+  for (;;) {
+    if (tid == 0) s_chunk = atomicAdd(&w.counters[13 + LC::cls], 1u);
+    __syncthreads();
+    const uint32_t c0 = s_chunk * K;
+    if (c0 >= w.n_tiles) break;
+    const uint32_t tb1 = min(w.n_tiles, c0 + K);
     const uint32_t E = tile_share_init<K>(counts, tb1, c0, s_pre, s_tsum);
     const bool sorted = N > 8 && E <= kSortCap;  // <= 8 B pieces: few merges, sorting does not pay
     if (sorted) {
@@ -971,9 +978,8 @@ static hipError_t launch_lds(const Work& w, const Tables& t, hipStream_t s) {
     attr = true;
   }
   if (!w.n_tiles) return hipSuccess;
-  const uint32_t grid = min(w.n_tiles, w.n_cus);
-  const uint32_t per = (w.n_tiles + grid - 1) / grid;
-  k_bpe_lds<N, C><<<(w.n_tiles + per - 1) / per, LdsClass<N>::threads, kLdsImageBytes, s>>>(w, t, per);
+  const uint32_t chunks = (w.n_tiles + 63) / 64;
+  k_bpe_lds<N, C><<<min(chunks, w.n_cus), LdsClass<N>::threads, kLdsImageBytes, s>>>(w, t);
   return hipGetLastError();
 }
 
@@ -1240,14 +1246,11 @@ __global__ __launch_bounds__(256) void k_bpe_long(Work w, Tables t) {
 }
 
 hipError_t launch_bpe_long(const Work& w, const Tables& t, hipStream_t s) {
-  static bool attr = false;
-  const size_t lds = 4 * 4 * kLdsPos * sizeof(uint32_t);
-  if (!attr) {
-    HIPCHK(hipFuncSetAttribute((const void*)k_bpe_long<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    attr = true;
-  }
-  k_bpe_long<false><<<256, 256, lds, s>>>(w, t);
-  k_bpe_long<true><<<256, 256, 0, s>>>(w, t);
+  // one wavefront per workgroup (32 KiB of LDS each): a long-piece workgroup fits on a CU next
+  // to a merge-pass workgroup (96 KiB), so this pass overlaps them instead of taking CUs away
+  const size_t lds = 4 * kLdsPos * sizeof(uint32_t);
+  k_bpe_long<false><<<512, 64, lds, s>>>(w, t);
+  k_bpe_long<true><<<128, 256, 0, s>>>(w, t);
   return hipGetLastError();
 }
 
