@@ -151,13 +151,12 @@ def main():
     # Per-kernel rooflines (HIP events on the encode stream, averaged over the timed steps).
     # Algorithmic bytes per launch (DESIGN.md "Measurement"):
     #   k_segment:      text read (B) + doc-start bitmap read (B/8) + piece-start bitmap written (B/8)
-    #   k_bpe_lds<N>:   text bytes of the pieces of its length class + 4 B per id it writes
+    #   merge passes:   text bytes of the pieces of their length classes + 4 B per id written
     cb, ci = st["class_bytes"], st["class_ids"]
     kernels = {
         "k_segment": (avg("ms_segment"), 1.25 * B),
-        "k_bpe_lds<8>": (avg("ms_bpe8"), cb[0] + 4 * ci[0]),
-        "k_bpe_lds<16>": (avg("ms_bpe16"), cb[1] + 4 * ci[1]),
-        "k_bpe_lds<32>": (avg("ms_bpe32"), cb[2] + 4 * ci[2]),
+        "k_bpe_short": (avg("ms_bpe_lo"), cb[0] + cb[1] + 4 * (ci[0] + ci[1])),
+        "k_bpe_c2": (avg("ms_bpe_hi"), cb[2] + 4 * ci[2]),
     }
     dom = max(kernels, key=lambda k: kernels[k][0])
     ms_dom, alg_dom = kernels[dom]

@@ -41,7 +41,7 @@ class Stats(ctypes.Structure):
                 ("ms_d2h", ctypes.c_double), ("bytes_in", ctypes.c_uint64), ("bytes_norm", ctypes.c_uint64),
                 ("docs", ctypes.c_uint64), ("pieces", ctypes.c_uint64), ("long_pieces", ctypes.c_uint64),
                 ("tokens", ctypes.c_uint64), ("nfc_docs", ctypes.c_uint64), ("ms_segment", ctypes.c_double),
-                ("ms_bpe8", ctypes.c_double), ("ms_bpe16", ctypes.c_double), ("ms_bpe32", ctypes.c_double),
+                ("ms_bpe_lo", ctypes.c_double), ("ms_bpe_hi", ctypes.c_double),
                 ("class_bytes", ctypes.c_uint64 * 3), ("class_ids", ctypes.c_uint64 * 3)]
 
     def as_dict(self):

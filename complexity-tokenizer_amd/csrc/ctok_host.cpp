@@ -159,7 +159,7 @@ struct DeviceState {
   uint32_t n_cus = 1;
   std::mutex mu;
   hipStream_t stream = nullptr;
-  hipEvent_t ev[10] = {};
+  hipEvent_t ev[12] = {};
   hipEvent_t ev_sync = nullptr;   // spin-waited completion marker (no blocking-wait wakeup latency)
   hipStream_t side = nullptr;     // long-piece pass, overlapped with the short merge passes
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
@@ -804,9 +804,10 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   w.scan_tmp = (uint32_t*)ds->scan_tmp.p;
   w.scan_tmp_cap = ds->scan_tmp.cap * 2;
 
-  // events: 0 start | 1 segment | 2 class 0 | 3 class 1 | 4 class 2 + dropped-byte pieces |
-  //         5 long pieces joined | 6 emit.  The long-piece pass runs on a side stream, forked
-  //         after k_segment and joined before k_emit (it only reads k_segment's output).
+  // events (main stream s): 0 start | 7 segment start | 1 segment end | 2 <= 16 B merge pass end |
+  //   8, 9 around the 17..32 B pass | 5 side stream joined | 3 dropped-byte pass end | 6 emit end.
+  //   The side stream runs the long-piece pass, forked after k_segment (it reads only its output)
+  //   and joined before the dropped-byte pass (fed by all merge passes) and k_emit.
   STEP("docstart", launch_docstart(w, s));
   if (timing) HIPTRY(hipEventRecord(ds->ev[7], s));
   STEP("segment", launch_segment(w, tb, s));
@@ -815,15 +816,15 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   HIPTRY(hipStreamWaitEvent(ds->side, ds->ev_fork, 0));
   STEP("bpe_long", launch_bpe_long(w, tb, ds->side));
   HIPTRY(hipEventRecord(ds->ev_join, ds->side));
-  STEP("bpe0", launch_bpe_class(w, tb, 0, s));
+  STEP("bpe_short", launch_bpe_class(w, tb, 0, s));
   if (timing) HIPTRY(hipEventRecord(ds->ev[2], s));
-  STEP("bpe1", launch_bpe_class(w, tb, 1, s));
-  if (timing) HIPTRY(hipEventRecord(ds->ev[3], s));
-  STEP("bpe2", launch_bpe_class(w, tb, 2, s));
-  STEP("bpe_mid", launch_bpe_class(w, tb, 3, s));
-  if (timing) HIPTRY(hipEventRecord(ds->ev[4], s));
+  if (timing) HIPTRY(hipEventRecord(ds->ev[8], s));
+  STEP("bpe_c2", launch_bpe_class(w, tb, 2, s));
+  if (timing) HIPTRY(hipEventRecord(ds->ev[9], s));
   HIPTRY(hipStreamWaitEvent(s, ds->ev_join, 0));
   if (timing) HIPTRY(hipEventRecord(ds->ev[5], s));
+  STEP("bpe_mid", launch_bpe_class(w, tb, 3, s));
+  if (timing) HIPTRY(hipEventRecord(ds->ev[3], s));
   STEP("emit", launch_emit(w, d_ids, ids_cap, d_tok_off, s));
   if (timing) HIPTRY(hipEventRecord(ds->ev[6], s));
   if (st && w.n_tiles) STEP("count", launch_count_pieces(w, s));
@@ -861,12 +862,11 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
       };
       st->ms_pretok = el(0, 1);
       st->ms_segment = el(7, 1);
-      st->ms_bpe8 = el(1, 2);
-      st->ms_bpe16 = el(2, 3);
-      st->ms_bpe32 = el(3, 4);
-      st->ms_bpe_short = el(1, 4);
-      st->ms_bpe_long = el(4, 5);
-      st->ms_emit = el(5, 6);
+      st->ms_bpe_lo = el(1, 2);
+      st->ms_bpe_hi = el(8, 9);
+      st->ms_bpe_short = el(1, 9);
+      st->ms_bpe_long = el(9, 5);
+      st->ms_emit = el(3, 6);
       st->ms_device = el(0, 6);
     }
   }

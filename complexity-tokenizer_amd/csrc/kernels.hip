@@ -734,13 +734,19 @@ struct PairLds {
 };
 
 // Rank lookup, LDS stage: the pair's value from the hot table, else kNoRank; `global` is set
-// when the hot table missed and the Bloom filter cannot rule the pair out.
+// when the hot table missed and the Bloom filter cannot rule the pair out.  HOT = false: the
+// Bloom filter only (workgroups that keep 32 KiB of LDS instead of 96).
+template <bool HOT>
 __device__ __forceinline__ uint32_t rank_lds(const PairLds& P, uint32_t a, uint32_t b, uint32_t h1, uint32_t h2,
                                              bool& global) {
-  const uint32_t c1 = 2 * (h1 & (kHotBuckets - 1)), c2 = 2 * (h2 & (kHotBuckets - 1));
-  const uint64_t x0 = P.hot[c1], x1 = P.hot[c1 + 1], y0 = P.hot[c2], y1 = P.hot[c2 + 1];
   const uint32_t b1 = (h1 >> 12) & (kBloomBits - 1), b2 = (h2 >> 12) & (kBloomBits - 1);
   const uint32_t f = (P.bloom[b1 >> 5] >> (b1 & 31)) & (P.bloom[b2 >> 5] >> (b2 & 31)) & 1u;
+  if constexpr (!HOT) {
+    global = f != 0;
+    return kNoRank;
+  }
+  const uint32_t c1 = 2 * (h1 & (kHotBuckets - 1)), c2 = 2 * (h2 & (kHotBuckets - 1));
+  const uint64_t x0 = P.hot[c1], x1 = P.hot[c1 + 1], y0 = P.hot[c2], y1 = P.hot[c2 + 1];
   // entry = value << 42 | a << 21 | b: compare the 42-bit key as (lo 32, hi 10)
   const uint32_t klo = (a << kIdBits) | b, khi = a >> (32 - kIdBits);
   uint32_t v = kNoRank;
@@ -760,9 +766,9 @@ __device__ __forceinline__ uint32_t rank_lds(const PairLds& P, uint32_t a, uint3
 }
 
 template <int N> struct LdsClass;
-template <> struct LdsClass<8> { static constexpr int cls = 0, threads = 1024; static constexpr uint32_t cap = kCap0; };
-template <> struct LdsClass<16> { static constexpr int cls = 1, threads = 1024; static constexpr uint32_t cap = kCap1; };
-template <> struct LdsClass<32> { static constexpr int cls = 2, threads = 512; static constexpr uint32_t cap = kCap2; };
+template <> struct LdsClass<8> { static constexpr int cls = 0; static constexpr uint32_t cap = kCap0; };
+template <> struct LdsClass<16> { static constexpr int cls = 1; static constexpr uint32_t cap = kCap1; };
+template <> struct LdsClass<32> { static constexpr int cls = 2; static constexpr uint32_t cap = kCap2; };
 
 template <int N>
 __device__ __forceinline__ const uint32_t* class_list(const Work& w) {
@@ -774,7 +780,7 @@ __device__ __forceinline__ const uint32_t* class_list(const Work& w) {
 // merged, the slots right of it shift left by one, the two new pairs' ranks are looked up.
 // Returns true when it stopped because the piece shrank to <= stop tokens (the caller continues
 // on fewer slots), false when no pair can merge.  Slots >= m hold kDead / kNoRank.
-template <int N, bool COMPACT>
+template <int N, bool COMPACT, bool HOT>
 __device__ __forceinline__ bool merge_slots(const Tables& t, const PairLds& P, uint32_t* tk, uint32_t* rk,
                                             uint32_t& m, uint32_t stop, uint32_t* err) {
   for (;;) {
@@ -794,8 +800,8 @@ __device__ __forceinline__ bool merge_slots(const Tables& t, const PairLds& P, u
     const bool has_l = bi > 0, has_r = bi + 2 < m;
     const uint32_t hl1 = mhash(L, nid), hr1 = mhash(nid, R);
     bool gl, gr;
-    uint32_t rl = rank_lds(P, L, nid, hl1, mhash2(hl1), gl);
-    uint32_t rr = rank_lds(P, nid, R, hr1, mhash2(hr1), gr);
+    uint32_t rl = rank_lds<HOT>(P, L, nid, hl1, mhash2(hl1), gl);
+    uint32_t rr = rank_lds<HOT>(P, nid, R, hr1, mhash2(hr1), gr);
     gl = gl && has_l;
     gr = gr && has_r;
     uint64_t el = 0, er = 0;
@@ -820,83 +826,81 @@ __device__ __forceinline__ bool merge_slots(const Tables& t, const PairLds& P, u
   }
 }
 
-// Merge pass over one length class (N = 8, 16, 32 slots): a persistent grid, one workgroup per
-// CU holding the merge LDS image; workgroups take chunks of 64 tiles from a counter and walk the
-// chunk's class lists as one concatenated list (see tile_share_init).
-// Thread per piece, tokens and pair ranks in registers (fully unrolled, compile-time slots).
-template <int N, bool COMPACT>
-__global__ __launch_bounds__(LdsClass<N>::threads) void k_bpe_lds(Work w, Tables t) {
+// Workgroup-shared scratch of a merge pass.
+template <uint32_t SORTCAP>
+struct PassLds {
+  uint32_t pre[65], tsum[64], stat[2], bcnt[4], bfill[4], chunk;
+  uint16_t perm[SORTCAP];  // the chunk's entries ordered by length bucket
+};
+
+// Merge pass over one length class (N = 8, 16, 32 slots), run by a persistent grid:
+// workgroups take chunks of 64 tiles from a counter (counters[13 + class]) and walk the chunk's
+// class lists as one concatenated list (see tile_share_init).  Thread per piece, tokens and pair
+// ranks in registers (fully unrolled, compile-time slots).
+template <int N, bool COMPACT, bool HOT, uint32_t NT, uint32_t SORTCAP>
+__device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const PairLds& P, const int32_t* s_b2id,
+                                           PassLds<SORTCAP>& S) {
   using LC = LdsClass<N>;
-  constexpr uint32_t NT = LC::threads;
   constexpr int K = 64;
-  extern __shared__ __attribute__((aligned(16))) uint4 s_img[];
-  __shared__ int32_t s_b2id[256];
-  __shared__ uint32_t s_pre[K + 1], s_tsum[K], s_stat[2];
-  __shared__ uint32_t s_bcnt[4], s_bfill[4];
-  __shared__ uint16_t s_perm[kSortCap];  // the chunk's entries ordered by length bucket
   const uint32_t tid = threadIdx.x;
-  if (tid < 2) s_stat[tid] = 0;
-  for (uint32_t i = tid; i < kLdsImageBytes / 16; i += NT) s_img[i] = t.lds_image[i];
-  for (uint32_t i = tid; i < 256; i += NT) s_b2id[i] = t.byte2id[i];
-  const PairLds P{(const lds_u64*)s_img, (const lds_u32*)(s_img + kHotBuckets)};
   uint32_t* err = &w.counters[2];
   const uint32_t* list = class_list<N>(w);
   const uint32_t* counts = w.tcls + (size_t)LC::cls * w.n_tiles;
   uint32_t st_bytes = 0, st_ids = 0;
-  __shared__ uint32_t s_chunk;
-  __syncthreads();
+  if (tid < 2) S.stat[tid] = 0;
   // length buckets (4 per class): a wavefront's pieces then have similar lengths, hence
   // similar merge counts, and fewer of its lanes idle while the longest piece finishes
   constexpr uint32_t blo = N == 8 ? 1 : N / 2 + 1, bw = N == 32 ? 4 : 2;
   auto bucket = [&](uint32_t n) { return min(3u, (n - blo) / bw); };
   // chunks of K tiles dealt dynamically (one atomic per chunk, taken by thread 0 and broadcast
   // through LDS): workgroups that start late, or whose CU is shared, take fewer chunks
+  __syncthreads();
   for (;;) {
-    if (tid == 0) s_chunk = atomicAdd(&w.counters[13 + LC::cls], 1u);
+    if (tid == 0) S.chunk = atomicAdd(&w.counters[13 + LC::cls], 1u);
     __syncthreads();
-    const uint32_t c0 = s_chunk * K;
+    const uint32_t c0 = S.chunk * K;
     if (c0 >= w.n_tiles) break;
     const uint32_t tb1 = min(w.n_tiles, c0 + K);
-    const uint32_t E = tile_share_init<K>(counts, tb1, c0, s_pre, s_tsum);
-    const bool sorted = N > 8 && E <= kSortCap;  // <= 8 B pieces: few merges, sorting does not pay
+    const uint32_t E = tile_share_init<K>(counts, tb1, c0, S.pre, S.tsum);
+    const bool sorted = N > 8 && E <= SORTCAP;  // <= 8 B pieces: few merges, sorting does not pay
     if (sorted) {
-      if (tid < 4) { s_bcnt[tid] = 0; s_bfill[tid] = 0; }
+      if (tid < 4) { S.bcnt[tid] = 0; S.bfill[tid] = 0; }
       __syncthreads();
       for (uint32_t q = tid; q < E; q += NT) {  // bucket sizes (one LDS add per wave and bucket)
-        const uint32_t kt = tile_of<K>(s_pre, q);
-        const uint32_t b = bucket(list[(size_t)(c0 + kt) * LC::cap + (q - s_pre[kt])] >> 24);
+        const uint32_t kt = tile_of<K>(S.pre, q);
+        const uint32_t b = bucket(list[(size_t)(c0 + kt) * LC::cap + (q - S.pre[kt])] >> 24);
 #pragma unroll
         for (uint32_t bb = 0; bb < 4; bb++) {
           const uint64_t m = __ballot(b == bb);
-          if (m && (threadIdx.x & 63) == __ffsll((unsigned long long)m) - 1) atomicAdd(&s_bcnt[bb], (uint32_t)__popcll(m));
+          if (m && (threadIdx.x & 63) == __ffsll((unsigned long long)m) - 1) atomicAdd(&S.bcnt[bb], (uint32_t)__popcll(m));
         }
       }
       __syncthreads();
       if (tid == 0) {
         uint32_t acc = 0;
         for (int bb = 0; bb < 4; bb++) {
-          const uint32_t c = s_bcnt[bb];
-          s_bfill[bb] = acc;
+          const uint32_t c = S.bcnt[bb];
+          S.bfill[bb] = acc;
           acc += c;
         }
       }
       __syncthreads();
       for (uint32_t q = tid; q < E; q += NT) {  // scatter entry numbers into bucket order
-        const uint32_t kt = tile_of<K>(s_pre, q);
-        const uint32_t b = bucket(list[(size_t)(c0 + kt) * LC::cap + (q - s_pre[kt])] >> 24);
+        const uint32_t kt = tile_of<K>(S.pre, q);
+        const uint32_t b = bucket(list[(size_t)(c0 + kt) * LC::cap + (q - S.pre[kt])] >> 24);
 #pragma unroll
         for (uint32_t bb = 0; bb < 4; bb++) {
-          const uint32_t slot = wave_append(&s_bfill[bb], b == bb);
-          if (b == bb) s_perm[slot] = (uint16_t)q;
+          const uint32_t slot = wave_append(&S.bfill[bb], b == bb);
+          if (b == bb) S.perm[slot] = (uint16_t)q;
         }
       }
       __syncthreads();
     }
     for (uint32_t i = tid; i < E; i += NT) {
-      const uint32_t q = sorted ? (uint32_t)s_perm[i] : i;
-      const uint32_t kt = tile_of<K>(s_pre, q);
+      const uint32_t q = sorted ? (uint32_t)S.perm[i] : i;
+      const uint32_t kt = tile_of<K>(S.pre, q);
       const uint32_t tile = c0 + kt;
-      const uint32_t e = list[(size_t)tile * LC::cap + (q - s_pre[kt])];
+      const uint32_t e = list[(size_t)tile * LC::cap + (q - S.pre[kt])];
       const uint32_t s = tile * kTile + (e & 0xFFFu);
       const uint32_t j = (e >> 12) & 0xFFFu;
       const uint32_t n = e >> 24;
@@ -935,21 +939,21 @@ __global__ __launch_bounds__(LdsClass<N>::threads) void k_bpe_lds(Work w, Tables
       uint32_t m = n;
       // tiers: N slots while the piece has more than N/2 tokens, then N/2, ... down to 8 slots
       bool more = true;
-      if constexpr (N >= 32) more = merge_slots<32, COMPACT>(t, P, tk, rk, m, 16, err);
+      if constexpr (N >= 32) more = merge_slots<32, COMPACT, HOT>(t, P, tk, rk, m, 16, err);
       if constexpr (N >= 16) {
-        if (more) more = merge_slots<16, COMPACT>(t, P, tk, rk, m, 8, err);
+        if (more) more = merge_slots<16, COMPACT, HOT>(t, P, tk, rk, m, 8, err);
       }
-      if (more) merge_slots<8, COMPACT>(t, P, tk, rk, m, 0, err);
+      if (more) merge_slots<8, COMPACT, HOT>(t, P, tk, rk, m, 0, err);
       uint32_t* out = w.scratch + s;
 #pragma unroll
       for (int k = 0; k < N; k++)
         if ((uint32_t)k < m) out[k] = tk[k];
       w.tcnt[(size_t)tile * kTileSlots + j] = rec_short(m, e & 0xFFFu);
-      atomicAdd(&s_tsum[kt], m);
+      atomicAdd(&S.tsum[kt], m);
       st_bytes += n;
       st_ids += m;
     }
-    tile_share_flush<K>(w, c0, s_tsum);
+    tile_share_flush<K>(w, c0, S.tsum);
     __syncthreads();
   }
   // statistics: bytes merged and ids produced by this pass (algorithmic bytes for the roofline)
@@ -959,27 +963,65 @@ __global__ __launch_bounds__(LdsClass<N>::threads) void k_bpe_lds(Work w, Tables
     st_ids += (uint32_t)__shfl_xor((int)st_ids, o, 64);
   }
   if ((tid & 63) == 0) {
-    atomicAdd(&s_stat[0], st_bytes);
-    atomicAdd(&s_stat[1], st_ids);
+    atomicAdd(&S.stat[0], st_bytes);
+    atomicAdd(&S.stat[1], st_ids);
   }
   __syncthreads();
   if (tid == 0) {
-    atomicAdd(&w.counters[6 + 2 * LC::cls], s_stat[0]);
-    atomicAdd(&w.counters[7 + 2 * LC::cls], s_stat[1]);
+    atomicAdd(&w.counters[6 + 2 * LC::cls], S.stat[0]);
+    atomicAdd(&w.counters[7 + 2 * LC::cls], S.stat[1]);
   }
+  __syncthreads();
 }
 
-template <int N, bool C>
-static hipError_t launch_lds(const Work& w, const Tables& t, hipStream_t s) {
+// Pieces of <= 16 bytes (classes 0 and 1): one 1024-thread workgroup per CU holding the whole
+// LDS image (hot table + Bloom filter); a workgroup moves on to class 1 as soon as class 0 has
+// no chunk left, with no kernel boundary in between.
+template <bool COMPACT>
+__global__ __launch_bounds__(1024) void k_bpe_short(Work w, Tables t) {
+  extern __shared__ __attribute__((aligned(16))) uint4 s_img[];
+  __shared__ int32_t s_b2id[256];
+  __shared__ PassLds<kSortCap> S;
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t i = tid; i < kLdsImageBytes / 16; i += 1024) s_img[i] = t.lds_image[i];
+  for (uint32_t i = tid; i < 256; i += 1024) s_b2id[i] = t.byte2id[i];
+  const PairLds P{(const lds_u64*)s_img, (const lds_u32*)(s_img + kHotBuckets)};
+  class_pass<8, COMPACT, true, 1024, kSortCap>(w, t, P, s_b2id, S);
+  class_pass<16, COMPACT, true, 1024, kSortCap>(w, t, P, s_b2id, S);
+}
+
+// Pieces of 17..32 bytes (class 2, ~0.5% of pieces): 512-thread workgroups (32 slots need the
+// registers) with the Bloom filter only in LDS (32 KiB).
+template <bool COMPACT>
+__global__ __launch_bounds__(512) void k_bpe_c2(Work w, Tables t) {
+  extern __shared__ __attribute__((aligned(16))) uint4 s_img[];
+  __shared__ int32_t s_b2id[256];
+  __shared__ PassLds<2048> S;
+  const uint32_t tid = threadIdx.x;
+  const uint4* bloom = t.lds_image + kHotBuckets;  // the image's Bloom half
+  for (uint32_t i = tid; i < kBloomWords / 4; i += 512) s_img[i] = bloom[i];
+  for (uint32_t i = tid; i < 256; i += 512) s_b2id[i] = t.byte2id[i];
+  const PairLds P{nullptr, (const lds_u32*)s_img};
+  class_pass<32, COMPACT, false, 512, 2048>(w, t, P, s_b2id, S);
+}
+
+template <bool C>
+static hipError_t launch_short(const Work& w, const Tables& t, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
-    HIPCHK(hipFuncSetAttribute((const void*)k_bpe_lds<N, C>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    HIPCHK(hipFuncSetAttribute((const void*)k_bpe_short<C>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)kLdsImageBytes));
     attr = true;
   }
   if (!w.n_tiles) return hipSuccess;
-  const uint32_t chunks = (w.n_tiles + 63) / 64;
-  k_bpe_lds<N, C><<<min(chunks, w.n_cus), LdsClass<N>::threads, kLdsImageBytes, s>>>(w, t);
+  k_bpe_short<C><<<min((w.n_tiles + 63) / 64, w.n_cus), 1024, kLdsImageBytes, s>>>(w, t);
+  return hipGetLastError();
+}
+
+template <bool C>
+static hipError_t launch_c2(const Work& w, const Tables& t, hipStream_t s) {
+  if (!w.n_tiles) return hipSuccess;
+  k_bpe_c2<C><<<min((w.n_tiles + 63) / 64, w.n_cus), 512, kBloomWords * 4, s>>>(w, t);
   return hipGetLastError();
 }
 
@@ -989,12 +1031,13 @@ hipError_t launch_bpe_class(const Work& w, const Tables& t, int cls, hipStream_t
     return hipGetLastError();
   }
   switch (cls) {
-    case 0: return t.compact ? launch_lds<8, true>(w, t, s) : launch_lds<8, false>(w, t, s);
-    case 1: return t.compact ? launch_lds<16, true>(w, t, s) : launch_lds<16, false>(w, t, s);
-    case 2: return t.compact ? launch_lds<32, true>(w, t, s) : launch_lds<32, false>(w, t, s);
-    default:  // pieces with dropped bytes, found by the merge passes
+    case 0: return t.compact ? launch_short<true>(w, t, s) : launch_short<false>(w, t, s);  // classes 0 and 1
+    case 2: return t.compact ? launch_c2<true>(w, t, s) : launch_c2<false>(w, t, s);
+    case 3:  // pieces with dropped bytes, found by the merge passes
       k_bpe_generic<true><<<64, 256, 0, s>>>(w, t);
       return hipGetLastError();
+    default:
+      return hipSuccess;
   }
 }
 

@@ -71,18 +71,18 @@ typedef struct ctok_stats {
   double ms_total;        /* wall time of the call (host clock)                        */
   double ms_device;       /* first kernel start -> last kernel end (HIP events)        */
   double ms_pretok;       /* normalise check + doc bitmap + pre-tokenizer/routing      */
-  double ms_bpe_short;    /* BPE merge kernels, pieces <= 32 bytes (thread per piece)  */
-  double ms_bpe_long;     /* BPE merge kernels, longer pieces (wavefront per piece)    */
+  double ms_bpe_short;    /* merge passes of pieces <= 32 bytes                          */
+  double ms_bpe_long;     /* wait for the long-piece pass (side stream) after them       */
   double ms_emit;         /* tile token scan + id emission + tok_off                   */
   double ms_h2d, ms_d2h;  /* host-buffer copies (ctok_encode_batch only)               */
   uint64_t bytes_in;      /* raw UTF-8 bytes of the batch                              */
   uint64_t bytes_norm;    /* bytes after normalisation / prefix space                  */
   uint64_t docs, pieces, long_pieces, tokens, nfc_docs;
   double ms_segment;      /* k_segment alone: piece starts + whole-piece probes/routing */
-  double ms_bpe8, ms_bpe16, ms_bpe32;  /* merge pass per length class (<= 8, 9..16, 17..32 B;
-                                          ms_bpe32 includes the dropped-byte generic pass) */
-  uint64_t class_bytes[3];  /* text bytes merged by each length-class pass                 */
-  uint64_t class_ids[3];    /* ids produced by each length-class pass                      */
+  double ms_bpe_lo;       /* k_bpe_short: pieces of <= 16 bytes (classes 0 and 1)        */
+  double ms_bpe_hi;       /* k_bpe_c2: pieces of 17..32 bytes (Bloom filter only in LDS) */
+  uint64_t class_bytes[3];  /* text bytes merged per length class (<= 8, 9..16, 17..32 B) */
+  uint64_t class_ids[3];    /* ids produced per length class                             */
 } ctok_stats;
 
 /* Upper bound on the ids of a batch whose docs total `n_bytes` bytes (ids <= 3*bytes + docs:
