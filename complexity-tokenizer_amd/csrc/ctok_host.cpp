@@ -509,7 +509,7 @@ void load(ctok* t, const char* buf, size_t len) {
     }
     size_t pcap = 1024;
     while (pcap < ents.size() * 2 + 16) pcap <<= 1;
-    t->piece_tab.assign(pcap * 4, 0);
+    t->piece_tab.assign((pcap + 1) * 4, 0);  // + one slot that stays empty (k_segment's no-probe lanes)
     t->piece_mask = (uint32_t)(pcap - 1);
     for (const auto& e : ents) {
       uint64_t v = 0;

@@ -93,7 +93,7 @@ struct Tables {            // device pointers, owned by the host runtime
   uint32_t merge_mask;     // capacity - 1 (power of two)
   const uint4* lds_image;  // hot table + Bloom filter (kLdsImageBytes), copied to LDS by the merge passes
   const uint32_t* pair0;   // [256 * 256] merge-table value of the byte pair (a, b), kNoRank if none
-  const uint4* piece_tab;  // whole-piece table (see piece_hash)
+  const uint4* piece_tab;  // whole-piece table (see piece_hash), piece_mask + 2 slots (the last stays empty)
   uint32_t piece_mask;
   const uint32_t* rank_newid;
   uint32_t n_ranks;

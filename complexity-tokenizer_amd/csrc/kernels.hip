@@ -268,15 +268,13 @@ __device__ __forceinline__ uint32_t select_bit(uint64_t x, uint32_t k) {
 //     9..16 B, 17..32 B) or to the long list, so that the merge passes run dense, length-uniform
 //     waves.
 __global__ __launch_bounds__(64 * kSegWaves) void k_segment(Work w, Tables t) {
-  __shared__ uint64_t s_st_all[kSegWaves][64];
-  __shared__ uint32_t s_wpre_all[kSegWaves][64];
+  __shared__ uint16_t s_pos_all[kSegWaves][64 * kSegUnroll + 8];  // one round's piece starts
   __shared__ uint32_t s_text_all[kSegWaves][(kTileWords + 1) * 16 + 4];  // the tile + look-ahead word
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wid = uni(threadIdx.x >> 6);
   const uint32_t tile = uni(blockIdx.x * kSegWaves + wid);
   if (tile >= w.n_tiles) return;
-  uint64_t* s_st = s_st_all[wid];
-  uint32_t* s_wpre = s_wpre_all[wid];
+  uint16_t* s_pos = s_pos_all[wid];
   const uint32_t B = w.n_bytes;
   const uint32_t t0 = tile * kTile;
   const int64_t g = (int64_t)tile * kTileWords - 1 + lane;  // this lane's word
@@ -380,29 +378,41 @@ __global__ __launch_bounds__(64 * kSegWaves) void k_segment(Work w, Tables t) {
   }
   const uint32_t c = (!first && !last) ? (uint32_t)__popcll(st) : 0u;
   const uint32_t inc = wave_incl_scan(c);
-  // tile word wi = lane - 1: s_st[wi], s_wpre[wi] = pieces before it; s_wpre[62] = s_wpre[63] = np
-  if (!first) {
-    s_st[lane - 1] = st;
-    s_wpre[lane - 1] = inc - c;
-    w.wpref[(size_t)tile * 64 + lane - 1] = (uint16_t)(inc - c);
-  } else {
-    s_st[63] = 0;
-  }
+  if (!first && !last) w.wpref[(size_t)tile * 64 + lane - 1] = (uint16_t)(inc - c);
   const uint32_t np = uni((uint32_t)__shfl((int)inc, 63, 64));
-  if (first) s_wpre[63] = np;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // where the tile's last piece ends (look-ahead lane): 0xFFFF = unknown (longer than the
+  // look-ahead can tell: a long piece)
+  const uint32_t tile_end =
+      uni((uint32_t)__shfl((int)(st ? (uint32_t)(kTileWords * 64 + __builtin_ctzll(st))
+                                    : ((uint64_t)B <= (uint64_t)t0 + kTile + 62 ? (uint32_t)(B - t0) : 0xFFFFu)),
+                           63, 64));
+  // expansion state: each tile word's lane emits the starts of its not yet emitted pieces
+  uint64_t rem = (!first && !last) ? st : 0ull;
+  uint32_t jj = inc - c;
+  const uint32_t wbase = (lane - 1) * 64;
 
   // ---- C: thread per piece, kSegUnroll pieces per lane per round with their LDS lookups and
   // table probes issued together (each round is one dependent global round trip)
   const bool generic = t.n_at != 0;  // added tokens can match inside pieces: no whole-piece shortcut
   uint32_t* tcnt = w.tcnt + (size_t)tile * kTileSlots;
-  const uint64_t trusted_end = (uint64_t)t0 + kTile + 62;  // the look-ahead's bits 0..61
   uint32_t hits = 0;
   uint32_t n0 = 0, n1 = 0, n2 = 0;  // class-list lengths (wave-uniform)
   constexpr int U = kSegUnroll;
-  for (uint32_t j0 = 0; j0 < np; j0 += 64 * U) {
+  constexpr uint32_t W = 64 * U;  // pieces per round
+  for (uint32_t j0 = 0; j0 < np; j0 += W) {
+    // expansion of this round's window [j0, j0 + W]: s_pos[j - j0] = start of piece j (the
+    // entry past the window is the next round's first piece, peeked, not consumed)
+    const uint32_t jend = min(j0 + W, np);
+    while (rem && jj <= jend) {
+      s_pos[jj - j0] = (uint16_t)(wbase + __builtin_ctzll(rem));
+      if (jj == j0 + W) break;
+      rem &= rem - 1;
+      jj++;
+    }
+    if (lane == 0 && np <= j0 + W) s_pos[np - j0] = (uint16_t)tile_end;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     uint32_t sl[U], n[U], cls[U], plo[U], phi[U], h[U];
 #pragma unroll
     for (int u = 0; u < U; u++) {
@@ -411,30 +421,12 @@ __global__ __launch_bounds__(64 * kSegWaves) void k_segment(Work w, Tables t) {
       n[u] = 0;
       cls[u] = 4;  // 0..2 class lists, 3 long, 4 done (or inactive), 5 probe
       if (j < np) {
-        // word of piece j: the last wi with s_wpre[wi] <= j (s_wpre[62] = s_wpre[63] = np > j)
-        uint32_t lo = 0;
-#pragma unroll
-        for (uint32_t step = 32; step >= 1; step >>= 1)
-          if (s_wpre[lo + step] <= j) lo += step;
-        const uint64_t xw = s_st[lo];
-        const uint32_t bit = select_bit(xw, j - s_wpre[lo]);
-        sl[u] = lo * 64 + bit;
-        // end: the next start (this word, a later word, or the look-ahead word)
-        const uint64_t rest = bit == 63 ? 0ull : (xw >> (bit + 1));
-        int64_t el = -1;
-        if (rest) {
-          el = sl[u] + 1 + __builtin_ctzll(rest);
-        } else {
-          for (uint32_t v = lo + 1; v <= kTileWords; v++) {
-            const uint64_t y = s_st[v];
-            if (y) { el = v * 64 + __builtin_ctzll(y); break; }
-          }
-          if (el < 0 && (uint64_t)B <= trusted_end) el = (int64_t)B - t0;
-        }
-        if (el < 0 || el - sl[u] > kShortMax) {
+        sl[u] = s_pos[64 * u + lane];
+        const uint32_t el = s_pos[64 * u + lane + 1];
+        if (el == 0xFFFFu || el - sl[u] > kShortMax) {
           cls[u] = 3;
         } else {
-          n[u] = (uint32_t)(el - sl[u]);
+          n[u] = el - sl[u];
           cls[u] = generic ? 0 : n[u] > 16 ? 2 : n[u] > 8 ? 1 : 5;
         }
       }
@@ -445,28 +437,34 @@ __global__ __launch_bounds__(64 * kSegWaves) void k_segment(Work w, Tables t) {
       const uint32_t nn = n[u];
       plo[u] = nn >= 4 ? w0 : w0 & ((1u << (8 * nn)) - 1u);
       phi[u] = nn >= 8 ? w1 : nn <= 4 ? 0u : w1 & ((1u << (8 * (nn - 4))) - 1u);
-      h[u] = piece_hash(plo[u], phi[u], nn) & t.piece_mask;
+      // lanes without a probe read the spare empty slot past the table (one shared line)
+      h[u] = cls[u] == 5 ? piece_hash(plo[u], phi[u], nn) & t.piece_mask : t.piece_mask + 1;
     }
-    static_assert(U == 4, "the probes below are unrolled by hand");
-    // all first probes in flight together
-    const uint4 e0 = t.piece_tab[h[0]], e1 = t.piece_tab[h[1]], e2 = t.piece_tab[h[2]], e3 = t.piece_tab[h[3]];
-    const uint32_t hit0 = piece_probe(t, e0, h[0], plo[0], phi[0], n[0]);
-    const uint32_t hit1 = piece_probe(t, e1, h[1], plo[1], phi[1], n[1]);
-    const uint32_t hit2 = piece_probe(t, e2, h[2], plo[2], phi[2], n[2]);
-    const uint32_t hit3 = piece_probe(t, e3, h[3], plo[3], phi[3], n[3]);
-    const uint32_t hitv[U] = {hit0, hit1, hit2, hit3};
+    // all first probes in flight together (unrolled by hand: a loop over u around the probing
+    // loop would not unroll, and the arrays would go to scratch)
+    uint32_t hitv[U];
+#define CTOK_PROBE_LOAD(u) const uint4 e##u = t.piece_tab[h[u]];
+#define CTOK_PROBE_USE(u) hitv[u] = piece_probe(t, e##u, h[u], plo[u], phi[u], n[u]);
+    static_assert(U == 4 || U == 8, "kSegUnroll: 4 or 8");
+    CTOK_PROBE_LOAD(0) CTOK_PROBE_LOAD(1) CTOK_PROBE_LOAD(2) CTOK_PROBE_LOAD(3)
+    if constexpr (U == 8) {
+      CTOK_PROBE_LOAD(4) CTOK_PROBE_LOAD(5) CTOK_PROBE_LOAD(6) CTOK_PROBE_LOAD(7)
+      CTOK_PROBE_USE(4) CTOK_PROBE_USE(5) CTOK_PROBE_USE(6) CTOK_PROBE_USE(7)
+    }
+    CTOK_PROBE_USE(0) CTOK_PROBE_USE(1) CTOK_PROBE_USE(2) CTOK_PROBE_USE(3)
+#undef CTOK_PROBE_LOAD
+#undef CTOK_PROBE_USE
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const uint32_t j = j0 + 64 * u + lane;
       uint32_t rec = 0;  // placeholder, rewritten by the pass that merges the piece
+      // (written as flag arithmetic: an if / else-if chain assigning cls[u] in each arm was
+      // miscompiled by this hipcc in the unrolled loop)
       if (cls[u] == 5) {
-        if (hitv[u] != kNone) {
-          rec = kRecHit | hitv[u];
-          hits++;
-          cls[u] = 4;
-        } else {
-          cls[u] = 0;
-        }
+        const bool hit = hitv[u] != kNone;
+        rec = hit ? kRecHit | hitv[u] : 0u;
+        hits += hit ? 1u : 0u;
+        cls[u] = hit ? 4u : 0u;
       }
       if (j < np) tcnt[j] = rec;  // every piece's slot: whole coalesced lines
     }
@@ -493,6 +491,10 @@ __global__ __launch_bounds__(64 * kSegWaves) void k_segment(Work w, Tables t) {
         if (cls[u] == 3) w.long_list[b + __popcll(lm & lanemask_lt())] = (uint64_t)(t0 + sl[u]) | ((uint64_t)j << 32);
       }
     }
+    // every lane has read this round's s_pos before the next round's expansion overwrites it
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) hits += (uint32_t)__shfl_xor((int)hits, o, 64);
