@@ -173,7 +173,9 @@ def main():
         traffic = None  # HBM bytes per launch of the dominant kernel from the committed PMC passes
         tr_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(tr_path):
-            traffic = json.load(open(tr_path)).get("hbm_bytes_per_launch", {}).get(dom)
+            per = json.load(open(tr_path)).get("hbm_bytes_per_launch", {})
+            hits = [v for k, v in per.items() if k.split("<")[0] == dom]
+            traffic = hits[0] if len(hits) == 1 else None
         ms_step = elapsed_max / args.steps * 1e3
         out = {
             "metric": METRIC,

@@ -454,3 +454,231 @@ int64_t ref_pieces(const uint8_t* s, uint64_t n, uint64_t* ends) {
   for (uint64_t i = 0; i < n;) { uint64_t e = gpt2_match(s, n, i); ends[k++] = e; i = e; }
   return k;
 }
+
+/* ================================================================== decode
+ * decode_batch_with_options (src/huggingface/mod.rs:771-785) -> decode_impl (:710-747) per doc,
+ * with the reference's cost model: a filtered id Vec when skipping special tokens (a string-keyed
+ * HashMap probe per id, :716-726), one String clone per id (:729-732), the ByteLevel decoder's
+ * unicode_to_bytes() HashMap rebuilt per doc with the O(256*188) `contains` loop
+ * (src/decoders.rs:74-92, called from :96), a char-keyed HashMap probe per char (:101-116),
+ * from_utf8_lossy (:118), then the 15 allocating `replace` passes and split_whitespace/join of
+ * clean_up_tokenization_spaces (:749-767); rayon-like doc parallelism. */
+typedef struct ref_dec {
+  char** tok; uint32_t* tok_len; uint64_t n_ids;   /* Vocab::id_to_token (model.vocab only) */
+  smap special;                                    /* special added tokens by content */
+  int kind;                                        /* 1 ByteLevel, 0 raw concatenation */
+} ref_dec;
+
+ref_dec* ref_dec_create(const char* const* tok, const uint32_t* tok_len, const uint8_t* has_tok, uint64_t n_ids,
+                        const char* const* special, const uint32_t* special_len, int64_t n_special, int kind) {
+  ref_dec* d = (ref_dec*)calloc(1, sizeof(ref_dec));
+  d->n_ids = n_ids; d->kind = kind;
+  d->tok = (char**)calloc(n_ids + 1, sizeof(char*));
+  d->tok_len = (uint32_t*)calloc(n_ids + 1, 4);
+  for (uint64_t i = 0; i < n_ids; i++)
+    if (has_tok[i]) {
+      d->tok[i] = (char*)malloc(tok_len[i] + 1);
+      memcpy(d->tok[i], tok[i], tok_len[i]);
+      d->tok_len[i] = tok_len[i];
+    }
+  smap_init(&d->special, (uint64_t)n_special);
+  for (int64_t i = 0; i < n_special; i++) smap_put(&d->special, special[i], special_len[i], 1);
+  return d;
+}
+
+void ref_dec_destroy(ref_dec* d) {
+  if (!d) return;
+  for (uint64_t i = 0; i < d->n_ids; i++) free(d->tok[i]);
+  free(d->tok); free(d->tok_len);
+  for (uint64_t i = 0; i < d->special.cap; i++) free(d->special.e[i].key);
+  free(d->special.e); free(d);
+}
+
+/* char -> byte HashMap of unicode_to_bytes (open addressing on the code point) */
+typedef struct { uint32_t key[512]; uint8_t val[512]; uint8_t used[512]; } cmap;
+static uint32_t chash(uint32_t c) { return (uint32_t)(mix64(c) & 511); }
+static void cmap_put(cmap* m, uint32_t c, uint8_t b) {
+  uint32_t i = chash(c);
+  while (m->used[i] && m->key[i] != c) i = (i + 1) & 511;
+  m->used[i] = 1; m->key[i] = c; m->val[i] = b;
+}
+static int cmap_get(const cmap* m, uint32_t c, uint8_t* b) {
+  uint32_t i = chash(c);
+  while (m->used[i]) { if (m->key[i] == c) { *b = m->val[i]; return 1; } i = (i + 1) & 511; }
+  return 0;
+}
+static void unicode_to_bytes(cmap* m) {  /* src/decoders.rs:74-92, the Vec::contains loop kept */
+  uint8_t bs[256]; uint32_t cs[256]; int nb = 0;
+  for (int b = '!'; b <= '~'; b++) bs[nb++] = (uint8_t)b;
+  for (int b = 0xA1; b <= 0xAC; b++) bs[nb++] = (uint8_t)b;
+  for (int b = 0xAE; b <= 0xFF; b++) bs[nb++] = (uint8_t)b;
+  for (int i = 0; i < nb; i++) cs[i] = bs[i];
+  uint32_t n = 0; int base = nb;
+  for (int b = 0; b < 256; b++) {
+    int found = 0;
+    for (int k = 0; k < nb; k++) if (bs[k] == b) { found = 1; break; }
+    if (!found) { bs[nb] = (uint8_t)b; cs[nb] = 256 + n; nb++; n++; }
+  }
+  (void)base;
+  memset(m, 0, sizeof(*m));
+  for (int i = 0; i < nb; i++) cmap_put(m, cs[i], bs[i]);
+}
+
+/* String::from_utf8_lossy (core::str::lossy::Utf8Chunks) */
+static void utf8_lossy(const uint8_t* v, uint64_t n, bbuf* out) {
+  uint64_t i = 0;
+  while (i < n) {
+    uint64_t start = i;
+    uint8_t c = v[i++];
+    if (c < 0x80) { bput(out, (const char*)&c, 1); continue; }
+#define NX(k) ((k) < n ? v[k] : 0)
+#define CONT(x) ((x) >= 0x80 && (x) <= 0xBF)
+    int ok = 0;
+    if (c >= 0xC2 && c <= 0xDF) {
+      if (CONT(NX(i))) { i++; ok = 1; }
+    } else if (c >= 0xE0 && c <= 0xEF) {
+      uint8_t c1 = NX(i);
+      if ((c == 0xE0 && c1 >= 0xA0 && c1 <= 0xBF) || (c >= 0xE1 && c <= 0xEC && CONT(c1)) ||
+          (c == 0xED && c1 >= 0x80 && c1 <= 0x9F) || (c >= 0xEE && CONT(c1))) {
+        i++;
+        if (CONT(NX(i))) { i++; ok = 1; }
+      }
+    } else if (c >= 0xF0 && c <= 0xF4) {
+      uint8_t c1 = NX(i);
+      if ((c == 0xF0 && c1 >= 0x90 && c1 <= 0xBF) || (c >= 0xF1 && c <= 0xF3 && CONT(c1)) ||
+          (c == 0xF4 && c1 >= 0x80 && c1 <= 0x8F)) {
+        i++;
+        if (CONT(NX(i))) { i++; if (CONT(NX(i))) { i++; ok = 1; } }
+      }
+    }
+#undef NX
+#undef CONT
+    if (ok) bput(out, (const char*)v + start, i - start);
+    else bput(out, "\xEF\xBF\xBD", 3);
+  }
+}
+
+/* str::replace: leftmost non-overlapping matches, a new String every call */
+static void str_replace(bbuf* s, const char* pat, uint64_t pn, const char* rep, uint64_t rn) {
+  bbuf o = {0};
+  uint64_t i = 0, last = 0;
+  while (i + pn <= s->n) {
+    if (memcmp(s->b + i, pat, pn) == 0) {
+      bput(&o, s->b + last, i - last); bput(&o, rep, rn);
+      i += pn; last = i;
+    } else i++;
+  }
+  bput(&o, s->b + last, s->n - last);
+  free(s->b); *s = o;
+}
+
+static int ws_len_at(const uint8_t* s, uint64_t n, uint64_t i) {  /* White_Space char at i: its length, else 0 */
+  uint8_t b = s[i];
+  if ((b >= 0x09 && b <= 0x0D) || b == 0x20) return 1;
+  if (b < 0x80) return 0;
+  uint32_t cp; int l = u8dec(s, n, i, &cp);
+  return cls_of(cp) == 0 && cp != 0xFFFD ? l : 0;
+}
+
+static void clean_up(bbuf* s) {  /* src/huggingface/mod.rs:749-767 */
+  static const char* pats[15][2] = {{" .", "."}, {" ,", ","}, {" !", "!"}, {" ?", "?"}, {" :", ":"}, {" ;", ";"},
+                                    {"\" ", "\""}, {" \"", "\""}, {"' ", "'"}, {" '", "'"}, {"( ", "("},
+                                    {" )", ")"}, {"[ ", "["}, {" ]", "]"}, {" - ", "-"}};
+  for (int k = 0; k < 15; k++) str_replace(s, pats[k][0], strlen(pats[k][0]), pats[k][1], strlen(pats[k][1]));
+  bbuf o = {0};
+  const uint8_t* t = (const uint8_t*)s->b;
+  uint64_t i = 0; int first = 1;
+  while (i < s->n) {
+    int w;
+    while (i < s->n && (w = ws_len_at(t, s->n, i)) > 0) i += (uint64_t)w;
+    if (i >= s->n) break;
+    uint64_t st = i;
+    while (i < s->n && ws_len_at(t, s->n, i) == 0) {
+      uint32_t cp; i += (uint64_t)u8dec(t, s->n, i, &cp);
+    }
+    if (!first) bput(&o, " ", 1);
+    bput(&o, s->b + st, i - st); first = 0;
+  }
+  free(s->b); *s = o;
+}
+
+static void decode_doc(const ref_dec* d, const uint32_t* ids, uint64_t n, int skip, int cleanup, bbuf* out) {
+  uint32_t* keep = (uint32_t*)malloc((n + 1) * 4); uint64_t nk = 0;
+  for (uint64_t i = 0; i < n; i++) {
+    uint32_t id = ids[i];
+    if (skip && id < d->n_ids && d->tok[id]) {
+      uint32_t v;
+      if (smap_get(&d->special, d->tok[id], d->tok_len[id], &v)) continue;
+    }
+    keep[nk++] = id;
+  }
+  char** toks = (char**)malloc((nk + 1) * sizeof(char*)); uint32_t* tl = (uint32_t*)malloc((nk + 1) * 4);
+  uint64_t nt = 0;
+  for (uint64_t i = 0; i < nk; i++) {
+    uint32_t id = keep[i];
+    if (id >= d->n_ids || !d->tok[id]) continue;
+    toks[nt] = (char*)malloc(d->tok_len[id] + 1); memcpy(toks[nt], d->tok[id], d->tok_len[id]);
+    tl[nt++] = d->tok_len[id];
+  }
+  bbuf text = {0};
+  if (d->kind == 1) {
+    cmap m; unicode_to_bytes(&m);
+    bbuf joined = {0};
+    for (uint64_t i = 0; i < nt; i++) bput(&joined, toks[i], tl[i]);
+    bbuf raw = {0};
+    for (uint64_t i = 0; i < joined.n;) {
+      uint32_t cp; i += (uint64_t)u8dec((const uint8_t*)joined.b, joined.n, i, &cp);
+      uint8_t b;
+      if (cp == 0x120) { b = 0x20; bput(&raw, (const char*)&b, 1); }
+      else if (cmap_get(&m, cp, &b)) bput(&raw, (const char*)&b, 1);
+      else if (cp < 0x80) { b = (uint8_t)cp; bput(&raw, (const char*)&b, 1); }
+    }
+    utf8_lossy((const uint8_t*)raw.b, raw.n, &text);
+    free(joined.b); free(raw.b);
+  } else {
+    for (uint64_t i = 0; i < nt; i++) bput(&text, toks[i], tl[i]);
+  }
+  for (uint64_t i = 0; i < nt; i++) free(toks[i]);
+  free(toks); free(tl); free(keep);
+  if (cleanup) clean_up(&text);
+  *out = text;
+}
+
+typedef struct {
+  const ref_dec* d; const uint32_t* ids; const uint64_t* off; int64_t nd; int skip, cleanup;
+  bbuf* per_doc; atomic_long next;
+} djob_t;
+
+static void* dworker(void* arg) {
+  djob_t* j = (djob_t*)arg;
+  for (;;) {
+    long d0 = atomic_fetch_add(&j->next, 16);
+    if (d0 >= j->nd) break;
+    long d1 = d0 + 16 < j->nd ? d0 + 16 : j->nd;
+    for (long k = d0; k < d1; k++)
+      decode_doc(j->d, j->ids + j->off[k], j->off[k + 1] - j->off[k], j->skip, j->cleanup, &j->per_doc[k]);
+  }
+  return NULL;
+}
+
+/* Decode n_docs id sequences (flat ids + n_docs+1 offsets) into UTF-8 strings packed in out
+ * (out_off[n_docs+1]).  Returns 0, or -2 when out_cap is too small (out_off[n_docs] = needed). */
+int ref_decode_batch(const ref_dec* d, const uint32_t* ids, const uint64_t* off, int64_t nd, int skip, int cleanup,
+                     uint8_t* out, uint64_t out_cap, uint64_t* out_off, int threads) {
+  djob_t j; j.d = d; j.ids = ids; j.off = off; j.nd = nd; j.skip = skip; j.cleanup = cleanup;
+  j.per_doc = (bbuf*)calloc((size_t)nd + 1, sizeof(bbuf));
+  atomic_init(&j.next, 0);
+  if (threads < 1) threads = 1;
+  pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * threads);
+  for (int i = 0; i < threads; i++) pthread_create(&th[i], NULL, dworker, &j);
+  for (int i = 0; i < threads; i++) pthread_join(th[i], NULL);
+  free(th);
+  uint64_t acc = 0;
+  for (int64_t k = 0; k < nd; k++) { out_off[k] = acc; acc += j.per_doc[k].n; }
+  out_off[nd] = acc;
+  int rc = acc > out_cap ? -2 : 0;
+  if (!rc) for (int64_t k = 0; k < nd; k++) if (j.per_doc[k].n) memcpy(out + out_off[k], j.per_doc[k].b, j.per_doc[k].n);
+  for (int64_t k = 0; k < nd; k++) free(j.per_doc[k].b);
+  free(j.per_doc);
+  return rc;
+}

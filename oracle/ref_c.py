@@ -43,6 +43,12 @@ def lib():
         L.ref_nfc.argtypes = [P, ctypes.c_uint64, P]
         L.ref_pieces.restype = ctypes.c_int64
         L.ref_pieces.argtypes = [P, ctypes.c_uint64, P]
+        L.ref_dec_create.restype = P
+        L.ref_dec_create.argtypes = [P, P, P, ctypes.c_uint64, P, P, ctypes.c_int64, ctypes.c_int]
+        L.ref_dec_destroy.argtypes = [P]
+        L.ref_decode_batch.restype = ctypes.c_int
+        L.ref_decode_batch.argtypes = [P, P, P, ctypes.c_int64, ctypes.c_int, ctypes.c_int, P, ctypes.c_uint64, P,
+                                       ctypes.c_int]
         _lib = L
     return _lib
 
@@ -93,6 +99,60 @@ class RefC:
         if getattr(self, "h", None):
             lib().ref_destroy(self.h)
             self.h = None
+        if getattr(self, "hd", None):
+            lib().ref_dec_destroy(self.hd)
+            self.hd = None
+
+    def _decoder(self):
+        """The decode-side state: Vocab::id_to_token (model.vocab only), the special added
+        tokens by content, and the decoder kind (ByteLevel or raw concatenation)."""
+        if getattr(self, "hd", None):
+            return self.hd
+        py = self.py
+        if py.decoder[0] == "unsupported":
+            raise ref_py.UnsupportedConfig("decoder " + py.decoder[1])
+        n = max(py.id_to_token_map, default=-1) + 1
+        toks = [py.id_to_token_map.get(i, "").encode("utf-8") for i in range(n)]
+        has = np.array([1 if i in py.id_to_token_map else 0 for i in range(n)] or [0], dtype=np.uint8)
+        ta, tl = _strarr(toks)
+        sp = [k.encode("utf-8") for k in py.special_tokens]
+        sa, sl = _strarr(sp)
+        self._keep += [ta, tl, has, sa, sl]
+        self.hd = lib().ref_dec_create(ctypes.cast(ta, ctypes.c_void_p), tl.ctypes.data, has.ctypes.data, n,
+                                       ctypes.cast(sa, ctypes.c_void_p), sl.ctypes.data, len(sp),
+                                       1 if py.decoder[0] == "ByteLevel" else 0)
+        return self.hd
+
+    def decode_packed(self, ids: np.ndarray, tok_off: np.ndarray, skip_special_tokens=False,
+                      clean_up_tokenization_spaces=True, threads: int = 0):
+        """decode_batch_with_options on packed ids -> (utf-8 bytes uint8[N], out_off uint64[D+1])."""
+        hd = self._decoder()
+        ids = np.ascontiguousarray(ids, dtype=np.uint32)
+        tok_off = np.ascontiguousarray(tok_off, dtype=np.uint64)
+        nd = len(tok_off) - 1
+        threads = threads or os.cpu_count() or 1
+        cap = 64
+        while True:
+            out = np.empty(cap, dtype=np.uint8)
+            out_off = np.empty(nd + 1, dtype=np.uint64)
+            rc = lib().ref_decode_batch(hd, ids.ctypes.data if len(ids) else None, tok_off.ctypes.data, nd,
+                                        int(bool(skip_special_tokens)), int(bool(clean_up_tokenization_spaces)),
+                                        out.ctypes.data, cap, out_off.ctypes.data, threads)
+            if rc == -2:
+                cap = int(out_off[-1]) + 64
+                continue
+            if rc != 0:
+                raise RuntimeError("ref_decode_batch rc=%d" % rc)
+            return out[: int(out_off[-1])].copy(), out_off
+
+    def decode_batch(self, batch, skip_special_tokens=False, clean_up_tokenization_spaces=True, threads: int = 0):
+        off = np.zeros(len(batch) + 1, dtype=np.uint64)
+        np.cumsum([len(b) for b in batch], out=off[1:])
+        ids = np.array([i for b in batch for i in b] or [0], dtype=np.uint32)
+        out, out_off = self.decode_packed(ids, off, skip_special_tokens, clean_up_tokenization_spaces, threads)
+        o = out_off.tolist()
+        raw = out.tobytes()
+        return [raw[o[k]:o[k + 1]].decode("utf-8") for k in range(len(batch))]
 
     def encode_packed(self, text: np.ndarray, off: np.ndarray, threads: int = 0):
         text = np.ascontiguousarray(text, dtype=np.uint8)

@@ -162,6 +162,7 @@ class RefTokenizer:
             raise UnsupportedConfig("pre_tokenizer chain must be no-op Splits around exactly one ByteLevel")
         self.byte_encoder = bytes_to_unicode()
         self.id_to_token_map = {v: k for k, v in vocab.items()}
+        self.decoder = parse_decoder(obj.get("decoder"))
 
     @classmethod
     def from_file(cls, path):
@@ -312,6 +313,31 @@ class RefTokenizer:
         """src/huggingface/mod.rs:694-696 (rayon par_iter, order-preserving)."""
         return [self.encode(t) for t in texts]
 
+    # --------------------------------------------------------------------- decode (SURVEY 8f row 1)
+    def decode_with_options(self, ids, skip_special_tokens=False, clean_up_tokenization_spaces=True):
+        """decode_impl, src/huggingface/mod.rs:710-747.  Ids are looked up in model.vocab only
+        (Vocab::get_token, src/vocab.rs:91-93): an added token that is not in model.vocab is
+        dropped.  skip_special_tokens drops ids whose model.vocab string is a special added
+        token's content (:716-726)."""
+        if self.decoder[0] == "unsupported":
+            raise UnsupportedConfig("decoder " + self.decoder[1])
+        if skip_special_tokens:
+            ids = [i for i in ids if not (i in self.id_to_token_map and self.id_to_token_map[i] in self.special_tokens)]
+        toks = [self.id_to_token_map[i] for i in ids if i in self.id_to_token_map]
+        if self.decoder[0] == "ByteLevel":
+            text = byte_level_decode(toks)          # src/decoders.rs:94-119
+        else:
+            text = "".join(toks)                    # BpeTokenizer::decode, src/bpe.rs:170-176
+        return clean_up_tokenization_spaces_(text) if clean_up_tokenization_spaces else text
+
+    def decode(self, ids):
+        """src/huggingface/mod.rs:698-700 (skip_special_tokens=false, clean-up on)."""
+        return self.decode_with_options(ids, False, True)
+
+    def decode_batch(self, batch, skip_special_tokens=False, clean_up_tokenization_spaces=True):
+        """src/huggingface/mod.rs:771-785 (rayon par_iter, order-preserving)."""
+        return [self.decode_with_options(ids, skip_special_tokens, clean_up_tokenization_spaces) for ids in batch]
+
     # convenience for tests: regex pieces as raw byte strings
     def pieces(self, text):
         if self.pre_tokenizer[0] == "ByteLevel" and self.pre_tokenizer[1] and text and not text.startswith(" "):
@@ -332,3 +358,129 @@ _WS = frozenset(map(chr, [0x9, 0xA, 0xB, 0xC, 0xD, 0x20, 0x85, 0xA0, 0x1680, 0x2
 def _rust_ws(ch):
     """Rust char::is_whitespace = Unicode White_Space (25 code points)."""
     return ch in _WS
+
+
+# ----------------------------------------------------------------------------- decode pieces
+
+def parse_decoder(value):
+    """src/huggingface/parsing.rs:272-364, reduced to what decode needs.  Returns
+    ("ByteLevel",), ("Raw",) for `None` (an unknown type string: BpeTokenizer::decode joins the
+    raw vocab strings, mod.rs:737-740), or ("unsupported", name) for a decoder outside the
+    ByteLevel-BPE path (Metaspace, WordPiece, BPE, CTC, Strip, or a Sequence holding one of them
+    or more than one ByteLevel).  Fuse inside a Sequence is the identity on a one-string list."""
+    if isinstance(value, dict) and "type" in value:
+        t = value["type"] if isinstance(value["type"], str) else ""
+        if t == "ByteLevel":
+            return ("ByteLevel",)
+        if t in ("Metaspace", "WordPiece", "BPE", "CTC", "Strip"):
+            return ("unsupported", t)
+        if t == "Fuse":
+            return ("Raw",)  # Fuse: tokens.join("") (src/decoders.rs), the raw concatenation
+        if t == "Sequence":
+            decs = value.get("decoders")
+            if not isinstance(decs, list):
+                return ("Raw",)
+            parsed = [parse_decoder(d) for d in decs]  # non-object entries parse as ByteLevel
+            if not parsed:
+                return ("Raw",)
+            names = []
+            for d, raw in zip(parsed, decs):
+                if d[0] == "unsupported":
+                    return d
+                is_fuse = isinstance(raw, dict) and raw.get("type") == "Fuse"
+                if d[0] == "Raw" and not is_fuse:
+                    continue  # filter_map drops entries that parse to None
+                names.append("Fuse" if is_fuse else d[0])
+            if not names:
+                return ("Raw",)
+            nbl = names.count("ByteLevel")
+            if nbl > 1:
+                return ("unsupported", "Sequence with more than one ByteLevel")
+            return ("ByteLevel",) if nbl == 1 else ("Raw",)
+        return ("Raw",)
+    return ("ByteLevel",)
+
+
+_BYTE_DECODER = {c: b for b, c in bytes_to_unicode().items()}  # unicode_to_bytes, src/decoders.rs:74-92
+
+
+def byte_level_decode(tokens):
+    """src/decoders.rs:94-119: join, map each char back to its byte ('Ġ' -> ' ', the 256 GPT-2
+    chars, other ASCII chars as themselves, everything else dropped), then from_utf8_lossy."""
+    out = bytearray()
+    for c in "".join(tokens):
+        if c == "\u0120":
+            out.append(0x20)
+        elif c in _BYTE_DECODER:
+            out.append(_BYTE_DECODER[c])
+        elif ord(c) < 0x80:
+            out.append(ord(c))
+    return from_utf8_lossy(bytes(out))
+
+
+def from_utf8_lossy(b: bytes) -> str:
+    """Rust String::from_utf8_lossy (core::str::lossy::Utf8Chunks): each maximal prefix of a
+    valid sequence that cannot be completed (or a lone invalid byte) becomes one U+FFFD."""
+    out = []
+    i, n = 0, len(b)
+    while i < n:
+        start = i
+        c = b[i]
+        i += 1
+        if c < 0x80:
+            out.append(chr(c))
+            continue
+        nxt = lambda k: b[k] if k < n else 0  # noqa: E731  (safe_get: 0 past the end)
+        ok = False
+        if 0xC2 <= c <= 0xDF:
+            if 0x80 <= nxt(i) <= 0xBF:
+                i += 1
+                ok = True
+        elif 0xE0 <= c <= 0xEF:
+            c1 = nxt(i)
+            if (c == 0xE0 and 0xA0 <= c1 <= 0xBF) or (0xE1 <= c <= 0xEC and 0x80 <= c1 <= 0xBF) or \
+                    (c == 0xED and 0x80 <= c1 <= 0x9F) or (0xEE <= c <= 0xEF and 0x80 <= c1 <= 0xBF):
+                i += 1
+                if 0x80 <= nxt(i) <= 0xBF:
+                    i += 1
+                    ok = True
+        elif 0xF0 <= c <= 0xF4:
+            c1 = nxt(i)
+            if (c == 0xF0 and 0x90 <= c1 <= 0xBF) or (0xF1 <= c <= 0xF3 and 0x80 <= c1 <= 0xBF) or \
+                    (c == 0xF4 and 0x80 <= c1 <= 0x8F):
+                i += 1
+                if 0x80 <= nxt(i) <= 0xBF:
+                    i += 1
+                    if 0x80 <= nxt(i) <= 0xBF:
+                        i += 1
+                        ok = True
+        if ok:
+            out.append(b[start:i].decode("utf-8"))
+        else:
+            out.append("\ufffd")
+    return "".join(out)
+
+
+# src/huggingface/mod.rs:749-767, applied in this order, each a leftmost non-overlapping replace
+CLEANUP_REPLACEMENTS = [(" .", "."), (" ,", ","), (" !", "!"), (" ?", "?"), (" :", ":"), (" ;", ";"),
+                        ('" ', '"'), (' "', '"'), ("' ", "'"), (" '", "'"), ("( ", "("), (" )", ")"),
+                        ("[ ", "["), (" ]", "]"), (" - ", "-")]
+
+
+def clean_up_tokenization_spaces_(text: str) -> str:
+    """HuggingFaceTokenizer::clean_up_tokenization_spaces (src/huggingface/mod.rs:749-767): the
+    replaces, then split_whitespace (Rust char::is_whitespace, the 25 White_Space code points --
+    not Python's str.split, which also splits on U+001C..U+001F) joined by single spaces."""
+    for a, b in CLEANUP_REPLACEMENTS:
+        text = text.replace(a, b)
+    words, cur = [], []
+    for ch in text:
+        if ch in _WS:
+            if cur:
+                words.append("".join(cur))
+                cur = []
+        else:
+            cur.append(ch)
+    if cur:
+        words.append("".join(cur))
+    return " ".join(words)
