@@ -1,8 +1,9 @@
 """complexity_tokenizer -- MI355X-native batch ByteLevel-BPE encode path.
 
-Drop-in for the encode surface of Complexity-ML/complexity-tokenizer's `Tokenizer`
+Drop-in for the encode / decode surface of Complexity-ML/complexity-tokenizer's `Tokenizer`
 (python/complexity_tokenizer/__init__.py:16-18 re-exporting the PyO3 class of
 src/bindings/tokenizer.rs:11-14): `from_file`, `from_pretrained`, `encode`, `encode_batch`,
+`decode`, `decode_with_options`, `decode_batch`, `decode_batch_with_options`, `batch_decode`,
 `vocab_size`, `token_to_id`, `id_to_token`, `special_tokens`.  The work runs in hand-written
 HIP kernels on an MI355X (gfx950) behind the C ABI of include/ctok.h; there is no CPU path.
 
@@ -76,6 +77,29 @@ def pack_texts(texts) -> tuple[np.ndarray, np.ndarray]:
     return buf, off
 
 
+def pack_ids(batch) -> tuple[np.ndarray, np.ndarray]:
+    """list[list[int]] -> (uint32 ids, uint64 offsets[D+1]).  Mirrors the PyO3 `Vec<Vec<u32>>`
+    extraction: a bare str is refused, elements must be ints in [0, 2**32)."""
+    if isinstance(batch, (str, bytes)):
+        raise TypeError("Can't extract `str` to `Vec`")
+    lens = []
+    flat = []
+    for seq in batch:
+        if isinstance(seq, (str, bytes)):
+            raise TypeError("Can't extract `str` to `Vec`")
+        seq = list(seq)
+        for x in seq:
+            if not isinstance(x, (int, np.integer)):
+                raise TypeError("'%s' object cannot be interpreted as an integer" % type(x).__name__)
+            if x < 0 or x > 0xFFFFFFFF:
+                raise OverflowError("can't convert %d to u32" % x)
+        lens.append(len(seq))
+        flat.extend(seq)
+    off = np.zeros(len(lens) + 1, dtype=np.uint64)
+    np.cumsum(np.asarray(lens, dtype=np.uint64), out=off[1:])
+    return np.asarray(flat, dtype=np.uint64).astype(np.uint32), off
+
+
 class Tokenizer:
     """HuggingFace-format ByteLevel-BPE tokenizer whose encode path runs on an MI355X."""
 
@@ -83,6 +107,7 @@ class Tokenizer:
         self._h = ctypes.c_void_p(handle)
         self.device = int(os.environ.get("CTOK_DEVICE", "0"))
         self.last_stats = None
+        self.last_decode_stats = None
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -227,6 +252,88 @@ class Tokenizer:
         if not isinstance(text, str):
             raise TypeError("'%s' object cannot be converted to 'PyString'" % type(text).__name__)
         return self.encode_batch([text])[0]
+
+    # ------------------------------------------------------------------ decode
+    def decode_packed(self, ids: np.ndarray, tok_off: np.ndarray, skip_special_tokens: bool = False,
+                      clean_up_tokenization_spaces: bool = True, timing: bool = False):
+        """Extension: decode packed ids (uint32[T], uint64 offsets[D+1]) and return
+        (utf-8 bytes uint8[N], out_off uint64[D+1]) without building Python strings."""
+        ids = np.ascontiguousarray(ids, dtype=np.uint32)
+        tok_off = np.ascontiguousarray(tok_off, dtype=np.uint64)
+        n_docs = len(tok_off) - 1
+        if n_docs < 0:
+            raise ValueError("offsets must hold n_docs + 1 entries")
+        if len(ids) < int(tok_off[-1]):
+            raise ValueError("ids shorter than tok_off[-1]")
+        opts = (_n.CTOK_D_SKIP_SPECIAL if skip_special_tokens else 0) | (
+            _n.CTOK_D_CLEANUP if clean_up_tokenization_spaces else 0)
+        cap = 4 * len(ids) + 64
+        while True:
+            out = np.empty(cap, dtype=np.uint8)
+            out_off = np.empty(n_docs + 1, dtype=np.uint64)
+            ex = _n.Exec(self.device, None, _n.CTOK_F_TIMING if timing else 0)
+            st = _n.DecodeStats()
+            rc = _n.lib.ctok_decode_batch(self._h, ids.ctypes.data if len(ids) else None, tok_off.ctypes.data, n_docs,
+                                          opts, out.ctypes.data, cap, out_off.ctypes.data, ctypes.byref(ex),
+                                          ctypes.byref(st))
+            if rc == _n.CTOK_E_CAPACITY:
+                cap = int(out_off[-1]) + 64
+                continue
+            if rc != _n.CTOK_OK:
+                _raise(rc)
+            self.last_decode_stats = st.as_dict()
+            return out[: int(out_off[-1])], out_off
+
+    def decode_packed_device(self, d_ids: int, d_tok_off: int, n_docs: int, n_ids: int, d_out: int, out_cap: int,
+                             d_out_off: int, skip_special_tokens: bool = False,
+                             clean_up_tokenization_spaces: bool = True, stream: int = 0, timing: bool = False,
+                             device: int | None = None):
+        """Extension: decode ids already resident in HBM (raw device pointers).  Returns the
+        number of output bytes; raises ValueError when out_cap is smaller (the size is in the
+        message and in last_decode_needed)."""
+        opts = (_n.CTOK_D_SKIP_SPECIAL if skip_special_tokens else 0) | (
+            _n.CTOK_D_CLEANUP if clean_up_tokenization_spaces else 0)
+        ex = _n.Exec(self.device if device is None else device, stream or None, _n.CTOK_F_TIMING if timing else 0)
+        st = _n.DecodeStats()
+        nb = ctypes.c_uint64()
+        rc = _n.lib.ctok_decode_batch_device(self._h, d_ids, d_tok_off, n_docs, n_ids, opts, d_out, out_cap, d_out_off,
+                                             ctypes.byref(nb), ctypes.byref(ex), ctypes.byref(st))
+        self.last_decode_needed = int(nb.value)
+        if rc == _n.CTOK_E_CAPACITY:
+            raise ValueError("out_cap too small: %d bytes needed" % nb.value)
+        if rc != _n.CTOK_OK:
+            _raise(rc)
+        self.last_decode_stats = st.as_dict()
+        return int(nb.value)
+
+    def decode_batch_with_options(self, batch, skip_special_tokens: bool = False,
+                                  clean_up_tokenization_spaces: bool = True) -> list:
+        """src/bindings/tokenizer.rs:231-238 -> src/huggingface/mod.rs:777-785."""
+        ids, off = pack_ids(batch)
+        out, out_off = self.decode_packed(ids, off, skip_special_tokens, clean_up_tokenization_spaces)
+        raw = out.tobytes()
+        o = out_off.tolist()
+        return [raw[o[i]:o[i + 1]].decode("utf-8") for i in range(len(o) - 1)]
+
+    def decode_batch(self, batch) -> list:
+        """src/bindings/tokenizer.rs:226-228 -> src/huggingface/mod.rs:771-773."""
+        return self.decode_batch_with_options(batch, False, True)
+
+    def batch_decode(self, sequences, skip_special_tokens: bool = False,
+                     clean_up_tokenization_spaces: bool = True) -> list:
+        """HF-compatible alias, src/bindings/tokenizer.rs:655-663."""
+        return self.decode_batch_with_options(sequences, skip_special_tokens, clean_up_tokenization_spaces)
+
+    def decode_with_options(self, ids, skip_special_tokens: bool = False,
+                            clean_up_tokenization_spaces: bool = True) -> str:
+        """src/bindings/tokenizer.rs:216-224 -> src/huggingface/mod.rs:702-709."""
+        if isinstance(ids, (str, bytes)):
+            raise TypeError("Can't extract `str` to `Vec`")
+        return self.decode_batch_with_options([ids], skip_special_tokens, clean_up_tokenization_spaces)[0]
+
+    def decode(self, ids) -> str:
+        """src/bindings/tokenizer.rs:212-214 -> src/huggingface/mod.rs:698-700."""
+        return self.decode_with_options(ids, False, True)
 
     def __repr__(self):
         return "Tokenizer(vocab_size=%d, device=%d)" % (self.vocab_size, self.device)

@@ -16,6 +16,28 @@ if not os.path.exists(LIB_PATH):
         "complexity_tokenizer: native library not found at %s -- build it with "
         "`make -C complexity-tokenizer_amd/csrc` (or `python -c 'import __graft_entry__ as g; g.build()'`)" % LIB_PATH)
 
+
+def _share_torch_hip_runtime():
+    """torch wheels bundle their own HIP runtime with the same SONAME (libamdhip64.so.7) as
+    /opt/rocm's.  Whichever copy loads first serves libctok.so; if /opt/rocm's came first and torch
+    were imported later, torch would load its copy next to it and two HIP runtimes in one process
+    fail to share the device.  Preloading torch's copy (without importing torch) makes every HIP
+    user in the process resolve to one runtime.  CTOK_NO_TORCH_HIP=1 disables this."""
+    if os.environ.get("CTOK_NO_TORCH_HIP"):
+        return
+    try:
+        import importlib.util
+        spec = importlib.util.find_spec("torch")
+    except (ImportError, ValueError):
+        return
+    if spec is None or not spec.origin:
+        return
+    path = os.path.join(os.path.dirname(spec.origin), "lib", "libamdhip64.so")
+    if os.path.exists(path):
+        ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+
+
+_share_torch_hip_runtime()
 lib = ctypes.CDLL(LIB_PATH)
 
 CTOK_OK = 0
@@ -52,6 +74,19 @@ class Stats(ctypes.Structure):
         return d
 
 
+class DecodeStats(ctypes.Structure):
+    _fields_ = [("ms_total", ctypes.c_double), ("ms_device", ctypes.c_double), ("ms_len", ctypes.c_double),
+                ("ms_gather", ctypes.c_double), ("ms_clean", ctypes.c_double), ("ms_h2d", ctypes.c_double),
+                ("ms_d2h", ctypes.c_double), ("ids", ctypes.c_uint64), ("docs", ctypes.c_uint64),
+                ("bytes_raw", ctypes.c_uint64), ("bytes_out", ctypes.c_uint64), ("direct", ctypes.c_uint32)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+CTOK_D_SKIP_SPECIAL = 1
+CTOK_D_CLEANUP = 2
+
 _p = ctypes.c_void_p
 _u64 = ctypes.c_uint64
 _u64p = ctypes.POINTER(ctypes.c_uint64)
@@ -74,6 +109,10 @@ SIGS = {
     "ctok_encode_batch_device": (ctypes.c_int, [_p, _p, _p, _u64, _u64, _p, _u64, _p, _u64p, ctypes.POINTER(Exec),
                                                 ctypes.POINTER(Stats)]),
     "ctok_device_count": (ctypes.c_int, []),
+    "ctok_decode_batch": (ctypes.c_int, [_p, _p, _p, _u64, ctypes.c_uint32, _p, _u64, _p, ctypes.POINTER(Exec),
+                                         ctypes.POINTER(DecodeStats)]),
+    "ctok_decode_batch_device": (ctypes.c_int, [_p, _p, _p, _u64, _u64, ctypes.c_uint32, _p, _u64, _p, _u64p,
+                                                ctypes.POINTER(Exec), ctypes.POINTER(DecodeStats)]),
 }
 
 for _name, (_res, _args) in SIGS.items():

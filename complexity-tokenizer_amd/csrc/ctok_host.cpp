@@ -7,6 +7,7 @@
 //   normaliser choice src/huggingface/parsing.rs:10-90 (NFC default at :89)
 //   pre-tokenizer     src/huggingface/parsing.rs:92-190; src/pretokenizers.rs:71-126, :298-302
 //   vocab getters     src/vocab.rs:34-100, src/huggingface/mod.rs:856-866
+//   decode            src/huggingface/mod.rs:698-785, src/decoders.rs:74-119, parsing.rs:272-364
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -22,6 +23,7 @@
 #include <sstream>
 #include <string>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "../../include/ctok.h"
@@ -183,6 +185,15 @@ struct DeviceState {
   DevBuf<uint32_t> doc_flag, ncp;
   DevBuf<uint64_t> norm_off;
   DevBuf<uint8_t> norm_text;
+  // decode: tables (uploaded on first use), workspace, events
+  bool dec_ready = false;
+  DevBuf<uint32_t> dec_ent;
+  DevBuf<uint8_t> dec_bytes;
+  DevBuf<uint32_t> dec_chunk, dec_del, dec_tile, dec_cnt;
+  DevBuf<uint8_t> dec_raw, dec_out;
+  DevBuf<uint64_t> dec_rawoff, dec_outoff, dec_tokoff;
+  DevBuf<uint32_t> dec_ids;
+  hipEvent_t dev_ev[8] = {};
   // host-API staging
   DevBuf<uint8_t> in_text;
   DevBuf<uint64_t> in_off, out_off;
@@ -191,6 +202,7 @@ struct DeviceState {
     if (device >= 0) {
       (void)hipSetDevice(device);
       for (auto& e : ev) if (e) (void)hipEventDestroy(e);
+      for (auto& e : dev_ev) if (e) (void)hipEventDestroy(e);
       if (ev_sync) (void)hipEventDestroy(ev_sync);
       if (ev_fork) (void)hipEventDestroy(ev_fork);
       if (ev_join) (void)hipEventDestroy(ev_join);
@@ -227,6 +239,11 @@ struct ctok {
   std::vector<uint8_t> at_flags;
   bool proper = true;
   bool compact = false;
+  // decode (src/huggingface/mod.rs:710-747): decoder kind, per-id decoded bytes
+  int decoder = 1;                  // 1 ByteLevel, 0 raw concatenation (unknown decoder type), -1 unsupported
+  std::string decoder_name;         // for the unsupported message
+  std::vector<uint32_t> dec_ent;    // 2 u32 per id: byte offset, length | kDecNonAscii | kDecSpecial
+  std::vector<uint8_t> dec_bytes;   // each id's bytes, 4-byte aligned, + 8 bytes of padding
   // per device
   std::mutex dev_mu;
   std::map<int, std::unique_ptr<DeviceState>> devs;
@@ -307,6 +324,84 @@ void parse_pre_tokenizer(const ctj::Value* v, std::vector<std::pair<char, bool>>
 }
 
 
+// parse_decoder (src/huggingface/parsing.rs:272-364) reduced to what decode needs: 1 = ByteLevel
+// (also the default for a null / absent / non-object value or an object without "type"),
+// 0 = None (an unknown type string: BpeTokenizer::decode joins the raw vocab strings,
+// src/huggingface/mod.rs:737-740), -1 = a decoder outside the ByteLevel-BPE path.  In a
+// Sequence, entries that parse to None are dropped (filter_map), Fuse is the identity on the
+// one-string list the previous decoder leaves, and one ByteLevel is the whole effect.
+int parse_decoder(const ctj::Value* v, std::string& name) {
+  if (!v || v->kind != ctj::Value::Object) return 1;
+  const ctj::Value* ty = v->get("type");
+  if (!ty) return 1;
+  const std::string t = ty->kind == ctj::Value::String ? ty->s : "";
+  if (t == "ByteLevel") return 1;
+  if (t == "Fuse") return 0;
+  if (t == "Metaspace" || t == "WordPiece" || t == "BPE" || t == "CTC" || t == "Strip") { name = t; return -1; }
+  if (t != "Sequence") return 0;
+  const ctj::Value* decs = v->get("decoders");
+  if (!decs || decs->kind != ctj::Value::Array || decs->arr.empty()) return 0;
+  int nbl = 0, kept = 0;
+  for (const auto& d : decs->arr) {
+    std::string sub;
+    const int k = parse_decoder(&d, sub);
+    if (k < 0) { name = sub; return -1; }
+    const ctj::Value* dt = d.kind == ctj::Value::Object ? d.get("type") : nullptr;
+    const bool fuse = dt && dt->kind == ctj::Value::String && dt->s == "Fuse";
+    if (k == 0 && !fuse) continue;  // None: dropped by filter_map
+    kept++;
+    if (k == 1) nbl++;
+  }
+  if (!kept) return 0;
+  if (nbl > 1) { name = "Sequence with more than one ByteLevel"; return -1; }
+  return nbl;
+}
+
+// Per-id decoded bytes: the ByteLevel decoder maps every char of the token back to a byte ('Ġ'
+// and the 255 other GPT-2 chars, src/decoders.rs:74-92,101-107), keeps other ASCII chars
+// (:108-110) and drops the rest; the raw decoder keeps the token's UTF-8 bytes.
+void build_decode_table(ctok* t) {
+  uint32_t n_ent = 0;
+  for (const auto& kv : t->id_to_token) n_ent = std::max(n_ent, kv.first + 1);
+  if (n_ent > (1u << 26)) throw_err(CTOK_E_UNSUPPORTED, "token ids above 2^26 are not supported by the decode table");
+  std::vector<int> inv(0x144, -1);  // GPT-2 char -> byte
+  {
+    std::vector<uint32_t> bm = byte_map();
+    for (int b = 0; b < 256; b++) inv[bm[b]] = b;
+  }
+  std::unordered_set<std::string> special;
+  for (const auto& sp : t->special) special.insert(sp.first);
+  t->dec_ent.assign(2 * (size_t)n_ent, 0);
+  t->dec_bytes.clear();
+  std::vector<uint32_t> cps;
+  std::string out;
+  for (uint32_t id = 0; id < n_ent; id++) {
+    auto it = t->id_to_token.find(id);
+    if (it == t->id_to_token.end()) continue;
+    const std::string& tok = it->second;
+    out.clear();
+    if (t->decoder == 1) {
+      if (!decode_utf8(tok, cps)) throw_err(CTOK_E_PARSE, "vocab entry is not valid UTF-8");
+      for (uint32_t c : cps) {
+        if (c < inv.size() && inv[c] >= 0) out += (char)inv[c];
+        else if (c < 0x80) out += (char)c;
+      }
+    } else {
+      out = tok;
+    }
+    if (out.size() > kDecLenMask) throw_err(CTOK_E_UNSUPPORTED, "vocab entry longer than 16 MiB");
+    uint32_t y = (uint32_t)out.size();
+    for (unsigned char c : out)
+      if (c >= 0x80) { y |= kDecNonAscii; break; }
+    if (special.count(tok)) y |= kDecSpecial;
+    while (t->dec_bytes.size() & 3) t->dec_bytes.push_back(0);
+    t->dec_ent[2 * id] = (uint32_t)t->dec_bytes.size();
+    t->dec_ent[2 * id + 1] = y;
+    t->dec_bytes.insert(t->dec_bytes.end(), out.begin(), out.end());
+  }
+  for (int k = 0; k < 8; k++) t->dec_bytes.push_back(0);
+}
+
 void load(ctok* t, const char* buf, size_t len) {
   ctj::Value root;
   try {
@@ -326,7 +421,15 @@ void load(ctok* t, const char* buf, size_t len) {
     if (!m.second.is_u32()) throw_err(CTOK_E_PARSE, "invalid value for vocab entry `" + m.first + "`, expected u32");
     t->vocab[m.first] = (uint32_t)m.second.u;  // HashMap insert: a later duplicate key wins
   }
-  for (const auto& kv : t->vocab) t->id_to_token[kv.second] = kv.first;
+  // Vocab::id_to_token (src/vocab.rs:47-52).  Several tokens sharing one id make the reference's
+  // choice depend on HashMap order; here the later entry of the file wins (first occurrence of a
+  // key, final value) -- parity for such files is unpinned.
+  {
+    std::unordered_set<std::string> seen;
+    seen.reserve(vocab->obj.size() * 2);
+    for (const auto& m : vocab->obj)
+      if (seen.insert(m.first).second) t->id_to_token[t->vocab[m.first]] = m.first;
+  }
 
   // merges: deserialize_merges (mod.rs:56-101) then split(' ') == 2 parts (mod.rs:252-264)
   std::vector<std::pair<std::string, std::string>> merges;
@@ -584,6 +687,10 @@ void load(ctok* t, const char* buf, size_t len) {
   for (auto& c : chain)
     if (c.first == 'B') { nbl++; t->add_prefix_space = c.second; }
   if (nbl != 1) throw_err(CTOK_E_UNSUPPORTED, "pre_tokenizer must contain exactly one ByteLevel");
+
+  // decoder (parsing.rs:272-364) and the per-id decode table
+  t->decoder = parse_decoder(root.get("decoder"), t->decoder_name);
+  build_decode_table(t);
 }
 
 template <typename T>
@@ -609,6 +716,7 @@ DeviceState* device_state(ctok* t, int device) {
     ds->n_cus = cus > 0 ? (uint32_t)cus : 1u;
   }
   for (auto& e : ds->ev) HIPTRY(hipEventCreate(&e));
+  for (auto& e : ds->dev_ev) HIPTRY(hipEventCreate(&e));
   HIPTRY(hipEventCreateWithFlags(&ds->ev_sync, hipEventDisableTiming));
   HIPTRY(hipEventCreateWithFlags(&ds->ev_fork, hipEventDisableTiming));
   HIPTRY(hipEventCreateWithFlags(&ds->ev_join, hipEventDisableTiming));
@@ -874,6 +982,110 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   }
 }
 
+// ----------------------------------------------------------------------------- decode
+
+void ensure_decode_tables(ctok* t, DeviceState* ds, hipStream_t s) {
+  if (ds->dec_ready) return;
+  upload(ds->dec_ent, t->dec_ent.data(), t->dec_ent.size(), s);
+  upload(ds->dec_bytes, t->dec_bytes.data(), t->dec_bytes.size(), s);
+  HIPTRY(hipStreamSynchronize(s));
+  ds->dec_ready = true;
+}
+
+// decode_batch_with_options on device-resident ids (src/huggingface/mod.rs:771-785).  Returns
+// the output byte count; get_out(n) supplies an output buffer of >= n bytes (or throws).
+uint64_t decode_device(ctok* t, DeviceState* ds, const uint32_t* d_ids, const uint64_t* d_tok_off, uint64_t n_docs,
+                       uint64_t n_ids, uint32_t opts, const std::function<uint8_t*(uint64_t)>& get_out,
+                       uint64_t* d_out_off, hipStream_t s, bool timing, ctok_decode_stats* st) {
+  if (t->decoder < 0)
+    throw_err(CTOK_E_UNSUPPORTED, "decoder " + t->decoder_name + " is outside the ByteLevel-BPE decode path");
+  if (n_ids >= 0xF0000000ull || n_docs >= 0xF0000000ull)
+    throw_err(CTOK_E_ARG, "a single decode call is limited to < 3.75 G ids and docs; split the batch");
+  if (n_ids && ((uintptr_t)d_ids & 3)) throw_err(CTOK_E_ARG, "device ids buffer must be 4-byte aligned");
+  ensure_decode_tables(t, ds, s);
+  DecTables tb{(const uint2*)ds->dec_ent.p, (uint32_t)(t->dec_ent.size() / 2), ds->dec_bytes.p};
+  DecWork w{};
+  w.ids = d_ids;
+  w.n_ids = (uint32_t)n_ids;
+  w.tok_off = d_tok_off;
+  w.n_docs = (uint32_t)n_docs;
+  w.opts = opts & (kDecOptSkipSpecial | kDecOptCleanup);
+  w.n_chunks = (uint32_t)((n_ids + kDecChunk - 1) / kDecChunk);
+  ds->dec_chunk.ensure(w.n_chunks + 8);
+  ds->dec_cnt.ensure(8);
+  ds->scan_tmp.ensure(scan_tmp_elems(w.n_chunks + 1) + 64);
+  w.chunk_off = ds->dec_chunk.p;
+  w.counters = ds->dec_cnt.p;
+  if (timing) HIPTRY(hipEventRecord(ds->dev_ev[0], s));
+  HIPTRY(hipMemsetAsync(ds->dec_cnt.p, 0, 32, s));
+  HIPTRY(launch_dec_len(w, tb, (uint32_t*)ds->scan_tmp.p, ds->scan_tmp.cap * 2, s));
+  if (timing) HIPTRY(hipEventRecord(ds->dev_ev[1], s));
+  HIPTRY(hipMemcpyAsync(ds->host, ds->dec_cnt.p, 16, hipMemcpyDeviceToHost, s));
+  spin_sync(ds, s);
+  const uint32_t err = ((volatile uint32_t*)ds->host)[0], nonascii = ((volatile uint32_t*)ds->host)[1];
+  const uint64_t R = ((volatile uint64_t*)ds->host)[1];
+  if (err) throw_err(CTOK_E_ARG, "tok_off must start at 0, be non-decreasing and end at the number of ids");
+  if (R >= 0xF0000000ull) throw_err(CTOK_E_ARG, "decoded batch exceeds 3.75 GiB; split the batch");
+  const bool direct = !(w.opts & kDecOptCleanup) && !nonascii;
+  uint64_t n_out = R;
+  if (direct) {  // every unit is a valid ASCII byte and nothing is cleaned: the gather is the output
+    uint8_t* d_out = get_out(R);
+    if (timing) HIPTRY(hipEventRecord(ds->dev_ev[2], s));
+    HIPTRY(launch_dec_gather(w, tb, d_out, d_out_off, s));
+    if (!n_ids) HIPTRY(hipMemsetAsync(d_out_off, 0, (n_docs + 1) * 8, s));
+    if (timing) HIPTRY(hipEventRecord(ds->dev_ev[3], s));
+  } else {
+    ds->dec_raw.ensure(R + 64);
+    ds->dec_rawoff.ensure(n_docs + 1);
+    w.raw = ds->dec_raw.p;
+    w.n_raw = (uint32_t)R;
+    w.raw_off = ds->dec_rawoff.p;
+    if (timing) HIPTRY(hipEventRecord(ds->dev_ev[2], s));
+    HIPTRY(launch_dec_gather(w, tb, w.raw, w.raw_off, s));
+    if (!n_ids) HIPTRY(hipMemsetAsync(w.raw_off, 0, (n_docs + 1) * 8, s));
+    if (timing) HIPTRY(hipEventRecord(ds->dev_ev[3], s));
+    w.n_tiles = (uint32_t)((R + kDecTile - 1) / kDecTile);
+    ds->dec_tile.ensure(w.n_tiles + 8);
+    ds->dec_del.ensure(R / 32 + 8);
+    ds->scan_tmp.ensure(scan_tmp_elems(w.n_tiles + 1) + 64);
+    w.tile_cnt = ds->dec_tile.p;
+    w.delbits = ds->dec_del.p;
+    if (timing) HIPTRY(hipEventRecord(ds->dev_ev[4], s));
+    if (w.opts & kDecOptCleanup) HIPTRY(hipMemsetAsync(w.delbits, 0, (R / 32 + 8) * 4, s));
+    HIPTRY(launch_dec_prepare(w, s));
+    HIPTRY(launch_dec_count(w, (uint32_t*)ds->scan_tmp.p, ds->scan_tmp.cap * 2, s));
+    if (timing) HIPTRY(hipEventRecord(ds->dev_ev[5], s));
+    HIPTRY(hipMemcpyAsync(ds->host, w.tile_cnt + w.n_tiles, 4, hipMemcpyDeviceToHost, s));
+    spin_sync(ds, s);
+    n_out = ((volatile uint32_t*)ds->host)[0];
+    uint8_t* d_out = get_out(n_out);
+    if (timing) HIPTRY(hipEventRecord(ds->dev_ev[6], s));
+    HIPTRY(launch_dec_write(w, d_out, d_out_off, s));
+    if (!R) HIPTRY(hipMemsetAsync(d_out_off, 0, (n_docs + 1) * 8, s));
+    if (timing) HIPTRY(hipEventRecord(ds->dev_ev[7], s));
+  }
+  if (st) {
+    st->ids = n_ids;
+    st->docs = n_docs;
+    st->bytes_raw = R;
+    st->bytes_out = n_out;
+    st->direct = direct ? 1 : 0;
+    if (timing) {
+      HIPTRY(hipEventSynchronize(ds->dev_ev[direct ? 3 : 7]));
+      auto el = [&](int i, int j) {
+        float v = 0;
+        HIPTRY(hipEventElapsedTime(&v, ds->dev_ev[i], ds->dev_ev[j]));
+        return (double)v;
+      };
+      st->ms_len = el(0, 1);
+      st->ms_gather = el(2, 3);
+      st->ms_clean = direct ? 0.0 : el(4, 5) + el(6, 7);
+      st->ms_device = st->ms_len + st->ms_gather + st->ms_clean;
+    }
+  }
+  return n_out;
+}
+
 }  // namespace
 
 // ----------------------------------------------------------------------------- C ABI
@@ -978,6 +1190,76 @@ int ctok_encode_batch_device(const ctok* tc, const uint8_t* d_utf8, const uint64
     uint64_t n = encode_device(t, ds, d_utf8, d_doc_off, n_docs, n_bytes, d_ids, ids_cap, d_tok_off, s, timing, stats);
     if (n_tokens_out) *n_tokens_out = n;
     if (stats) stats->ms_total = now_ms() - t0;
+  });
+}
+
+int ctok_decode_batch_device(const ctok* tc, const uint32_t* d_ids, const uint64_t* d_tok_off, uint64_t n_docs,
+                             uint64_t n_ids, uint32_t options, uint8_t* d_out, uint64_t out_cap, uint64_t* d_out_off,
+                             uint64_t* n_bytes_out, const ctok_exec* exec, ctok_decode_stats* stats) {
+  if (!tc || !d_tok_off || !d_out_off || (n_ids && !d_ids)) return fail(CTOK_E_ARG, "null argument");
+  ctok* t = const_cast<ctok*>(tc);
+  return run([&] {
+    double t0 = now_ms();
+    int dev = exec ? exec->device : 0;
+    DeviceState* ds = device_state(t, dev);
+    std::lock_guard<std::mutex> lk(ds->mu);
+    HIPTRY(hipSetDevice(dev));
+    hipStream_t s = exec && exec->stream ? (hipStream_t)exec->stream : ds->stream;
+    bool timing = exec && (exec->flags & CTOK_F_TIMING);
+    auto get_out = [&](uint64_t n) -> uint8_t* {
+      if (n_bytes_out) *n_bytes_out = n;
+      if (n > out_cap) throw_err(CTOK_E_CAPACITY, "out_cap too small: *n_bytes_out holds the number of bytes needed");
+      if (n && !d_out) throw_err(CTOK_E_ARG, "null output buffer");
+      return d_out;
+    };
+    uint64_t n = decode_device(t, ds, d_ids, d_tok_off, n_docs, n_ids, options, get_out, d_out_off, s, timing, stats);
+    if (n_bytes_out) *n_bytes_out = n;
+    if (stats) stats->ms_total = now_ms() - t0;
+  });
+}
+
+int ctok_decode_batch(const ctok* tc, const uint32_t* ids, const uint64_t* tok_off, uint64_t n_docs, uint32_t options,
+                      uint8_t* out, uint64_t out_cap, uint64_t* out_off, const ctok_exec* exec,
+                      ctok_decode_stats* stats) {
+  if (!tc || !tok_off || !out_off) return fail(CTOK_E_ARG, "null argument");
+  ctok* t = const_cast<ctok*>(tc);
+  return run([&] {
+    double t0 = now_ms();
+    if (tok_off[0] != 0) throw_err(CTOK_E_ARG, "tok_off[0] must be 0");
+    for (uint64_t d = 0; d < n_docs; d++)
+      if (tok_off[d + 1] < tok_off[d]) throw_err(CTOK_E_ARG, "tok_off must be non-decreasing");
+    const uint64_t T = tok_off[n_docs];
+    if (T && !ids) throw_err(CTOK_E_ARG, "null ids");
+    int dev = exec ? exec->device : 0;
+    DeviceState* ds = device_state(t, dev);
+    std::lock_guard<std::mutex> lk(ds->mu);
+    HIPTRY(hipSetDevice(dev));
+    hipStream_t s = exec && exec->stream ? (hipStream_t)exec->stream : ds->stream;
+    bool timing = exec && (exec->flags & CTOK_F_TIMING);
+    double h0 = now_ms();
+    ds->dec_ids.ensure(T + 4);
+    ds->dec_tokoff.ensure(n_docs + 1);
+    ds->dec_outoff.ensure(n_docs + 1);
+    if (T) HIPTRY(hipMemcpyAsync(ds->dec_ids.p, ids, T * 4, hipMemcpyHostToDevice, s));
+    HIPTRY(hipMemcpyAsync(ds->dec_tokoff.p, tok_off, (n_docs + 1) * 8, hipMemcpyHostToDevice, s));
+    HIPTRY(hipStreamSynchronize(s));
+    double h1 = now_ms();
+    auto get_out = [&](uint64_t n) -> uint8_t* {
+      ds->dec_out.ensure(n + 16);
+      return ds->dec_out.p;
+    };
+    uint64_t n = decode_device(t, ds, ds->dec_ids.p, ds->dec_tokoff.p, n_docs, T, options, get_out, ds->dec_outoff.p,
+                               s, timing, stats);
+    double d0 = now_ms();
+    HIPTRY(hipMemcpyAsync(out_off, ds->dec_outoff.p, (n_docs + 1) * 8, hipMemcpyDeviceToHost, s));
+    if (n <= out_cap && n) HIPTRY(hipMemcpyAsync(out, ds->dec_out.p, n, hipMemcpyDeviceToHost, s));
+    HIPTRY(hipStreamSynchronize(s));
+    if (n > out_cap) throw_err(CTOK_E_CAPACITY, "out_cap too small: out_off[n_docs] holds the number of bytes needed");
+    if (stats) {
+      stats->ms_h2d = h1 - h0;
+      stats->ms_d2h = now_ms() - d0;
+      stats->ms_total = now_ms() - t0;
+    }
   });
 }
 

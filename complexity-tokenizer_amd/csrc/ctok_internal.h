@@ -154,6 +154,43 @@ struct Work {              // device pointers, sized by the host for one call
   uint64_t scan_tmp_cap;
 };
 
+// ---- decode (decode.hip): ids -> UTF-8 text -------------------------------------------
+// Per-id decode entry: x = offset of the id's decoded bytes in `bytes`, y = length [0,24) |
+// kDecNonAscii (a byte >= 0x80 among them) | kDecSpecial (the id's token is a special added token).
+constexpr uint32_t kDecLenMask = 0xFFFFFFu, kDecNonAscii = 1u << 30, kDecSpecial = 1u << 31;
+constexpr uint32_t kDecOptSkipSpecial = 1u, kDecOptCleanup = 2u;
+constexpr int kDecChunk = 4096;  // ids per workgroup of the gather pass (256 threads x 16)
+constexpr int kDecTile = 4096;   // bytes per workgroup of the clean-up passes (256 threads x 16)
+
+struct DecTables {
+  const uint2* ent;        // [n_ent]
+  uint32_t n_ent;
+  const uint8_t* bytes;    // every id's decoded bytes, each entry starting on a 4-byte boundary
+};
+
+struct DecWork {
+  const uint32_t* ids;     // [n_ids] input
+  uint32_t n_ids;
+  const uint64_t* tok_off; // [n_docs + 1] input
+  uint32_t n_docs;
+  uint32_t opts;           // kDecOpt*
+  uint32_t n_chunks;
+  uint32_t* chunk_off;     // [n_chunks + 1] decoded bytes per id chunk, scanned
+  uint8_t* raw;            // [n_raw + 64] decoded bytes before from_utf8_lossy / clean-up
+  uint32_t n_raw;
+  uint64_t* raw_off;       // [n_docs + 1]
+  uint32_t* delbits;       // [n_raw / 32 + 8] units the clean-up deletes (bit at the unit's first byte)
+  uint32_t n_tiles;
+  uint32_t* tile_cnt;      // [n_tiles + 1] output bytes per tile, scanned
+  uint32_t* counters;      // [0] error bits (1: bad offsets), [1] a decoded byte >= 0x80 exists
+};
+
+hipError_t launch_dec_len(const DecWork& w, const DecTables& t, uint32_t* tmp, uint64_t tmp_cap, hipStream_t s);
+hipError_t launch_dec_gather(const DecWork& w, const DecTables& t, uint8_t* dst, uint64_t* dst_off, hipStream_t s);
+hipError_t launch_dec_prepare(const DecWork& w, hipStream_t s);  // clean-up: trimmed and replaced units
+hipError_t launch_dec_count(const DecWork& w, uint32_t* tmp, uint64_t tmp_cap, hipStream_t s);
+hipError_t launch_dec_write(const DecWork& w, uint8_t* out, uint64_t* out_off, hipStream_t s);
+
 // ---- launchers (kernels.hip) -----------------------------------------------------------
 void upload_done();
 hipError_t launch_docstart(const Work& w, hipStream_t s);

@@ -106,6 +106,50 @@ int ctok_encode_batch_device(const ctok* tok, const uint8_t* d_utf8, const uint6
                              uint64_t* d_tok_off, uint64_t* n_tokens_out,
                              const ctok_exec* exec, ctok_stats* stats);
 
+/* ---------------------------------------------------------------- decode (ids -> UTF-8 text)
+ * decode_impl, src/huggingface/mod.rs:710-747, per document:
+ *   - skip_special_tokens drops ids whose model.vocab string is a special added token (:716-726);
+ *   - ids are looked up in model.vocab only (Vocab::get_token, src/vocab.rs:91-93); unknown ids
+ *     are dropped;
+ *   - the ByteLevel decoder maps the tokens' chars back to bytes, then from_utf8_lossy
+ *     (src/decoders.rs:94-119); an unknown decoder type joins the raw token strings
+ *     (BpeTokenizer::decode, src/bpe.rs:170-176); other decoders -> CTOK_E_UNSUPPORTED;
+ *   - clean_up_tokenization_spaces: 15 replaces, then split_whitespace joined by ' ' (:749-767). */
+#define CTOK_D_SKIP_SPECIAL 1u  /* skip_special_tokens                          */
+#define CTOK_D_CLEANUP 2u       /* clean_up_tokenization_spaces (the default on) */
+
+typedef struct ctok_decode_stats {
+  double ms_total;        /* wall time of the call (host clock)                          */
+  double ms_device;       /* ms_len + ms_gather + ms_clean                                */
+  double ms_len;          /* offsets check + decoded bytes per id chunk + scan (HIP events) */
+  double ms_gather;       /* id -> bytes gather                                           */
+  double ms_clean;        /* lossy UTF-8 + clean-up: mark, count, scan, write            */
+  double ms_h2d, ms_d2h;  /* host-buffer copies (ctok_decode_batch only)                  */
+  uint64_t ids, docs;
+  uint64_t bytes_raw;     /* decoded bytes before lossy UTF-8 / clean-up                  */
+  uint64_t bytes_out;     /* output bytes                                                 */
+  uint32_t direct;        /* 1: no clean-up and all bytes ASCII, the gather wrote the output */
+} ctok_decode_stats;
+
+/* Tokenizer.decode_batch_with_options(batch, skip_special_tokens, clean_up_tokenization_spaces)
+ *   src/bindings/tokenizer.rs:231-238 -> src/huggingface/mod.rs:777-785; decode_batch (:226-228
+ *   -> :771-773), decode (:212-214), decode_with_options (:217-224) and batch_decode (:656-663)
+ *   are the same call with options CTOK_D_CLEANUP and/or one document.
+ * ids[tok_off[d] .. tok_off[d+1]) are document d's ids (tok_off[0] == 0, non-decreasing).  On
+ * success out[out_off[d] .. out_off[d+1]) is its UTF-8 text.  out_cap too small -> CTOK_E_CAPACITY
+ * with out_off filled (out_off[n_docs] = bytes needed). */
+int ctok_decode_batch(const ctok* tok, const uint32_t* ids, const uint64_t* tok_off, uint64_t n_docs,
+                      uint32_t options, uint8_t* out, uint64_t out_cap, uint64_t* out_off,
+                      const ctok_exec* exec, ctok_decode_stats* stats);
+
+/* Same, with ids / tok_off / out / out_off resident in HBM of exec->device and the work ordered
+ * on exec->stream; n_ids = tok_off[n_docs].  *n_bytes_out receives the output size (also on
+ * CTOK_E_CAPACITY, when out_cap is too small and nothing is written). */
+int ctok_decode_batch_device(const ctok* tok, const uint32_t* d_ids, const uint64_t* d_tok_off, uint64_t n_docs,
+                             uint64_t n_ids, uint32_t options, uint8_t* d_out, uint64_t out_cap,
+                             uint64_t* d_out_off, uint64_t* n_bytes_out, const ctok_exec* exec,
+                             ctok_decode_stats* stats);
+
 /* Number of HIP devices visible to the library (0 when none; encode calls then fail with
  * CTOK_E_DEVICE -- there is no CPU fallback). */
 int ctok_device_count(void);

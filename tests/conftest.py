@@ -40,3 +40,4 @@ def llama3_path(fixture_dir):
 def multi_path(fixture_dir):
     from datagen.build_tokenizers import fixture_path
     return fixture_path("multi_32k", fixture_dir)
+

@@ -126,6 +126,28 @@ def test_encode_without_gpu_fails_loudly(gpt2_path):
         tok.encode("hello world")
 
 
+@pytest.mark.skipif(ct.device_count() > 0, reason="a HIP device is present")
+def test_decode_without_gpu_fails_loudly(gpt2_path):
+    tok = Tokenizer.from_file(gpt2_path)
+    with pytest.raises(ct.DeviceError):
+        tok.decode([1, 2, 3])
+    with pytest.raises(ct.DeviceError):
+        tok.decode_batch([[1], []])
+
+
+def test_pack_ids_type_errors():
+    ids, off = ct.pack_ids([[1, 2], [], [3]])
+    assert ids.tolist() == [1, 2, 3] and off.tolist() == [0, 2, 2, 3]
+    with pytest.raises(TypeError):
+        ct.pack_ids("abc")
+    with pytest.raises(TypeError):
+        ct.pack_ids([[1, "x"]])
+    with pytest.raises(OverflowError):
+        ct.pack_ids([[-1]])
+    with pytest.raises(OverflowError):
+        ct.pack_ids([[2 ** 32]])
+
+
 def test_shard_bounds_cover_and_balance():
     from complexity_tokenizer.parallel import concat_results, shard_bounds
     rng = np.random.default_rng(0)

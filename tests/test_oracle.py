@@ -368,3 +368,63 @@ def test_hf_tokenizers_agree_on_shared_domain(gpt2_path, gpt2_obj):
         if rng.random() < 0.5:
             s = " " + s
         assert hf.encode(s, add_special_tokens=False).ids == py.encode(s), repr(s)
+
+
+# ----------------------------------------------------------------------------- decode oracles
+
+
+def test_decode_kat_byte_level():
+    """reference src/decoders.rs:275-281."""
+    out = ref_py.byte_level_decode(["\u0120Hello", "\u0120world"])
+    assert "Hello" in out and out == " Hello world"
+
+
+def test_from_utf8_lossy_matches_python_codec():
+    """Rust from_utf8_lossy and CPython's 'replace' error handler both substitute one U+FFFD per
+    maximal subpart (Unicode 'best practice'); checked on random and adversarial byte strings."""
+    import random
+    rng = random.Random(3)
+    special = [0x80, 0xBF, 0xC0, 0xC1, 0xC2, 0xDF, 0xE0, 0xED, 0xEF, 0xF0, 0xF4, 0xF5, 0xFF, 0x9F, 0xA0, 0x90, 0x8F]
+    for _ in range(100000):
+        b = bytes(rng.choice(special) if rng.random() < 0.6 else rng.randrange(256) for _ in range(rng.randint(0, 9)))
+        assert ref_py.from_utf8_lossy(b) == b.decode("utf-8", "replace"), b
+
+
+def test_cleanup_rules():
+    f = ref_py.clean_up_tokenization_spaces_
+    assert f("a , b . c") == "a, b. c"
+    assert f(" - - ") == "--"
+    assert f('say " hi " now') == 'say"hi"now'
+    assert f("x\u001cy z") == "x\u001cy z"  # U+001C is not White_Space (Python's split would split)
+    assert f("\u3000x\u00a0\u0085y ") == "x y"
+
+
+def test_parse_decoder_variants():
+    pd = ref_py.parse_decoder
+    assert pd(None) == ("ByteLevel",) and pd("x") == ("ByteLevel",) and pd({}) == ("ByteLevel",)
+    assert pd({"type": "ByteLevel"}) == ("ByteLevel",)
+    assert pd({"type": "Unknown"}) == ("Raw",) and pd({"type": 3}) == ("Raw",)
+    assert pd({"type": "Fuse"}) == ("Raw",)
+    assert pd({"type": "Metaspace"})[0] == "unsupported"
+    assert pd({"type": "Sequence", "decoders": [{"type": "ByteLevel"}, {"type": "Fuse"}]}) == ("ByteLevel",)
+    assert pd({"type": "Sequence", "decoders": [{"type": "Nope"}]}) == ("Raw",)
+    assert pd({"type": "Sequence", "decoders": ["x"]}) == ("ByteLevel",)
+    assert pd({"type": "Sequence", "decoders": [{"type": "ByteLevel"}, {}]})[0] == "unsupported"
+    assert pd({"type": "Sequence", "decoders": [{"type": "WordPiece"}]})[0] == "unsupported"
+
+
+@pytest.mark.parametrize("name", ["gpt2_50k", "multi_32k", "llama3_128k"])
+def test_decode_oracles_agree(name, fixture_dir):
+    from datagen.build_tokenizers import fixture_path
+    from tests import decode_cases
+    with open(fixture_path(name, fixture_dir)) as f:
+        obj = json.load(f)
+    py = ref_py.RefTokenizer(obj)
+    rc = ref_c.RefC(obj)
+    special = list(py.special_tokens.values())
+    batch = decode_cases.random_batches(len(py.id_to_token_map), 400, 5, special_ids=special)
+    batch += decode_cases.split_docs(batch[:100], 6)
+    batch += [py.encode(t) for t in decode_cases.CLEANUP_TEXTS]
+    for skip in (False, True):
+        for clean in (False, True):
+            assert rc.decode_batch(batch, skip, clean, threads=4) == py.decode_batch(batch, skip, clean)
