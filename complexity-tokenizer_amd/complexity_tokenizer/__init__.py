@@ -15,6 +15,7 @@ Example:
 from __future__ import annotations
 
 import ctypes
+import gc
 import os
 
 import numpy as np
@@ -100,12 +101,32 @@ def pack_ids(batch) -> tuple[np.ndarray, np.ndarray]:
     return np.asarray(flat, dtype=np.uint64).astype(np.uint32), off
 
 
+def _split_lists(flat: np.ndarray, off: np.ndarray) -> list:
+    """(flat uint array, offsets[D+1]) -> D Python lists.  The cyclic garbage collector is paused
+    while the lists are built: creating ~1e5 container objects otherwise triggers collections
+    that rescan every list built so far (3x the cost of the conversion itself)."""
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        f = flat.tolist()
+        o = off.tolist()
+        return [f[o[i]:o[i + 1]] for i in range(len(o) - 1)]
+    finally:
+        if was:
+            gc.enable()
+
+
 class Tokenizer:
     """HuggingFace-format ByteLevel-BPE tokenizer whose encode path runs on an MI355X."""
 
     def __init__(self, handle):
         self._h = ctypes.c_void_p(handle)
         self.device = int(os.environ.get("CTOK_DEVICE", "0"))
+        # host-buffer encode over several GPUs of this process (byte-balanced doc shards, one
+        # host thread per device): e.g. tok.devices = list(range(device_count()))
+        env = os.environ.get("CTOK_DEVICES", "")
+        self.devices = [int(x) for x in env.split(",") if x.strip()] or None
+        self.chunk_mb = 0  # pipeline chunk of the host-buffer path (0 = library default)
         self.last_stats = None
         self.last_decode_stats = None
 
@@ -208,7 +229,7 @@ class Tokenizer:
         while True:
             ids = np.empty(max(cap, 1), dtype=np.uint32)
             tok_off = np.empty(n_docs + 1, dtype=np.uint64)
-            ex = _n.Exec(self.device, None, _n.CTOK_F_TIMING if timing else 0)
+            ex = self._host_exec(timing)
             st = _n.Stats()
             rc = _n.lib.ctok_encode_batch(self._h, text.ctypes.data, off.ctypes.data, n_docs, ids.ctypes.data, cap,
                                           tok_off.ctypes.data, ctypes.byref(ex), ctypes.byref(st))
@@ -219,6 +240,16 @@ class Tokenizer:
                 _raise(rc)
             self.last_stats = st.as_dict()
             return ids[: int(tok_off[-1])], tok_off
+
+    def _host_exec(self, timing: bool):
+        ex = _n.Exec(self.device, None, _n.CTOK_F_TIMING if timing else 0)
+        if self.devices:
+            arr = (ctypes.c_int * len(self.devices))(*[int(d) for d in self.devices])
+            ex.devices = ctypes.cast(arr, ctypes.POINTER(ctypes.c_int))
+            ex.n_devices = len(self.devices)
+            ex._keep = arr  # keeps the array alive as long as the struct
+        ex.chunk_mb = int(self.chunk_mb)
+        return ex
 
     def encode_packed_device(self, d_text: int, d_off: int, n_docs: int, n_bytes: int, d_ids: int, ids_cap: int,
                              d_tok_off: int, stream: int = 0, timing: bool = False, device: int | None = None):
@@ -243,9 +274,7 @@ class Tokenizer:
     def encode_batch(self, texts) -> list:
         """src/bindings/tokenizer.rs:207-210 -> src/huggingface/mod.rs:694-696."""
         ids, tok_off = self.encode_batch_flat(texts)
-        flat = ids.tolist()
-        o = tok_off.tolist()
-        return [flat[o[i]:o[i + 1]] for i in range(len(o) - 1)]
+        return _split_lists(ids, tok_off)
 
     def encode(self, text: str) -> list:
         """src/bindings/tokenizer.rs:203-205 -> src/huggingface/mod.rs:551-613."""

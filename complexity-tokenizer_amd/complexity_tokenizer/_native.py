@@ -53,7 +53,9 @@ CTOK_F_TIMING = 1
 
 
 class Exec(ctypes.Structure):
-    _fields_ = [("device", ctypes.c_int), ("stream", ctypes.c_void_p), ("flags", ctypes.c_uint32)]
+    _fields_ = [("device", ctypes.c_int), ("stream", ctypes.c_void_p), ("flags", ctypes.c_uint32),
+                ("devices", ctypes.POINTER(ctypes.c_int)), ("n_devices", ctypes.c_int),
+                ("chunk_mb", ctypes.c_uint32), ("host_threads", ctypes.c_uint32)]
 
 
 class Stats(ctypes.Structure):

@@ -21,6 +21,7 @@
 #include <memory>
 #include <mutex>
 #include <sstream>
+#include <thread>
 #include <string>
 #include <unordered_map>
 #include <unordered_set>
@@ -156,6 +157,37 @@ struct DevBuf {
   ~DevBuf() { if (p) (void)hipFree(p); }
 };
 
+// Pinned (page-locked) host buffer: the staging side of the host-buffer pipeline.
+template <typename T>
+struct PinBuf {
+  T* p = nullptr;
+  size_t cap = 0;  // elements
+  void ensure(size_t n) {
+    if (n <= cap && p) return;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    size_t want = std::max<size_t>(n + n / 8, 1024);
+    HIPTRY(hipHostMalloc((void**)&p, want * sizeof(T), hipHostMallocDefault));
+    cap = want;
+  }
+  ~PinBuf() { if (p) (void)hipHostFree(p); }
+};
+
+// Double-buffered host-buffer pipeline of one device (ctok_encode_batch): chunk c's text is
+// staged into pin_in[c & 1] and copied to d_in[c & 1] on the copy stream while chunk c - 1 is
+// encoded; its ids come back through d_ids / pin_ids[c & 1] while chunk c + 1 is encoded.
+struct HostPipe {
+  hipStream_t up = nullptr, down = nullptr;  // H2D and D2H copy streams (both directions at once)
+  hipEvent_t ev_h2d[2] = {}, ev_enc[2] = {}, ev_d2h[2] = {};
+  hipEvent_t ev_t[4] = {};  // timing of the first chunk's H2D and the last chunk's D2H
+  PinBuf<uint8_t> pin_in[2];
+  PinBuf<uint64_t> pin_off[2], pin_tokoff[2];
+  PinBuf<uint32_t> pin_ids[2];
+  DevBuf<uint8_t> d_in[2];
+  DevBuf<uint64_t> d_off[2], d_tokoff[2];
+  DevBuf<uint32_t> d_ids[2];
+};
+
 struct DeviceState {
   int device = -1;
   uint32_t n_cus = 1;
@@ -195,12 +227,21 @@ struct DeviceState {
   DevBuf<uint32_t> dec_ids;
   hipEvent_t dev_ev[8] = {};
   // host-API staging
-  DevBuf<uint8_t> in_text;
-  DevBuf<uint64_t> in_off, out_off;
-  DevBuf<uint32_t> out_ids;
+  std::unique_ptr<HostPipe> pipe;
   ~DeviceState() {
     if (device >= 0) {
       (void)hipSetDevice(device);
+      if (pipe) {
+        for (int i = 0; i < 2; i++) {
+          if (pipe->ev_h2d[i]) (void)hipEventDestroy(pipe->ev_h2d[i]);
+          if (pipe->ev_enc[i]) (void)hipEventDestroy(pipe->ev_enc[i]);
+          if (pipe->ev_d2h[i]) (void)hipEventDestroy(pipe->ev_d2h[i]);
+        }
+        for (auto& e : pipe->ev_t) if (e) (void)hipEventDestroy(e);
+        if (pipe->up) (void)hipStreamDestroy(pipe->up);
+        if (pipe->down) (void)hipStreamDestroy(pipe->down);
+        pipe.reset();
+      }
       for (auto& e : ev) if (e) (void)hipEventDestroy(e);
       for (auto& e : dev_ev) if (e) (void)hipEventDestroy(e);
       if (ev_sync) (void)hipEventDestroy(ev_sync);
@@ -1086,6 +1127,192 @@ uint64_t decode_device(ctok* t, DeviceState* ds, const uint32_t* d_ids, const ui
   return n_out;
 }
 
+// ----------------------------------------------------------------------------- host-buffer pipeline
+//
+// ctok_encode_batch on host memory.  The batch is cut into chunks of about `chunk` text bytes
+// (whole documents); per chunk c (slot c & 1):
+//   stage   host threads copy the chunk's text into pinned pin_in and its rebased offsets into
+//           pin_off, then the copy stream moves them to d_in / d_off           (ev_h2d)
+//   encode  the encode stream waits for ev_h2d (and for the D2H of chunk c - 2, which used the
+//           same d_ids), runs encode_device                                    (ev_enc)
+//   drain   the copy stream moves ids / tok_off to pinned pin_ids / pin_tokoff (ev_d2h), host
+//           threads copy them to the caller's ids (at the running token base) and tok_off.
+// stage(c + 1) and drain(c - 1) run on helper threads while encode(c) runs, so PCIe traffic in
+// both directions and the host copies overlap the kernels.  The caller's buffers are never
+// registered: pinning them costs more per call than the staging copies.
+
+// memcpy split over up to `nt` threads (the calling thread takes the first part)
+void par_copy(void* dst, const void* src, size_t n, unsigned nt) {
+  constexpr size_t kMin = 4u << 20;
+  unsigned k = (unsigned)std::min<size_t>(nt, std::max<size_t>(1, n / kMin));
+  if (k <= 1) {
+    if (n) std::memcpy(dst, src, n);
+    return;
+  }
+  const size_t per = (n + k - 1) / k;
+  std::vector<std::thread> th;
+  for (unsigned i = 1; i < k; i++) {
+    const size_t a = i * per, b = std::min(n, a + per);
+    if (a < b) th.emplace_back([=] { std::memcpy((char*)dst + a, (const char*)src + a, b - a); });
+  }
+  std::memcpy(dst, src, std::min(n, per));
+  for (auto& x : th) x.join();
+}
+
+HostPipe* host_pipe(DeviceState* ds) {
+  if (ds->pipe) return ds->pipe.get();
+  auto p = std::make_unique<HostPipe>();
+  HIPTRY(hipStreamCreateWithFlags(&p->up, hipStreamNonBlocking));
+  HIPTRY(hipStreamCreateWithFlags(&p->down, hipStreamNonBlocking));
+  for (int i = 0; i < 2; i++) {
+    HIPTRY(hipEventCreateWithFlags(&p->ev_h2d[i], hipEventDisableTiming));
+    HIPTRY(hipEventCreateWithFlags(&p->ev_enc[i], hipEventDisableTiming));
+    HIPTRY(hipEventCreateWithFlags(&p->ev_d2h[i], hipEventDisableTiming));
+  }
+  for (auto& e : p->ev_t) HIPTRY(hipEventCreate(&e));
+  ds->pipe = std::move(p);
+  return ds->pipe.get();
+}
+
+struct RangeOut {
+  uint64_t ntok = 0;     // ids of the range
+  bool overflow = false;  // ntok > cap: nothing past cap was written
+};
+
+// Encode docs [d0, d1) of a host batch on one device; ids go to ids[0, cap), tok_off[i] (i in
+// [1, d1 - d0]) = ids of docs d0 .. d0 + i - 1 (tok_off[0] is not written: with several shards
+// it is the previous shard's last entry).  The device lock is held by the caller.
+RangeOut encode_host_range(ctok* t, DeviceState* ds, const uint8_t* text, const uint64_t* off, uint64_t d0,
+                           uint64_t d1, uint32_t* ids, uint64_t cap, uint64_t* tok_off, uint64_t chunk,
+                           unsigned nthreads, bool timing, ctok_stats* st) {
+  RangeOut r;
+  if (d1 <= d0) return r;
+  HostPipe* P = host_pipe(ds);
+  hipStream_t s = ds->stream;
+  // chunk boundaries: whole docs, about `chunk` bytes each (a longer doc is a chunk by itself)
+  std::vector<uint64_t> cut{d0};
+  while (cut.back() < d1) {
+    const uint64_t a = cut.back();
+    const uint64_t* e = std::upper_bound(off + a + 1, off + d1 + 1, off[a] + chunk);
+    uint64_t b = (uint64_t)(e - off) - 1;  // last doc end <= off[a] + chunk
+    if (b <= a) b = a + 1;
+    cut.push_back(std::min(b, d1));
+  }
+  const size_t C = cut.size() - 1;
+  std::vector<uint64_t> ntok(C, 0), base(C + 1, 0);
+  double ms_h2d = 0, ms_d2h = 0, ms_dev = 0, ms_pre = 0, ms_bs = 0, ms_bl = 0, ms_em = 0, ms_seg = 0, ms_lo = 0, ms_hi = 0;
+
+  auto stage = [&](size_t c) {
+    const int k = (int)(c & 1);
+    const uint64_t a = cut[c], b = cut[c + 1], n = b - a, B = off[b] - off[a];
+    HIPTRY(hipEventSynchronize(P->ev_h2d[k]));  // chunk c - 2's H2D from these pinned buffers
+    P->pin_in[k].ensure(B + 16);
+    P->pin_off[k].ensure(n + 1);
+    par_copy(P->pin_in[k].p, text + off[a], B, nthreads);
+    std::memset(P->pin_in[k].p + B, 0, 16);
+    for (uint64_t i = 0; i <= n; i++) P->pin_off[k].p[i] = off[a + i] - off[a];
+    if (timing && c == 0) HIPTRY(hipEventRecord(P->ev_t[0], P->up));
+    HIPTRY(hipMemcpyAsync(P->d_in[k].p, P->pin_in[k].p, B + 16, hipMemcpyHostToDevice, P->up));
+    HIPTRY(hipMemcpyAsync(P->d_off[k].p, P->pin_off[k].p, (n + 1) * 8, hipMemcpyHostToDevice, P->up));
+    if (timing && c == 0) HIPTRY(hipEventRecord(P->ev_t[1], P->up));
+    HIPTRY(hipEventRecord(P->ev_h2d[k], P->up));
+  };
+  auto drain = [&](size_t c) {
+    const int k = (int)(c & 1);
+    const uint64_t a = cut[c], n = cut[c + 1] - a;
+    HIPTRY(hipEventSynchronize(P->ev_d2h[k]));
+    const uint64_t b0 = base[c], nt = ntok[c];
+    if (b0 < cap) par_copy(ids + b0, P->pin_ids[k].p, std::min(nt, cap - b0) * 4, nthreads);
+    const uint64_t* to = P->pin_tokoff[k].p;
+    uint64_t* dst = tok_off + (a - d0);
+    for (uint64_t i = 1; i <= n; i++) dst[i] = b0 + to[i];
+  };
+  // device buffers sized for the largest chunk up front (no reallocation while copies are in flight)
+  {
+    uint64_t maxB = 0, maxD = 0;
+    for (size_t c = 0; c < C; c++) {
+      maxB = std::max(maxB, off[cut[c + 1]] - off[cut[c]]);
+      maxD = std::max(maxD, cut[c + 1] - cut[c]);
+    }
+    for (int k = 0; k < 2; k++) {
+      P->d_in[k].ensure(maxB + 16);
+      P->d_off[k].ensure(maxD + 1);
+      P->d_tokoff[k].ensure(maxD + 1);
+      P->d_ids[k].ensure(ctok_ids_bound(t, maxB, maxD));
+    }
+  }
+  stage(0);
+  for (size_t c = 0; c < C; c++) {
+    const int k = (int)(c & 1);
+    const uint64_t a = cut[c], n = cut[c + 1] - a, B = off[cut[c + 1]] - off[a];
+    // helper threads; an exception inside one is rethrown here after the join
+    std::exception_ptr ex_stage, ex_drain;
+    std::thread th_stage, th_drain;
+    if (c + 1 < C)
+      th_stage = std::thread([&, c] {
+        try { stage(c + 1); } catch (...) { ex_stage = std::current_exception(); }
+      });
+    if (c >= 1)
+      th_drain = std::thread([&, c] {
+        try { drain(c - 1); } catch (...) { ex_drain = std::current_exception(); }
+      });
+    struct Joiner {
+      std::thread& a;
+      std::thread& b;
+      ~Joiner() {
+        if (a.joinable()) a.join();
+        if (b.joinable()) b.join();
+      }
+    } joiner{th_stage, th_drain};
+    HIPTRY(hipStreamWaitEvent(s, P->ev_h2d[k], 0));
+    HIPTRY(hipStreamWaitEvent(s, P->ev_d2h[k], 0));  // chunk c - 2's ids have left d_ids[k]
+    ctok_stats cs{};
+    ntok[c] = encode_device(t, ds, P->d_in[k].p, P->d_off[k].p, n, B, P->d_ids[k].p, P->d_ids[k].cap,
+                            P->d_tokoff[k].p, s, timing, &cs);
+    base[c + 1] = base[c] + ntok[c];
+    if (st) {
+      st->pieces += cs.pieces;
+      st->long_pieces += cs.long_pieces;
+      st->nfc_docs += cs.nfc_docs;
+      st->bytes_norm += cs.bytes_norm;
+      for (int q = 0; q < 3; q++) {
+        st->class_bytes[q] += cs.class_bytes[q];
+        st->class_ids[q] += cs.class_ids[q];
+      }
+      ms_dev += cs.ms_device, ms_pre += cs.ms_pretok, ms_bs += cs.ms_bpe_short, ms_bl += cs.ms_bpe_long;
+      ms_em += cs.ms_emit, ms_seg += cs.ms_segment, ms_lo += cs.ms_bpe_lo, ms_hi += cs.ms_bpe_hi;
+    }
+    if (th_drain.joinable()) th_drain.join();  // pin_ids[k ^ 1] is free again
+    if (ex_drain) std::rethrow_exception(ex_drain);
+    // D2H of chunk c (encode_device returned, so its ids are complete)
+    P->pin_ids[k].ensure(ntok[c] + 1);
+    P->pin_tokoff[k].ensure(n + 1);
+    HIPTRY(hipEventRecord(P->ev_enc[k], s));
+    HIPTRY(hipStreamWaitEvent(P->down, P->ev_enc[k], 0));
+    if (timing && c + 1 == C) HIPTRY(hipEventRecord(P->ev_t[2], P->down));
+    if (ntok[c]) HIPTRY(hipMemcpyAsync(P->pin_ids[k].p, P->d_ids[k].p, ntok[c] * 4, hipMemcpyDeviceToHost, P->down));
+    HIPTRY(hipMemcpyAsync(P->pin_tokoff[k].p, P->d_tokoff[k].p, (n + 1) * 8, hipMemcpyDeviceToHost, P->down));
+    if (timing && c + 1 == C) HIPTRY(hipEventRecord(P->ev_t[3], P->down));
+    HIPTRY(hipEventRecord(P->ev_d2h[k], P->down));
+    if (th_stage.joinable()) th_stage.join();
+    if (ex_stage) std::rethrow_exception(ex_stage);
+  }
+  drain(C - 1);
+  r.ntok = base[C];
+  r.overflow = r.ntok > cap;
+  if (st && timing) {
+    float v = 0;
+    HIPTRY(hipEventElapsedTime(&v, P->ev_t[0], P->ev_t[1]));
+    ms_h2d = v;
+    HIPTRY(hipEventElapsedTime(&v, P->ev_t[2], P->ev_t[3]));
+    ms_d2h = v;
+    st->ms_h2d += ms_h2d, st->ms_d2h += ms_d2h, st->ms_device += ms_dev, st->ms_pretok += ms_pre;
+    st->ms_bpe_short += ms_bs, st->ms_bpe_long += ms_bl, st->ms_emit += ms_em, st->ms_segment += ms_seg;
+    st->ms_bpe_lo += ms_lo, st->ms_bpe_hi += ms_hi;
+  }
+  return r;
+}
+
 }  // namespace
 
 // ----------------------------------------------------------------------------- C ABI
@@ -1274,32 +1501,132 @@ int ctok_encode_batch(const ctok* tc, const uint8_t* utf8_in, const uint64_t* do
       if (doc_off[d + 1] < doc_off[d]) throw_err(CTOK_E_ARG, "doc_off must be non-decreasing");
     const uint64_t B = doc_off[n_docs];
     if (B && !utf8_in) throw_err(CTOK_E_ARG, "null text");
-    int dev = exec ? exec->device : 0;
-    DeviceState* ds = device_state(t, dev);
-    std::lock_guard<std::mutex> lk(ds->mu);
-    HIPTRY(hipSetDevice(dev));
-    hipStream_t s = exec && exec->stream ? (hipStream_t)exec->stream : ds->stream;
-    bool timing = exec && (exec->flags & CTOK_F_TIMING);
-    double h0 = now_ms();
-    ds->in_text.ensure(B + 16);
-    ds->in_off.ensure(n_docs + 1);
-    ds->out_off.ensure(n_docs + 1);
-    const uint64_t cap_dev = ctok_ids_bound(t, B, n_docs);
-    ds->out_ids.ensure(cap_dev);
-    if (B) HIPTRY(hipMemcpyAsync(ds->in_text.p, utf8_in, B, hipMemcpyHostToDevice, s));
-    HIPTRY(hipMemcpyAsync(ds->in_off.p, doc_off, (n_docs + 1) * 8, hipMemcpyHostToDevice, s));
-    HIPTRY(hipStreamSynchronize(s));
-    double h1 = now_ms();
-    uint64_t n = encode_device(t, ds, ds->in_text.p, ds->in_off.p, n_docs, B, ds->out_ids.p, ds->out_ids.cap,
-                               ds->out_off.p, s, timing, stats);
-    double d0 = now_ms();
-    HIPTRY(hipMemcpyAsync(tok_off, ds->out_off.p, (n_docs + 1) * 8, hipMemcpyDeviceToHost, s));
-    if (n <= ids_cap && n) HIPTRY(hipMemcpyAsync(ids, ds->out_ids.p, n * 4, hipMemcpyDeviceToHost, s));
-    HIPTRY(hipStreamSynchronize(s));
-    if (n > ids_cap) throw_err(CTOK_E_CAPACITY, "ids_cap too small: tok_off[n_docs] holds the number of ids needed");
+    if (ids_cap && !ids) throw_err(CTOK_E_ARG, "null ids");
+    std::vector<int> devs;
+    if (exec && exec->devices && exec->n_devices > 0) devs.assign(exec->devices, exec->devices + exec->n_devices);
+    else devs.push_back(exec ? exec->device : 0);
+    const bool timing = exec && (exec->flags & CTOK_F_TIMING);
+    const uint64_t chunk = (uint64_t)(exec && exec->chunk_mb ? exec->chunk_mb : 32u) << 20;
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const unsigned nthr = exec && exec->host_threads ? exec->host_threads
+                                                     : std::max(1u, std::min(8u, hw / (2u * (unsigned)devs.size())));
+    if (stats) *stats = ctok_stats{};
+    // shards: contiguous doc ranges balanced by bytes (cut at the first doc start >= k * B / G)
+    const size_t G = devs.size();
+    std::vector<uint64_t> cut(G + 1, 0);
+    for (size_t g = 1; g < G; g++) {
+      const uint64_t target = B / G * g;
+      cut[g] = (uint64_t)(std::lower_bound(doc_off, doc_off + n_docs, target) - doc_off);
+      cut[g] = std::max(cut[g], cut[g - 1]);
+    }
+    cut[G] = n_docs;
+    // output placement: shard g writes its ids at region[g] of the caller's buffer, sized for
+    // ids <= bytes + docs (true unless NFC grows the text or a prefix space is added) when the
+    // regions fit, else into a private buffer; a shard that outgrows its region runs again
+    std::vector<uint64_t> region(G + 1, 0);
+    for (size_t g = 0; g < G; g++)
+      region[g + 1] = region[g] + (doc_off[cut[g + 1]] - doc_off[cut[g]]) + (cut[g + 1] - cut[g]);
+    std::vector<std::unique_ptr<uint32_t[]>> priv(G);
+    std::vector<RangeOut> res(G);
+    std::vector<ctok_stats> sst(G);
+    // one pass over all shards; in_place: shard g writes at region[g] of the caller's ids, else
+    // into priv[g] of priv_size[g] ids
+    auto attempt = [&](bool in_place, const std::vector<uint64_t>& priv_size) {
+      std::vector<std::exception_ptr> err(G);
+      auto shard = [&](size_t g) {
+        try {
+          DeviceState* ds = device_state(t, devs[g]);
+          std::lock_guard<std::mutex> lk(ds->mu);
+          HIPTRY(hipSetDevice(devs[g]));
+          uint32_t* out = ids;
+          uint64_t cap = ids_cap;
+          if (G > 1) {
+            if (in_place) {
+              out = ids + region[g];
+              cap = region[g + 1] - region[g];
+            } else {
+              priv[g].reset(new uint32_t[priv_size[g] + 1]);  // no zero fill: ids[0, ntok) are written
+              out = priv[g].get();
+              cap = priv_size[g] + 1;
+            }
+          }
+          sst[g] = ctok_stats{};
+          res[g] = encode_host_range(t, ds, utf8_in, doc_off, cut[g], cut[g + 1], out, cap, tok_off + cut[g], chunk,
+                                     nthr, timing, stats ? &sst[g] : nullptr);
+        } catch (...) {
+          err[g] = std::current_exception();
+        }
+      };
+      if (G == 1) {
+        shard(0);
+      } else {
+        std::vector<std::thread> th;
+        for (size_t g = 0; g < G; g++) th.emplace_back(shard, g);
+        for (auto& x : th) x.join();
+      }
+      for (size_t g = 0; g < G; g++)
+        if (err[g]) std::rethrow_exception(err[g]);
+    };
+    tok_off[0] = 0;
+    bool in_place = G == 1 || region[G] <= ids_cap;
+    {
+      std::vector<uint64_t> sz(G);
+      for (size_t g = 0; g < G; g++) sz[g] = region[g + 1] - region[g];
+      attempt(in_place, sz);
+    }
+    uint64_t total = 0;
+    bool overflow = false;
+    for (size_t g = 0; g < G; g++) total += res[g].ntok, overflow |= res[g].overflow;
+    if (G > 1 && overflow && total <= ids_cap) {
+      // a shard outgrew its id bound region (NFC growth): again, into private buffers of the
+      // now known sizes
+      std::vector<uint64_t> sz(G);
+      for (size_t g = 0; g < G; g++) sz[g] = res[g].ntok;
+      in_place = false;
+      attempt(false, sz);
+    }
+    if (G > 1) {
+      // rebase: tok_off of shard g gets the ids of shards < g added; its ids move from
+      // region[g] (or priv[g]) to that base.  In place, the regions start at or after their
+      // destinations, so moving in shard order never overwrites ids not yet moved.
+      uint64_t basev = 0;
+      for (size_t g = 0; g < G; g++) {
+        const uint64_t n = res[g].ntok;
+        if (g > 0)
+          for (uint64_t d = cut[g] + 1; d <= cut[g + 1]; d++) tok_off[d] += basev;
+        if (total <= ids_cap && n) {
+          if (in_place) {
+            if (region[g] != basev) std::memmove(ids + basev, ids + region[g], n * 4);
+          } else {
+            std::memcpy(ids + basev, priv[g].get(), n * 4);
+          }
+        }
+        basev += n;
+      }
+    }
+    tok_off[n_docs] = total;
+    if (total > ids_cap) throw_err(CTOK_E_CAPACITY, "ids_cap too small: tok_off[n_docs] holds the number of ids needed");
     if (stats) {
-      stats->ms_h2d = h1 - h0;
-      stats->ms_d2h = now_ms() - d0;
+      for (size_t g = 0; g < G; g++) {
+        const ctok_stats& q = sst[g];
+        stats->pieces += q.pieces, stats->long_pieces += q.long_pieces, stats->nfc_docs += q.nfc_docs;
+        stats->bytes_norm += q.bytes_norm;
+        for (int c = 0; c < 3; c++) stats->class_bytes[c] += q.class_bytes[c], stats->class_ids[c] += q.class_ids[c];
+        // device times: the slowest shard
+        stats->ms_device = std::max(stats->ms_device, q.ms_device);
+        stats->ms_pretok = std::max(stats->ms_pretok, q.ms_pretok);
+        stats->ms_segment = std::max(stats->ms_segment, q.ms_segment);
+        stats->ms_bpe_short = std::max(stats->ms_bpe_short, q.ms_bpe_short);
+        stats->ms_bpe_lo = std::max(stats->ms_bpe_lo, q.ms_bpe_lo);
+        stats->ms_bpe_hi = std::max(stats->ms_bpe_hi, q.ms_bpe_hi);
+        stats->ms_bpe_long = std::max(stats->ms_bpe_long, q.ms_bpe_long);
+        stats->ms_emit = std::max(stats->ms_emit, q.ms_emit);
+        stats->ms_h2d = std::max(stats->ms_h2d, q.ms_h2d);
+        stats->ms_d2h = std::max(stats->ms_d2h, q.ms_d2h);
+      }
+      stats->bytes_in = B;
+      stats->docs = n_docs;
+      stats->tokens = total;
       stats->ms_total = now_ms() - t0;
     }
   });
