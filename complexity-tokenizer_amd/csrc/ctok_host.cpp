@@ -210,7 +210,7 @@ struct DeviceState {
   DevBuf<uint64_t> comp_key;
   Tables t{};
   // workspace
-  DevBuf<uint32_t> docbits, pbits, tile_np, tile_tok, tcls, list0, list1, list2, tcnt, scratch, counters, lw;
+  DevBuf<uint32_t> docbits, pbits, tile_np, tile_tok, tcls, list0, list1, list2, list3, tcnt, scratch, counters, lw;
   DevBuf<uint16_t> wpref;
   DevBuf<uint32_t> long_cnt;
   DevBuf<uint64_t> long_list, mid_list, scan_tmp;
@@ -866,8 +866,8 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   for (;;) {
   if (timing) HIPTRY(hipEventRecord(ds->ev[0], s));
 
-  ds->counters.ensure(16);
-  HIPTRY(hipMemsetAsync(ds->counters.p, 0, 16 * 4, s));
+  ds->counters.ensure(kNumCounters);
+  HIPTRY(hipMemsetAsync(ds->counters.p, 0, kNumCounters * 4, s));
   const uint8_t* text = d_text;
   const uint64_t* off = d_off;
   uint64_t B = n_bytes;
@@ -921,11 +921,12 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   ds->wpref.ensure(nt * 64 + 8);
   ds->tile_np.ensure(nt + 8);
   ds->tile_tok.ensure(nt + 8);
-  ds->tcls.ensure(3 * nt + 8);
+  ds->tcls.ensure(kNumClasses * nt + 8);
   ds->list0.ensure(nt * kCap0 + 8);
   if (tb.n_at == 0) {
     ds->list1.ensure(nt * kCap1 + 8);
     ds->list2.ensure(nt * kCap2 + 8);
+    ds->list3.ensure(nt * kCap3 + 8);
   }
   ds->tcnt.ensure(nt * kTileSlots + 8);
   ds->scratch.ensure(nt * kTile + 8);  // whole tiles: k_emit gathers unconditionally
@@ -943,6 +944,7 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   w.list0 = ds->list0.p;
   w.list1 = ds->list1.p;
   w.list2 = ds->list2.p;
+  w.list3 = ds->list3.p;
   w.long_cnt = ds->long_cnt.p;
   w.tcnt = ds->tcnt.p;
   w.scratch = ds->scratch.p;
@@ -968,21 +970,21 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   STEP("bpe_short", launch_bpe_class(w, tb, 0, s));
   if (timing) HIPTRY(hipEventRecord(ds->ev[2], s));
   if (timing) HIPTRY(hipEventRecord(ds->ev[8], s));
-  STEP("bpe_c2", launch_bpe_class(w, tb, 2, s));
+  STEP("bpe_mid", launch_bpe_class(w, tb, 2, s));
   if (timing) HIPTRY(hipEventRecord(ds->ev[9], s));
   HIPTRY(hipStreamWaitEvent(s, ds->ev_join, 0));
   if (timing) HIPTRY(hipEventRecord(ds->ev[5], s));
-  STEP("bpe_mid", launch_bpe_class(w, tb, 3, s));
+  STEP("bpe_dropped", launch_bpe_class(w, tb, 3, s));
   if (timing) HIPTRY(hipEventRecord(ds->ev[3], s));
   STEP("emit", launch_emit(w, d_ids, ids_cap, d_tok_off, s));
   if (timing) HIPTRY(hipEventRecord(ds->ev[6], s));
   if (st && w.n_tiles) STEP("count", launch_count_pieces(w, s));
   HIPTRY(hipMemcpyAsync(ds->host, d_tok_off + n_docs, 8, hipMemcpyDeviceToHost, s));
-  HIPTRY(hipMemcpyAsync(ds->host + 1, ds->counters.p, 64, hipMemcpyDeviceToHost, s));
+  HIPTRY(hipMemcpyAsync(ds->host + 1, ds->counters.p, kNumCounters * 4, hipMemcpyDeviceToHost, s));
   spin_sync(ds, s);
   const uint64_t ntok = ((volatile uint64_t*)ds->host)[0];
-  uint32_t cnt[16];
-  for (int i = 0; i < 16; i++) cnt[i] = ((volatile uint32_t*)(ds->host + 1))[i];
+  uint32_t cnt[kNumCounters];
+  for (int i = 0; i < kNumCounters; i++) cnt[i] = ((volatile uint32_t*)(ds->host + 1))[i];
   if (speculate && cnt[12]) {  // a code point NFC may change: check, normalise, run again
     speculate = false;
     continue;
@@ -999,9 +1001,9 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
     st->long_pieces = cnt[0];
     st->tokens = ntok;
     st->nfc_docs = nfc_docs;
-    for (int c = 0; c < 3; c++) {
-      st->class_bytes[c] = cnt[6 + 2 * c];
-      st->class_ids[c] = cnt[7 + 2 * c];
+    for (int c = 0; c < kNumClasses; c++) {
+      st->class_bytes[c] = cnt[ctr_stat(c)];
+      st->class_ids[c] = cnt[ctr_stat(c) + 1];
     }
     if (timing) {
       auto el = [&](int i, int j) {
@@ -1013,6 +1015,7 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
       st->ms_segment = el(7, 1);
       st->ms_bpe_lo = el(1, 2);
       st->ms_bpe_hi = el(8, 9);
+      st->ms_bpe_med = 0;  // classes 2 and 3 share k_bpe_mid (ms_bpe_hi)
       st->ms_bpe_short = el(1, 9);
       st->ms_bpe_long = el(9, 5);
       st->ms_emit = el(3, 6);
@@ -1201,6 +1204,7 @@ RangeOut encode_host_range(ctok* t, DeviceState* ds, const uint8_t* text, const 
   const size_t C = cut.size() - 1;
   std::vector<uint64_t> ntok(C, 0), base(C + 1, 0);
   double ms_h2d = 0, ms_d2h = 0, ms_dev = 0, ms_pre = 0, ms_bs = 0, ms_bl = 0, ms_em = 0, ms_seg = 0, ms_lo = 0, ms_hi = 0;
+  double ms_med = 0;
 
   auto stage = [&](size_t c) {
     const int k = (int)(c & 1);
@@ -1275,12 +1279,13 @@ RangeOut encode_host_range(ctok* t, DeviceState* ds, const uint8_t* text, const 
       st->long_pieces += cs.long_pieces;
       st->nfc_docs += cs.nfc_docs;
       st->bytes_norm += cs.bytes_norm;
-      for (int q = 0; q < 3; q++) {
+      for (int q = 0; q < kNumClasses; q++) {
         st->class_bytes[q] += cs.class_bytes[q];
         st->class_ids[q] += cs.class_ids[q];
       }
       ms_dev += cs.ms_device, ms_pre += cs.ms_pretok, ms_bs += cs.ms_bpe_short, ms_bl += cs.ms_bpe_long;
       ms_em += cs.ms_emit, ms_seg += cs.ms_segment, ms_lo += cs.ms_bpe_lo, ms_hi += cs.ms_bpe_hi;
+      ms_med += cs.ms_bpe_med;
     }
     if (th_drain.joinable()) th_drain.join();  // pin_ids[k ^ 1] is free again
     if (ex_drain) std::rethrow_exception(ex_drain);
@@ -1308,7 +1313,7 @@ RangeOut encode_host_range(ctok* t, DeviceState* ds, const uint8_t* text, const 
     ms_d2h = v;
     st->ms_h2d += ms_h2d, st->ms_d2h += ms_d2h, st->ms_device += ms_dev, st->ms_pretok += ms_pre;
     st->ms_bpe_short += ms_bs, st->ms_bpe_long += ms_bl, st->ms_emit += ms_em, st->ms_segment += ms_seg;
-    st->ms_bpe_lo += ms_lo, st->ms_bpe_hi += ms_hi;
+    st->ms_bpe_lo += ms_lo, st->ms_bpe_hi += ms_hi, st->ms_bpe_med += ms_med;
   }
   return r;
 }
@@ -1611,7 +1616,8 @@ int ctok_encode_batch(const ctok* tc, const uint8_t* utf8_in, const uint64_t* do
         const ctok_stats& q = sst[g];
         stats->pieces += q.pieces, stats->long_pieces += q.long_pieces, stats->nfc_docs += q.nfc_docs;
         stats->bytes_norm += q.bytes_norm;
-        for (int c = 0; c < 3; c++) stats->class_bytes[c] += q.class_bytes[c], stats->class_ids[c] += q.class_ids[c];
+        for (int c = 0; c < kNumClasses; c++)
+          stats->class_bytes[c] += q.class_bytes[c], stats->class_ids[c] += q.class_ids[c];
         // device times: the slowest shard
         stats->ms_device = std::max(stats->ms_device, q.ms_device);
         stats->ms_pretok = std::max(stats->ms_pretok, q.ms_pretok);
@@ -1619,6 +1625,7 @@ int ctok_encode_batch(const ctok* tc, const uint8_t* utf8_in, const uint64_t* do
         stats->ms_bpe_short = std::max(stats->ms_bpe_short, q.ms_bpe_short);
         stats->ms_bpe_lo = std::max(stats->ms_bpe_lo, q.ms_bpe_lo);
         stats->ms_bpe_hi = std::max(stats->ms_bpe_hi, q.ms_bpe_hi);
+        stats->ms_bpe_med = std::max(stats->ms_bpe_med, q.ms_bpe_med);
         stats->ms_bpe_long = std::max(stats->ms_bpe_long, q.ms_bpe_long);
         stats->ms_emit = std::max(stats->ms_emit, q.ms_emit);
         stats->ms_h2d = std::max(stats->ms_h2d, q.ms_h2d);

@@ -26,10 +26,17 @@ constexpr int kTile = kTileWords * 64;  // 3968 bytes per pre-tokenizer tile (pi
 constexpr int kTileSlots = 4096;        // per-tile stride of the piece-indexed arrays (pieces <= kTile)
 constexpr int kSegWaves = 4;            // tiles (wavefronts) per k_segment workgroup
 constexpr int kSegUnroll = 4;           // pieces per lane per routing round in k_segment
-constexpr int kShortMax = 32;      // pieces up to this many bytes are merged thread-per-piece
-// Per-tile piece lists by length class: <= 8 B (whole-piece probe missed), 9..16 B, 17..32 B.
-// Capacities are the most pieces of that class that can start in one tile.
-constexpr uint32_t kCap0 = kTile, kCap1 = (kTile + 8) / 9, kCap2 = (kTile + 16) / 17;
+constexpr int kShortMax = 32;      // pieces up to this many bytes: classes 0..2 (and the generic pass)
+constexpr int kMedMax = 64;        // class 3: 33..64 B, still thread-per-piece (64 register slots)
+// Per-tile piece lists by length class: <= 8 B (whole-piece probe missed), 9..16 B, 17..32 B,
+// 33..64 B.  Capacities are the most pieces of that class that can start in one tile.
+constexpr uint32_t kCap0 = kTile, kCap1 = (kTile + 8) / 9, kCap2 = (kTile + 16) / 17, kCap3 = (kTile + 32) / 33;
+constexpr int kNumClasses = 4;
+constexpr int kNumCounters = 32;
+// counters[] slots of class pass c: bytes merged / ids produced (statistics), next chunk
+__host__ __device__ constexpr int ctr_stat(int c) { return c < 3 ? 6 + 2 * c : 16; }
+__host__ __device__ constexpr int ctr_chunk(int c) { return c < 3 ? 13 + c : 18; }
+constexpr int kCtrAnyMid = 19;  // counters[19] != 0: some tile has a class-2 or class-3 piece
 // List entry (u32): start within the tile [0,12), piece index within the tile [12,24), length [24,30).
 __host__ __device__ inline uint32_t list_entry(uint32_t sl, uint32_t j, uint32_t n) { return sl | (j << 12) | (n << 24); }
 
@@ -136,19 +143,22 @@ struct Work {              // device pointers, sized by the host for one call
   uint16_t* wpref;         // [n_tiles * 64] pieces of the tile before each 64-byte word
   uint32_t* tile_np;       // [n_tiles] pieces starting in the tile
   uint32_t* tile_tok;      // [n_tiles + 1] tokens per tile, scanned in place to the tile's first id
-  uint32_t* tcls;          // [3][n_tiles] entries of each class list
+  uint32_t* tcls;          // [kNumClasses][n_tiles] entries of each class list
   uint32_t* list0;         // [n_tiles * kCap0] (also every <= 32 B piece when added tokens can match)
   uint32_t* list1;         // [n_tiles * kCap1]
   uint32_t* list2;         // [n_tiles * kCap2]
+  uint32_t* list3;         // [n_tiles * kCap3]
   uint32_t* tcnt;          // [n_tiles * kTileSlots] record of piece j (see kRecHit), then (k_emit) its
                            // first id within the tile
   uint32_t* long_cnt;      // ids of long piece li
   uint32_t* scratch;       // [n_bytes] ids of the piece starting at byte s at scratch[s ..]
-  uint64_t* long_list;     // pieces > kShortMax B (or of unknown length at a tile end): s | j << 32
+  uint64_t* long_list;     // pieces > kMedMax B (> kShortMax B in generic mode), or of unknown length
+                           // at a tile end: s | j << 32
   uint64_t* mid_list;      // pieces with dropped bytes for the generic kernel: s | j << 32 | n << 48
-  uint32_t* counters;      // [0] long count, [2] err, [3] nfc docs, [4] mid count, [5] pieces (stats),
-                           // [6 + 2c], [7 + 2c]: bytes merged / ids produced by class pass c (stats),
-                           // [12] NFC speculation failed, [13 + c] next chunk of class pass c
+  uint32_t* counters;      // [kNumCounters] [0] long count, [2] err, [3] nfc docs, [4] mid count,
+                           // [5] pieces (stats), [ctr_stat(c)], [ctr_stat(c) + 1]: bytes merged /
+                           // ids produced by class pass c (stats), [12] NFC speculation failed,
+                           // [ctr_chunk(c)] next chunk of class pass c, [kCtrAnyMid]
   uint32_t* lw;            // long-piece workspace: 4 * n_bytes u32
   uint32_t* scan_tmp;      // scan partials
   uint64_t scan_tmp_cap;
@@ -201,7 +211,8 @@ hipError_t launch_norm(const uint8_t* text, const uint64_t* doc_off, uint32_t n_
                        uint64_t* new_len_then_off, uint8_t* out_text, int phase, hipStream_t s);
 hipError_t launch_segment(const Work& w, const Tables& t, hipStream_t s);
 hipError_t launch_count_pieces(const Work& w, hipStream_t s);
-hipError_t launch_bpe_class(const Work& w, const Tables& t, int cls, hipStream_t s);  // 0,1,2 lists; 3 dropped-byte pieces
+// cls 0: classes 0 and 1; 2: classes 2 and 3; 3: dropped-byte pieces (mid_list)
+hipError_t launch_bpe_class(const Work& w, const Tables& t, int cls, hipStream_t s);
 hipError_t launch_bpe_long(const Work& w, const Tables& t, hipStream_t s);
 hipError_t launch_emit(const Work& w, uint32_t* ids, uint64_t ids_cap, uint64_t* tok_off, hipStream_t s);
 // exclusive scan of n u32 (n read from *n_dev when non-null, else n_max); out[n] = total

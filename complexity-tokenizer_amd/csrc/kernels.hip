@@ -396,7 +396,7 @@ __global__ __launch_bounds__(64 * kSegWaves) void k_segment(Work w, Tables t) {
   const bool generic = t.n_at != 0;  // added tokens can match inside pieces: no whole-piece shortcut
   uint32_t* tcnt = w.tcnt + (size_t)tile * kTileSlots;
   uint32_t hits = 0;
-  uint32_t n0 = 0, n1 = 0, n2 = 0;  // class-list lengths (wave-uniform)
+  uint32_t n0 = 0, n1 = 0, n2 = 0, n3 = 0;  // class-list lengths (wave-uniform)
   constexpr int U = kSegUnroll;
   constexpr uint32_t W = 64 * U;  // pieces per round
   for (uint32_t j0 = 0; j0 < np; j0 += W) {
@@ -419,15 +419,15 @@ __global__ __launch_bounds__(64 * kSegWaves) void k_segment(Work w, Tables t) {
       const uint32_t j = j0 + 64 * u + lane;
       sl[u] = 0;
       n[u] = 0;
-      cls[u] = 4;  // 0..2 class lists, 3 long, 4 done (or inactive), 5 probe
+      cls[u] = 4;  // 0..2 class lists, 3 long, 4 done (or inactive), 5 probe, 6 class list 3
       if (j < np) {
         sl[u] = s_pos[64 * u + lane];
         const uint32_t el = s_pos[64 * u + lane + 1];
-        if (el == 0xFFFFu || el - sl[u] > kShortMax) {
+        if (el == 0xFFFFu || el - sl[u] > (generic ? (uint32_t)kShortMax : (uint32_t)kMedMax)) {
           cls[u] = 3;
         } else {
           n[u] = el - sl[u];
-          cls[u] = generic ? 0 : n[u] > 16 ? 2 : n[u] > 8 ? 1 : 5;
+          cls[u] = generic ? 0 : n[u] > 32 ? 6 : n[u] > 16 ? 2 : n[u] > 8 ? 1 : 5;
         }
       }
       // whole-piece probe key: the piece's raw bytes (from LDS), zero-padded to 8
@@ -474,13 +474,16 @@ __global__ __launch_bounds__(64 * kSegWaves) void k_segment(Work w, Tables t) {
       const uint32_t e = list_entry(sl[u], j, n[u]);
       {  // the wave owns its tile's lists: running counts in scalar registers, no atomics
         const uint64_t m0 = __ballot(cls[u] == 0), m1 = __ballot(cls[u] == 1), m2 = __ballot(cls[u] == 2);
+        const uint64_t m3 = __ballot(cls[u] == 6);
         const uint64_t below = lanemask_lt();
         if (cls[u] == 0) w.list0[(size_t)tile * kCap0 + n0 + __popcll(m0 & below)] = e;
         if (cls[u] == 1) w.list1[(size_t)tile * kCap1 + n1 + __popcll(m1 & below)] = e;
         if (cls[u] == 2) w.list2[(size_t)tile * kCap2 + n2 + __popcll(m2 & below)] = e;
+        if (cls[u] == 6) w.list3[(size_t)tile * kCap3 + n3 + __popcll(m3 & below)] = e;
         n0 += __popcll(m0);
         n1 += __popcll(m1);
         n2 += __popcll(m2);
+        n3 += __popcll(m3);
       }
       const uint64_t lm = __ballot(cls[u] == 3);
       if (lm) {  // rare: one global atomic per wave
@@ -504,7 +507,9 @@ __global__ __launch_bounds__(64 * kSegWaves) void k_segment(Work w, Tables t) {
     w.tile_tok[tile] = hits;  // initial token count (the merge passes add theirs atomically)
     w.tile_np[tile] = np;
   }
-  if (lane < 3) w.tcls[(size_t)lane * w.n_tiles + tile] = lane == 0 ? n0 : lane == 1 ? n1 : n2;
+  if (lane < kNumClasses)
+    w.tcls[(size_t)lane * w.n_tiles + tile] = lane == 0 ? n0 : lane == 1 ? n1 : lane == 2 ? n2 : n3;
+  if (lane == 0 && (n2 | n3)) w.counters[kCtrAnyMid] = 1;  // plain store: every writer stores 1
 }
 
 hipError_t launch_segment(const Work& w, const Tables& t, hipStream_t s) {
@@ -561,10 +566,12 @@ struct AddedMatch {  // first occurrence of added token k in bytes[0, n) honouri
   }
 };
 
-#define TOK(i) s_tok[(i) * 256 + tid]
-#define RK(i) s_rk[(i) * 256 + tid]
+#define TOK(i) s_tok[(i) * NT + tid]
+#define RK(i) s_rk[(i) * NT + tid]
 
-// BPE over bytes[0, n) (n <= kShortMax), appending ids to out; returns the id count
+// BPE over bytes[0, n) (n <= the slots per thread), appending ids to out; returns the id count.
+// s_tok / s_rk hold NT threads' slots interleaved.
+template <uint32_t NT>
 __device__ __forceinline__ uint32_t bpe_short(const Tables& t, const uint8_t* bytes, uint32_t n,
                                               const int32_t* s_b2id, uint32_t* s_tok, uint32_t* s_rk,
                                               uint32_t tid, uint32_t* out, uint32_t* err) {
@@ -640,14 +647,17 @@ constexpr int kTilesGeneric = 2;  // tiles per workgroup, generic pass over list
 // MID = false: every piece of list0 (launched instead of the register passes when the tokenizer
 // has added tokens that can match inside a piece); MID = true: the pieces the register passes
 // found to contain a byte whose char is not in the vocab (mid_list).
+// MID pieces can be up to kMedMax bytes (class 3 finds them too): 64 slots, 128 threads.
 template <bool MID>
-__global__ __launch_bounds__(256) void k_bpe_generic(Work w, Tables t) {
-  __shared__ uint32_t s_tok[kShortMax * 256];
-  __shared__ uint32_t s_rk[kShortMax * 256];
+__global__ __launch_bounds__(MID ? 128 : 256) void k_bpe_generic(Work w, Tables t) {
+  constexpr uint32_t NT = MID ? 128 : 256;
+  constexpr uint32_t SLOTS = MID ? kMedMax : kShortMax;
+  __shared__ uint32_t s_tok[SLOTS * NT];
+  __shared__ uint32_t s_rk[SLOTS * NT];
   __shared__ int32_t s_b2id[256];
   __shared__ uint32_t s_pre[kTilesGeneric + 1], s_tsum[kTilesGeneric];
   const uint32_t tid = threadIdx.x;
-  s_b2id[tid] = t.byte2id[tid];
+  for (uint32_t i = tid; i < 256; i += NT) s_b2id[i] = t.byte2id[i];
   uint32_t* err = &w.counters[2];
   uint32_t E, t0 = 0;
   if (MID) {
@@ -657,8 +667,8 @@ __global__ __launch_bounds__(256) void k_bpe_generic(Work w, Tables t) {
     t0 = blockIdx.x * kTilesGeneric;
     E = tile_share_init<kTilesGeneric>(w.tcls, w.n_tiles, t0, s_pre, s_tsum);
   }
-  const uint32_t stride = MID ? gridDim.x * 256 : 256;
-  for (uint32_t q = (MID ? blockIdx.x * 256 : 0) + tid; q < E; q += stride) {
+  const uint32_t stride = MID ? gridDim.x * NT : NT;
+  for (uint32_t q = (MID ? blockIdx.x * NT : 0) + tid; q < E; q += stride) {
     uint32_t s, j, n, tile, kt = 0;
     if (MID) {
       const uint64_t e = w.mid_list[q];
@@ -678,7 +688,7 @@ __global__ __launch_bounds__(256) void k_bpe_generic(Work w, Tables t) {
     uint32_t* out = w.scratch + s;
     uint32_t cnt = 0;
     if (t.n_at == 0) {
-      cnt = bpe_short(t, bytes, n, s_b2id, s_tok, s_rk, tid, out, err);
+      cnt = bpe_short<NT>(t, bytes, n, s_b2id, s_tok, s_rk, tid, out, err);
     } else {
       // added-token split of the word (src/huggingface/mod.rs:566-610), on raw bytes
       uint32_t pos = 0;
@@ -695,7 +705,7 @@ __global__ __launch_bounds__(256) void k_bpe_generic(Work w, Tables t) {
           const int64_t f = AddedMatch::find(t, k, bytes + pos, n - pos);
           if (f > 0 && (uint32_t)f < nxt) nxt = (uint32_t)f;
         }
-        cnt += bpe_short(t, bytes + pos, nxt, s_b2id, s_tok, s_rk, tid, out + cnt, err);
+        cnt += bpe_short<NT>(t, bytes + pos, nxt, s_b2id, s_tok, s_rk, tid, out + cnt, err);
         pos += nxt;
       }
     }
@@ -771,10 +781,11 @@ template <int N> struct LdsClass;
 template <> struct LdsClass<8> { static constexpr int cls = 0; static constexpr uint32_t cap = kCap0; };
 template <> struct LdsClass<16> { static constexpr int cls = 1; static constexpr uint32_t cap = kCap1; };
 template <> struct LdsClass<32> { static constexpr int cls = 2; static constexpr uint32_t cap = kCap2; };
+template <> struct LdsClass<64> { static constexpr int cls = 3; static constexpr uint32_t cap = kCap3; };
 
 template <int N>
 __device__ __forceinline__ const uint32_t* class_list(const Work& w) {
-  return N == 8 ? w.list0 : N == 16 ? w.list1 : w.list2;
+  return N == 8 ? w.list0 : N == 16 ? w.list1 : N == 32 ? w.list2 : w.list3;
 }
 
 // The merge loop on the first N register slots of tk / rk (compile-time indices only, so the
@@ -787,10 +798,10 @@ __device__ __forceinline__ bool merge_slots(const Tables& t, const PairLds& P, u
                                             uint32_t& m, uint32_t stop, uint32_t* err) {
   for (;;) {
     if (m <= stop) return true;
-    uint32_t key = ~0u;  // rank << 5 | position: one v_min per slot (ranks < 2^22)
+    uint32_t key = ~0u;  // rank << 6 | position: one v_min per slot (ranks < 2^22, N <= 64)
 #pragma unroll
-    for (int k = 0; k < N - 1; k++) key = min(key, (rk[k] << 5) | (uint32_t)k);
-    const uint32_t best = key >> 5, bi = key & 31u;
+    for (int k = 0; k < N - 1; k++) key = min(key, (rk[k] << 6) | (uint32_t)k);
+    const uint32_t best = key >> 6, bi = key & 63u;
     if (best == kNoRank) return false;
     const uint32_t nid = COMPACT ? best : t.rank_newid[best];
     uint32_t L = 0, R = 0;
@@ -836,12 +847,15 @@ struct PassLds {
 };
 
 // Merge pass over one length class (N = 8, 16, 32 slots), run by a persistent grid:
-// workgroups take chunks of 64 tiles from a counter (counters[13 + class]) and walk the chunk's
+// workgroups take chunks of 64 tiles from a counter (counters[ctr_chunk(class)]) and walk the chunk's
 // class lists as one concatenated list (see tile_share_init).  Thread per piece, tokens and pair
 // ranks in registers (fully unrolled, compile-time slots).
-template <int N, bool COMPACT, bool HOT, uint32_t NT, uint32_t SORTCAP>
+// `load` fills the workgroup's LDS tables (image, byte -> id); it runs at the first chunk with
+// work, so a workgroup that finds only empty lists never reads the 32..96 KiB image (`loaded`
+// is shared by the passes of one kernel).
+template <int N, bool COMPACT, bool HOT, uint32_t NT, uint32_t SORTCAP, typename Load>
 __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const PairLds& P, const int32_t* s_b2id,
-                                           PassLds<SORTCAP>& S) {
+                                           PassLds<SORTCAP>& S, bool& loaded, Load&& load) {
   using LC = LdsClass<N>;
   constexpr int K = 64;
   const uint32_t tid = threadIdx.x;
@@ -852,18 +866,23 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
   if (tid < 2) S.stat[tid] = 0;
   // length buckets (4 per class): a wavefront's pieces then have similar lengths, hence
   // similar merge counts, and fewer of its lanes idle while the longest piece finishes
-  constexpr uint32_t blo = N == 8 ? 1 : N / 2 + 1, bw = N == 32 ? 4 : 2;
+  constexpr uint32_t blo = N == 8 ? 1 : N / 2 + 1, bw = N == 64 ? 8 : N == 32 ? 4 : 2;
   auto bucket = [&](uint32_t n) { return min(3u, (n - blo) / bw); };
   // chunks of K tiles dealt dynamically (one atomic per chunk, taken by thread 0 and broadcast
   // through LDS): workgroups that start late, or whose CU is shared, take fewer chunks
   __syncthreads();
   for (;;) {
-    if (tid == 0) S.chunk = atomicAdd(&w.counters[13 + LC::cls], 1u);
+    if (tid == 0) S.chunk = atomicAdd(&w.counters[ctr_chunk(LC::cls)], 1u);
     __syncthreads();
     const uint32_t c0 = S.chunk * K;
     if (c0 >= w.n_tiles) break;
     const uint32_t tb1 = min(w.n_tiles, c0 + K);
     const uint32_t E = tile_share_init<K>(counts, tb1, c0, S.pre, S.tsum);
+    if (E && !loaded) {  // E is workgroup-uniform (read from LDS after a barrier)
+      load();
+      loaded = true;
+      __syncthreads();
+    }
     const bool sorted = N > 8 && E <= SORTCAP;  // <= 8 B pieces: few merges, sorting does not pay
     if (sorted) {
       if (tid < 4) { S.bcnt[tid] = 0; S.bfill[tid] = 0; }
@@ -941,7 +960,10 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
       uint32_t m = n;
       // tiers: N slots while the piece has more than N/2 tokens, then N/2, ... down to 8 slots
       bool more = true;
-      if constexpr (N >= 32) more = merge_slots<32, COMPACT, HOT>(t, P, tk, rk, m, 16, err);
+      if constexpr (N >= 64) more = merge_slots<64, COMPACT, HOT>(t, P, tk, rk, m, 32, err);
+      if constexpr (N >= 32) {
+        if (more) more = merge_slots<32, COMPACT, HOT>(t, P, tk, rk, m, 16, err);
+      }
       if constexpr (N >= 16) {
         if (more) more = merge_slots<16, COMPACT, HOT>(t, P, tk, rk, m, 8, err);
       }
@@ -970,8 +992,8 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
   }
   __syncthreads();
   if (tid == 0) {
-    atomicAdd(&w.counters[6 + 2 * LC::cls], S.stat[0]);
-    atomicAdd(&w.counters[7 + 2 * LC::cls], S.stat[1]);
+    atomicAdd(&w.counters[ctr_stat(LC::cls)], S.stat[0]);
+    atomicAdd(&w.counters[ctr_stat(LC::cls) + 1], S.stat[1]);
   }
   __syncthreads();
 }
@@ -985,26 +1007,50 @@ __global__ __launch_bounds__(1024) void k_bpe_short(Work w, Tables t) {
   __shared__ int32_t s_b2id[256];
   __shared__ PassLds<kSortCap> S;
   const uint32_t tid = threadIdx.x;
-  for (uint32_t i = tid; i < kLdsImageBytes / 16; i += 1024) s_img[i] = t.lds_image[i];
-  for (uint32_t i = tid; i < 256; i += 1024) s_b2id[i] = t.byte2id[i];
+  auto load = [&] {
+    for (uint32_t i = tid; i < kLdsImageBytes / 16; i += 1024) s_img[i] = t.lds_image[i];
+    for (uint32_t i = tid; i < 256; i += 1024) s_b2id[i] = t.byte2id[i];
+  };
+  bool loaded = false;
   const PairLds P{(const lds_u64*)s_img, (const lds_u32*)(s_img + kHotBuckets)};
-  class_pass<8, COMPACT, true, 1024, kSortCap>(w, t, P, s_b2id, S);
-  class_pass<16, COMPACT, true, 1024, kSortCap>(w, t, P, s_b2id, S);
+  class_pass<8, COMPACT, true, 1024, kSortCap>(w, t, P, s_b2id, S, loaded, load);
+  class_pass<16, COMPACT, true, 1024, kSortCap>(w, t, P, s_b2id, S, loaded, load);
 }
 
-// Pieces of 17..32 bytes (class 2, ~0.5% of pieces): 512-thread workgroups (32 slots need the
-// registers) with the Bloom filter only in LDS (32 KiB).
+// Pieces of 17..64 bytes (class 2, then class 3: e.g. runs of CJK letters, 3 bytes each) in one
+// kernel: 512-thread workgroups (two waves per SIMD at <= 256 VGPRs: 32 and 64 register slots
+// per thread) with the whole LDS image.  A workgroup moves on to class 3 when class 2 has no
+// chunk left, so the latency tail of the few long register pieces overlaps class-2 work.
 template <bool COMPACT>
-__global__ __launch_bounds__(512) void k_bpe_c2(Work w, Tables t) {
+__global__ __launch_bounds__(512) void k_bpe_mid(Work w, Tables t) {
   extern __shared__ __attribute__((aligned(16))) uint4 s_img[];
   __shared__ int32_t s_b2id[256];
-  __shared__ PassLds<2048> S;
+  __shared__ PassLds<kSortCap> S;
+  // (the image is loaded up front: a lazy load pushes the 64-slot pass into scratch; the kernel
+  // returns at once when k_segment found no piece of either class)
+  if (w.counters[kCtrAnyMid] == 0) return;
   const uint32_t tid = threadIdx.x;
-  const uint4* bloom = t.lds_image + kHotBuckets;  // the image's Bloom half
-  for (uint32_t i = tid; i < kBloomWords / 4; i += 512) s_img[i] = bloom[i];
+  for (uint32_t i = tid; i < kLdsImageBytes / 16; i += 512) s_img[i] = t.lds_image[i];
   for (uint32_t i = tid; i < 256; i += 512) s_b2id[i] = t.byte2id[i];
-  const PairLds P{nullptr, (const lds_u32*)s_img};
-  class_pass<32, COMPACT, false, 512, 2048>(w, t, P, s_b2id, S);
+  bool loaded = true;
+  const PairLds P{(const lds_u64*)s_img, (const lds_u32*)(s_img + kHotBuckets)};
+  // class 3 first: its pieces have the longest merge chains, so their latency tail overlaps the
+  // class-2 work of the other workgroups instead of ending the kernel
+  class_pass<64, COMPACT, true, 512, kSortCap>(w, t, P, s_b2id, S, loaded, [] {});
+  class_pass<32, COMPACT, true, 512, kSortCap>(w, t, P, s_b2id, S, loaded, [] {});
+}
+
+template <bool C>
+static hipError_t launch_mid(const Work& w, const Tables& t, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    HIPCHK(hipFuncSetAttribute((const void*)k_bpe_mid<C>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)kLdsImageBytes));
+    attr = true;
+  }
+  if (!w.n_tiles) return hipSuccess;
+  k_bpe_mid<C><<<min((w.n_tiles + 63) / 64, w.n_cus), 512, kLdsImageBytes, s>>>(w, t);
+  return hipGetLastError();
 }
 
 template <bool C>
@@ -1020,13 +1066,6 @@ static hipError_t launch_short(const Work& w, const Tables& t, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <bool C>
-static hipError_t launch_c2(const Work& w, const Tables& t, hipStream_t s) {
-  if (!w.n_tiles) return hipSuccess;
-  k_bpe_c2<C><<<min((w.n_tiles + 63) / 64, w.n_cus), 512, kBloomWords * 4, s>>>(w, t);
-  return hipGetLastError();
-}
-
 hipError_t launch_bpe_class(const Work& w, const Tables& t, int cls, hipStream_t s) {
   if (t.n_at != 0) {  // every <= 32 B piece is in list0
     if (cls == 0 && w.n_tiles) k_bpe_generic<false><<<(w.n_tiles + kTilesGeneric - 1) / kTilesGeneric, 256, 0, s>>>(w, t);
@@ -1034,9 +1073,9 @@ hipError_t launch_bpe_class(const Work& w, const Tables& t, int cls, hipStream_t
   }
   switch (cls) {
     case 0: return t.compact ? launch_short<true>(w, t, s) : launch_short<false>(w, t, s);  // classes 0 and 1
-    case 2: return t.compact ? launch_c2<true>(w, t, s) : launch_c2<false>(w, t, s);
+    case 2: return t.compact ? launch_mid<true>(w, t, s) : launch_mid<false>(w, t, s);  // classes 2 and 3
     case 3:  // pieces with dropped bytes, found by the merge passes
-      k_bpe_generic<true><<<64, 256, 0, s>>>(w, t);
+      k_bpe_generic<true><<<64, 128, 0, s>>>(w, t);
       return hipGetLastError();
     default:
       return hipSuccess;
@@ -1184,7 +1223,8 @@ __device__ uint32_t bpe_wave(const Tables& t, const uint8_t* bytes, uint32_t n, 
       }
     }
     L.sync();
-    if (uni(__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) break;
+    // (no per-round read of the panic flag: a panicking pair ranks as kNoRank, so the loop still
+    // ends, and the host discards the batch -- a global load per round would double its latency)
   }
   // emit surviving tokens in order
   uint32_t c = 0;
@@ -1199,6 +1239,7 @@ __device__ uint32_t bpe_wave(const Tables& t, const uint8_t* bytes, uint32_t n, 
 }
 
 constexpr uint32_t kLdsPos = 2048;  // positions per wave in LDS (4 u32 arrays: 32 KiB per wave)
+constexpr uint32_t kWaveMax = 64 * 64;  // longest piece of the dense wave tiers (k_bpe_wave)
 
 template <bool G>
 __device__ uint32_t long_piece(const Tables& t, const uint8_t* bytes, uint32_t n, const LongState<G>& L,
@@ -1269,7 +1310,10 @@ __global__ __launch_bounds__(256) void k_bpe_long(Work w, Tables t) {
     const uint32_t s = uni((uint32_t)e);
     const uint32_t j = uni((uint32_t)(e >> 32));
     const uint32_t n = uni(piece_end(w, s) - s);
-    if (GMEM != (n > kLdsPos)) continue;
+    // tiers: LDS up to kLdsPos positions, global memory beyond (only beyond the dense wave tiers
+    // when those run, i.e. without added tokens)
+    const uint32_t gmin = (t.n_at != 0 || t.dbg == 7) ? kLdsPos : kWaveMax;
+    if (GMEM != (n > gmin)) continue;
     const uint8_t* bytes = w.text + s;
     uint32_t* out = w.scratch + s;
     uint32_t cnt;
@@ -1290,11 +1334,426 @@ __global__ __launch_bounds__(256) void k_bpe_long(Work w, Tables t) {
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// BPE, pieces of kMedMax+1 .. 64K bytes without added tokens: one wavefront per piece, the
+// piece's tokens and pair ranks dense in the wave's LDS slice (position p in lane p % 64 of
+// step p / 64).  A round: r = wave minimum of the pair ranks; the merge sites are every
+// position whose pair has rank r (proper tables: occurrences never overlap unless the pair is
+// (x, x), where runs take every other site from the left, as the sequential loop does;
+// non-monotone tables: the leftmost site only); the sites' right tokens are dropped while the
+// survivors are compacted into the other buffer (ballot prefix counts), and only pairs that
+// touch a new token are looked up again (Bloom filter in LDS, global table on a Bloom hit).
+// The live token count shrinks every round, and so does the work per round.
+
+template <int K>
+struct WaveSlice {  // per-wave LDS slice: 64K positions (compacted in place every round)
+  static constexpr uint32_t C = 64 * K;
+  static constexpr uint32_t kBytes = 8 * C + 2 * (C + 64);
+  lds_u32* base;  // tok | rk | chg | sel
+  __device__ __forceinline__ lds_u32* tok() const { return base; }
+  __device__ __forceinline__ lds_u32* rk() const { return base + C; }
+  __device__ __forceinline__ __attribute__((address_space(3))) uint8_t* chg() const {
+    return (__attribute__((address_space(3))) uint8_t*)(base + 2 * C);
+  }
+  __device__ __forceinline__ __attribute__((address_space(3))) uint8_t* sel() const {
+    return (__attribute__((address_space(3))) uint8_t*)(base + 2 * C) + C + 64;
+  }
+};
+
+__device__ __forceinline__ void wave_sync_lds() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// value of pair (a, b) (never a byte pair): LDS hot table (HOT) and Bloom filter, the global
+// table when neither settles it
+template <bool HOT>
+__device__ __forceinline__ uint32_t rank_pair(const Tables& t, const PairLds& P, uint32_t a, uint32_t b,
+                                              uint32_t* err) {
+  const uint32_t h1 = mhash(a, b);
+  bool g;
+  const uint32_t v = rank_lds<HOT>(P, a, b, h1, mhash2(h1), g);
+  if (!g) return v;
+  const uint32_t h = h1 & t.merge_mask;
+  return resolve_rank(t, pair_key(a, b), h, t.merge_tab[h], err);
+}
+
+template <int K, bool HOT>
+__device__ uint32_t bpe_wave_dense(const Tables& t, const PairLds& P, const int32_t* s_b2id, const uint8_t* bytes,
+                                   uint32_t n, const WaveSlice<K>& S, uint32_t* out, uint32_t* err) {
+  const uint32_t lane = threadIdx.x & 63;
+  lds_u32* tok = S.tok();
+  lds_u32* rk = S.rk();
+  auto chg = S.chg();
+  auto sel = S.sel();
+  // initial ids (bytes whose char is not in the vocab are dropped: order-preserving compaction);
+  // the raw bytes go to chg for the initial pair ranks
+  uint32_t m = 0;
+  for (uint32_t i0 = 0; i0 < n; i0 += 64) {
+    const uint32_t i = i0 + lane;
+    const int32_t id = i < n ? s_b2id[bytes[i]] : -1;
+    const uint64_t bal = __ballot(id >= 0);
+    if (id >= 0) {
+      const uint32_t q = m + __popcll(bal & lanemask_lt());
+      tok[q] = (uint32_t)id;
+      chg[q] = bytes[i];
+    }
+    m = uni(m + __popcll(bal));
+  }
+  wave_sync_lds();
+  if (m == 0) return 0;
+  // initial pairs are byte pairs: the 256 x 256 byte-pair table (byte pairs are left out of the
+  // LDS image; every later pair holds a merged token)
+#pragma unroll 4
+  for (uint32_t p = lane; p < m; p += 64) {
+    uint32_t r = kNoRank;
+    if (p + 1 < m) {
+      r = t.pair0[((uint32_t)chg[p] << 8) | chg[p + 1]];
+      if (r != kNoRank && value_panics(t, r)) {
+        atomicOr(err, kErrPanic);
+        r = kNoRank;
+      }
+    }
+    rk[p] = r;
+  }
+  wave_sync_lds();
+  for (;;) {
+    uint32_t lmin = kNoRank;
+#pragma unroll 8
+    for (uint32_t p = lane; p < m; p += 64) lmin = min(lmin, (uint32_t)rk[p]);
+    const uint32_t r = uni(wave_min_u32(lmin));
+    if (r == kNoRank) break;
+    const uint32_t nid = uni(new_id_of(t, r));
+    // sites: positions whose pair has rank r; lm = the leftmost
+    uint32_t lpos = kNone;
+#pragma unroll 4
+    for (uint32_t p = lane; p < m; p += 64) {
+      const bool site = rk[p] == r;
+      sel[p] = site ? 1 : 0;
+      lpos = min(lpos, site ? p : kNone);
+    }
+    const uint32_t lm = uni(wave_min_u32(lpos));
+    const bool chain = uni(tok[lm] == tok[lm + 1] ? 1u : 0u) != 0;
+    wave_sync_lds();
+    if (!t.proper) {
+      for (uint32_t p = lane; p < m; p += 64) sel[p] = p == lm ? 1 : 0;
+      wave_sync_lds();
+    } else if (chain) {
+      // (x, x): in a run of consecutive sites the sequential loop merges the 1st, 3rd, ... one
+      // (the choice goes through chg, rewritten by the compaction below)
+      for (uint32_t p = lane; p < m; p += 64) {
+        uint32_t d = 0;
+        if (sel[p]) {
+          while (d < p && sel[p - 1 - d]) d++;
+        }
+        chg[p] = (sel[p] && (d & 1) == 0) ? 1 : 0;
+      }
+      wave_sync_lds();
+      for (uint32_t p = lane; p < m; p += 64) sel[p] = chg[p];
+      wave_sync_lds();
+    }
+    // in-place compaction: a site's right neighbour is dropped, the site takes nid.  Position p
+    // moves to q <= p; a step reads its 64 positions before it writes, and later steps read only
+    // positions past every q written so far.
+    uint32_t base = 0;
+    for (uint32_t p0 = 0; p0 < m; p0 += 64) {
+      const uint32_t p = p0 + lane;
+      const bool in = p < m;
+      const bool site = in && sel[p];
+      const bool dead = in && p > 0 && sel[p - 1];
+      const bool alive = in && !dead;
+      const uint32_t tv = in ? (uint32_t)tok[p] : 0u, rv = in ? (uint32_t)rk[p] : 0u;
+      const uint64_t bal = __ballot(alive);
+      if (alive) {
+        const uint32_t q = base + __popcll(bal & lanemask_lt());
+        tok[q] = site ? nid : tv;
+        rk[q] = rv;
+        chg[q] = site ? 1 : 0;
+      }
+      base = uni(base + __popcll(bal));
+    }
+    m = base;
+    if (lane == 0) chg[m] = 0;
+    wave_sync_lds();
+    // pairs touching a new token get their rank again
+    for (uint32_t p = lane; p < m; p += 64) {
+      if (chg[p] | chg[p + 1]) rk[p] = p + 1 < m ? rank_pair<HOT>(t, P, tok[p], tok[p + 1], err) : kNoRank;
+    }
+    wave_sync_lds();
+    // (no per-round read of the panic flag: a panicking pair ranks as kNoRank, so the loop still
+    // ends, and the host discards the batch -- a global load per round would double its latency)
+  }
+#pragma unroll 4
+  for (uint32_t p = lane; p < m; p += 64) out[p] = tok[p];
+  return m;
+}
+
+// Long pieces (hundreds to thousands of tokens): positions stay put and are linked into a list
+// (nxt / prv, u16); lane l owns the contiguous segment [l*S, (l+1)*S) and keeps the minimum pair
+// rank of its segment in a register.  A round costs a 64-lane minimum, then only the lanes
+// that hold a site (or whose segment changed) walk their S positions -- instead of every round
+// sweeping and compacting the whole piece.
+template <int K>
+struct SegSlice {  // per-wave LDS slice for up to 64K positions
+  static constexpr uint32_t C = 64 * K;
+  static constexpr uint32_t kBytes = 13 * C + 64;
+  lds_u32* base;  // tok[C] | rk[C] | nxt[C] u16 | prv[C] u16 | sel[C] u8 | dirty[64] u8
+  __device__ __forceinline__ lds_u32* tok() const { return base; }
+  __device__ __forceinline__ lds_u32* rk() const { return base + C; }
+  __device__ __forceinline__ __attribute__((address_space(3))) uint16_t* nxt() const {
+    return (__attribute__((address_space(3))) uint16_t*)(base + 2 * C);
+  }
+  __device__ __forceinline__ __attribute__((address_space(3))) uint16_t* prv() const { return nxt() + C; }
+  __device__ __forceinline__ __attribute__((address_space(3))) uint8_t* sel() const {
+    return (__attribute__((address_space(3))) uint8_t*)(prv() + C);
+  }
+  __device__ __forceinline__ __attribute__((address_space(3))) uint8_t* dirty() const { return sel() + C; }
+};
+
+constexpr uint32_t kNoPos = 0xFFFFu;
+
+template <int K, bool HOT>
+__device__ uint32_t bpe_wave_seg(const Tables& t, const PairLds& P, const int32_t* s_b2id, const uint8_t* bytes,
+                                 uint32_t n, const SegSlice<K>& S, uint32_t* out, uint32_t* err) {
+  static_assert(K % 4 == 0 && K <= 64, "segment width: a multiple of 4, at most 64");
+  const uint32_t lane = threadIdx.x & 63;
+  lds_u32* tok = S.tok();
+  lds_u32* rk = S.rk();
+  auto nxt = S.nxt();
+  auto prv = S.prv();
+  auto sel = S.sel();
+  auto dirty = S.dirty();
+  // initial ids (dropped bytes compacted away); raw bytes parked in sel for the byte-pair ranks
+  uint32_t m = 0;
+  for (uint32_t i0 = 0; i0 < n; i0 += 64) {
+    const uint32_t i = i0 + lane;
+    const int32_t id = i < n ? s_b2id[bytes[i]] : -1;
+    const uint64_t bal = __ballot(id >= 0);
+    if (id >= 0) {
+      const uint32_t q = m + __popcll(bal & lanemask_lt());
+      tok[q] = (uint32_t)id;
+      sel[q] = bytes[i];
+    }
+    m = uni(m + __popcll(bal));
+  }
+  wave_sync_lds();
+  if (m == 0) return 0;
+  // lane l owns positions [l*SW, l*SW + SW): SW is a multiple of 4, so a segment's ranks are
+  // read with SW/4 independent 16-byte LDS loads into v[] (one LDS latency per scan instead of
+  // one per position); positions >= m hold kNoRank
+  const uint32_t SW = (((m + 63) / 64) + 3) & ~3u;  // <= K
+  const uint32_t a0 = lane * SW;
+  for (uint32_t k = 0; k < SW; k++) {
+    const uint32_t p = a0 + k;
+    uint32_t r = kNoRank;
+    if (p + 1 < m) {
+      r = t.pair0[((uint32_t)sel[p] << 8) | sel[p + 1]];
+      if (r != kNoRank && value_panics(t, r)) {
+        atomicOr(err, kErrPanic);
+        r = kNoRank;
+      }
+    }
+    rk[p] = r;
+    if (p < m) {
+      nxt[p] = p + 1 < m ? (uint16_t)(p + 1) : (uint16_t)kNoPos;
+      prv[p] = p > 0 ? (uint16_t)(p - 1) : (uint16_t)kNoPos;
+    }
+  }
+  wave_sync_lds();
+  for (uint32_t k = 0; k < SW; k++) sel[a0 + k] = 0;
+  dirty[lane] = 1;  // first round: every lane loads its segment
+  uint32_t v[K];
+  uint32_t smin = kNoRank;
+  wave_sync_lds();
+  for (;;) {
+    if (dirty[lane]) {  // (re)load this segment's ranks and their minimum
+      const uint4* src = (const uint4*)(rk + a0);
+      smin = kNoRank;
+#pragma unroll
+      for (int q = 0; q < K / 4; q++) {
+        const uint4 x = (uint32_t)(4 * q) < SW ? src[q] : make_uint4(kNoRank, kNoRank, kNoRank, kNoRank);
+        v[4 * q] = x.x;
+        v[4 * q + 1] = x.y;
+        v[4 * q + 2] = x.z;
+        v[4 * q + 3] = x.w;
+      }
+#pragma unroll
+      for (int k = 0; k < K; k++) smin = min(smin, v[k]);
+      dirty[lane] = 0;
+    }
+    const uint32_t r = uni(wave_min_u32(smin));
+    if (r == kNoRank) break;
+    const uint32_t nid = uni(new_id_of(t, r));
+    // this segment's sites as a bit mask (bit k: position a0 + k); the leftmost site decides
+    // the mode
+    uint64_t sites = 0;
+    if (smin == r) {
+#pragma unroll
+      for (int k = 0; k < K; k++) sites |= (uint64_t)(v[k] == r) << k;
+    }
+    const uint32_t first = sites ? a0 + (uint32_t)__builtin_ctzll(sites) : kNone;
+    const uint32_t lm = uni(wave_min_u32(first));
+    const bool chain = uni(tok[lm] == tok[nxt[lm]] ? 1u : 0u) != 0;
+    if (!t.proper) {
+      sites = first == lm ? 1ull << (lm - a0) : 0ull;  // the leftmost site only
+    } else if (chain && sites) {
+      // (x, x) runs: the 1st, 3rd, ... site of a run (d = sites before p in its run)
+      uint64_t keep = 0, rest = sites;
+      uint32_t d = 0, last = kNone;
+      while (rest) {
+        const uint32_t k = (uint32_t)__builtin_ctzll(rest);
+        rest &= rest - 1;
+        const uint32_t p = a0 + k;
+        if (last != kNone && prv[p] == last) {
+          d++;
+        } else {  // run start, or a run entering from the previous segment: walk back
+          d = 0;
+          for (uint32_t q = prv[p]; q != kNoPos && rk[q] == r; q = prv[q]) d++;
+        }
+        last = p;
+        if ((d & 1) == 0) keep |= 1ull << k;
+      }
+      sites = keep;
+    }
+    const bool any = sites != 0;
+    for (uint64_t rest = sites; rest; rest &= rest - 1) sel[a0 + (uint32_t)__builtin_ctzll(rest)] = 1;
+    wave_sync_lds();
+    // phase A: every selected site merges with its right neighbour
+    for (uint64_t rest = sites; rest; rest &= rest - 1) {
+      const uint32_t p = a0 + (uint32_t)__builtin_ctzll(rest);
+      const uint32_t q = nxt[p];
+      const uint32_t nq = nxt[q];
+      tok[p] = nid;
+      tok[q] = kDead;
+      rk[q] = kNoRank;
+      nxt[p] = (uint16_t)nq;
+      if (nq != kNoPos) prv[nq] = (uint16_t)p;
+      dirty[q / SW] = 1;
+    }
+    wave_sync_lds();
+    // phase B: the new pairs' ranks (a left neighbour that is itself a site leaves the pair to
+    // that site's right-pair lookup)
+    for (uint64_t rest = sites; rest; rest &= rest - 1) {
+      const uint32_t p = a0 + (uint32_t)__builtin_ctzll(rest);
+      const uint32_t q = nxt[p];
+      rk[p] = q != kNoPos ? rank_pair<HOT>(t, P, nid, tok[q], err) : kNoRank;
+      const uint32_t pp = prv[p];
+      if (pp != kNoPos && !sel[pp]) {
+        rk[pp] = rank_pair<HOT>(t, P, tok[pp], nid, err);
+        dirty[pp / SW] = 1;
+      }
+    }
+    if (any) dirty[lane] = 1;
+    wave_sync_lds();
+    for (uint64_t rest = sites; rest; rest &= rest - 1) sel[a0 + (uint32_t)__builtin_ctzll(rest)] = 0;
+    // (no per-round read of the panic flag: a panicking pair ranks as kNoRank, so the loop still
+    // ends, and the host discards the batch -- a global load per round would double its latency)
+  }
+  // surviving tokens in position order
+  uint32_t c = 0;
+  for (uint32_t i0 = 0; i0 < m; i0 += 64) {
+    const uint32_t i = i0 + lane;
+    const uint32_t v = i < m ? (uint32_t)tok[i] : kDead;
+    const uint64_t bal = __ballot(v != kDead);
+    if (v != kDead) out[c + __popcll(bal & lanemask_lt())] = v;
+    c = uni(c + __popcll(bal));
+  }
+  return c;
+}
+
+// One wavefront per piece of (LO, 64K] bytes; NW waves per workgroup, pieces dealt to waves by a
+// static stride over the long list.  LDS: the merge-table image (HOT: hot table + Bloom filter,
+// 96 KiB; else the Bloom filter, 32 KiB), loaded when the workgroup meets its first piece, and
+// one slice per wave.
+template <int K, uint32_t LO, int NW, bool HOT, bool SEG>
+__global__ __launch_bounds__(64 * NW) void k_bpe_wave(Work w, Tables t) {
+  constexpr uint32_t kSlice = SEG ? SegSlice<K>::kBytes : WaveSlice<K>::kBytes;
+  extern __shared__ __attribute__((aligned(16))) uint4 s_dyn[];
+  __shared__ int32_t s_b2id[256];
+  __shared__ uint32_t s_any;
+  constexpr uint32_t kImg = HOT ? kLdsImageBytes / 16 : kBloomWords / 4;  // uint4 units
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  const uint32_t wid = uni(tid >> 6);
+  const uint32_t n_long = uni(w.counters[0]);
+  if (n_long == 0) return;
+  const uint32_t n_waves = gridDim.x * NW;
+  // does any wave of this workgroup have a piece of this tier?  (the image is loaded only then)
+  if (tid == 0) s_any = 0;
+  __syncthreads();
+  for (uint32_t li = blockIdx.x * NW + wid; li < n_long; li += n_waves) {
+    const uint32_t s = uni((uint32_t)w.long_list[li]);
+    const uint32_t n = uni(piece_end(w, s) - s);
+    if (n > LO && n <= 64u * K) {
+      if (lane == 0) s_any = 1;
+      break;
+    }
+  }
+  __syncthreads();
+  if (s_any == 0) return;
+  const uint4* img = HOT ? t.lds_image : t.lds_image + kHotBuckets;
+  for (uint32_t i = tid; i < kImg; i += 64 * NW) s_dyn[i] = img[i];
+  for (uint32_t i = tid; i < 256; i += 64 * NW) s_b2id[i] = t.byte2id[i];
+  __syncthreads();
+  const PairLds P = HOT ? PairLds{(const lds_u64*)s_dyn, (const lds_u32*)(s_dyn + kHotBuckets)}
+                        : PairLds{nullptr, (const lds_u32*)s_dyn};
+  lds_u32* slice = (lds_u32*)((__attribute__((address_space(3))) uint8_t*)(s_dyn + kImg) + (size_t)wid * kSlice);
+  uint32_t* err = &w.counters[2];
+  for (uint32_t li = uni(blockIdx.x * NW + wid); li < n_long; li += n_waves) {
+    const uint64_t e = w.long_list[li];
+    const uint32_t s = uni((uint32_t)e);
+    const uint32_t j = uni((uint32_t)(e >> 32));
+    const uint32_t n = uni(piece_end(w, s) - s);
+    if (n <= LO || n > 64u * K) continue;
+    uint32_t cnt;
+    if constexpr (SEG) cnt = bpe_wave_seg<K, HOT>(t, P, s_b2id, w.text + s, n, SegSlice<K>{slice}, w.scratch + s, err);
+    else cnt = bpe_wave_dense<K, HOT>(t, P, s_b2id, w.text + s, n, WaveSlice<K>{slice}, w.scratch + s, err);
+    if (lane == 0) {
+      const uint32_t tile = s / kTile;
+      w.long_cnt[li] = cnt;
+      w.tcnt[(size_t)tile * kTileSlots + j] = kRecLong | li;
+      atomicAdd(&w.tile_tok[tile], cnt);
+    }
+  }
+}
+
+template <int K, uint32_t LO, int NW, bool HOT, bool SEG>
+static hipError_t launch_wave(const Work& w, const Tables& t, uint32_t grid, hipStream_t s) {
+  static bool attr = false;
+  const size_t slice = SEG ? SegSlice<K>::kBytes : WaveSlice<K>::kBytes;
+  const size_t lds = (HOT ? kLdsImageBytes : kBloomWords * 4) + (size_t)NW * slice;
+  if (!attr) {
+    HIPCHK(hipFuncSetAttribute((const void*)k_bpe_wave<K, LO, NW, HOT, SEG>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    attr = true;
+  }
+  k_bpe_wave<K, LO, NW, HOT, SEG><<<grid, 64 * NW, lds, s>>>(w, t);
+  return hipGetLastError();
+}
+
 hipError_t launch_bpe_long(const Work& w, const Tables& t, hipStream_t s) {
-  // one wavefront per workgroup (32 KiB of LDS each): a long-piece workgroup fits on a CU next
-  // to a merge-pass workgroup (96 KiB), so this pass overlaps them instead of taking CUs away
-  const size_t lds = 4 * kLdsPos * sizeof(uint32_t);
-  k_bpe_long<false><<<512, 64, lds, s>>>(w, t);
+  if (t.n_at != 0 || t.dbg == 7) {
+    // added tokens can match inside pieces: the linked-list kernel with the added-token split.
+    // One wavefront per workgroup (32 KiB of LDS each): a long-piece workgroup fits on a CU next
+    // to a merge-pass workgroup (96 KiB), so this pass overlaps them instead of taking CUs away
+    const size_t lds = 4 * kLdsPos * sizeof(uint32_t);
+    k_bpe_long<false><<<512, 64, lds, s>>>(w, t);
+    k_bpe_long<true><<<128, 256, 0, s>>>(w, t);
+    return hipGetLastError();
+  }
+  // dense wave tiers: <= 256 B (4 waves per workgroup, Bloom filter only, 43 KiB of LDS: fits
+  // next to a merge-pass workgroup), 257..2048 B and 2049..4096 B (one wave per workgroup with the
+  // whole image, 117 / 137 KiB); longer pieces: GMEM linked list.
+  // The long list holds pieces > kMedMax B and pieces whose end lies past the tile's look-ahead
+  // (>= 63 B: they can be shorter than kMedMax), so the first tier starts at 1 B.
+  HIPCHK((launch_wave<4, 0, 4, false, false>(w, t, 2 * w.n_cus, s)));
+  if (t.dbg == 8) {  // A/B: the compacting kernel for the long tiers too
+    HIPCHK((launch_wave<32, 256, 1, true, false>(w, t, w.n_cus, s)));
+    HIPCHK((launch_wave<64, 2048, 1, true, false>(w, t, w.n_cus, s)));
+  } else {
+    HIPCHK((launch_wave<16, 256, 2, true, true>(w, t, w.n_cus, s)));
+    HIPCHK((launch_wave<64, 1024, 1, true, true>(w, t, w.n_cus, s)));
+  }
   k_bpe_long<true><<<128, 256, 0, s>>>(w, t);
   return hipGetLastError();
 }

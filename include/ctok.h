@@ -77,7 +77,7 @@ typedef struct ctok_stats {
   double ms_total;        /* wall time of the call (host clock)                        */
   double ms_device;       /* first kernel start -> last kernel end (HIP events)        */
   double ms_pretok;       /* normalise check + doc bitmap + pre-tokenizer/routing      */
-  double ms_bpe_short;    /* merge passes of pieces <= 32 bytes                          */
+  double ms_bpe_short;    /* merge passes of pieces <= 64 bytes                          */
   double ms_bpe_long;     /* wait for the long-piece pass (side stream) after them       */
   double ms_emit;         /* tile token scan + id emission + tok_off                   */
   double ms_h2d, ms_d2h;  /* host-buffer copies (ctok_encode_batch only)               */
@@ -86,9 +86,10 @@ typedef struct ctok_stats {
   uint64_t docs, pieces, long_pieces, tokens, nfc_docs;
   double ms_segment;      /* k_segment alone: piece starts + whole-piece probes/routing */
   double ms_bpe_lo;       /* k_bpe_short: pieces of <= 16 bytes (classes 0 and 1)        */
-  double ms_bpe_hi;       /* k_bpe_c2: pieces of 17..32 bytes (Bloom filter only in LDS) */
-  uint64_t class_bytes[3];  /* text bytes merged per length class (<= 8, 9..16, 17..32 B) */
-  uint64_t class_ids[3];    /* ids produced per length class                             */
+  double ms_bpe_hi;       /* k_bpe_mid: pieces of 17..64 bytes                           */
+  uint64_t class_bytes[4];  /* text bytes merged per length class (<= 8, 9..16, 17..32, 33..64 B) */
+  uint64_t class_ids[4];    /* ids produced per length class                             */
+  double ms_bpe_med;      /* reserved (0): classes 2 and 3 share k_bpe_mid               */
 } ctok_stats;
 
 /* Upper bound on the ids of a batch whose docs total `n_bytes` bytes (ids <= 3*bytes + docs:

@@ -1,0 +1,102 @@
+"""Every length tier of the BPE kernels against the C oracle, at and around its boundaries:
+the whole-piece probe (<= 8 B), the register passes (9..16, 17..32, 33..64 B: k_bpe_short,
+k_bpe_c2, k_bpe_c3), the dense wave tiers (65..256, 257..2048, 2049..4096 B: k_bpe_wave) and
+the global-memory linked-list tier beyond 4096 B (k_bpe_long).  Each length is tried with
+letters drawn from a small alphabet (many merges), with (x, x) chains ("aaaa", "====", whose
+rounds take every other site), with two-token periods, with multi-byte letters (CJK, 3 bytes
+each) and with a table that is not rank-monotone (one site per round)."""
+import json
+import random
+
+import pytest
+
+from complexity_tokenizer import Tokenizer
+from datagen import corpus
+from oracle import ref_c
+from tests import toys
+from tests.test_gpu_parity import assert_same
+
+pytestmark = pytest.mark.gpu
+
+LENGTHS = [8, 9, 16, 17, 31, 32, 33, 40, 63, 64, 65, 100, 255, 256, 257, 1000, 2047, 2048, 2049, 3000, 4095,
+           4096, 4097, 6000]
+
+
+def tier_docs(seed):
+    rng = random.Random(seed)
+    docs = []
+    for n in LENGTHS:
+        docs.append("".join(rng.choice("etaoinshr") for _ in range(n)))        # letters, many merges
+        docs.append("a" * n)                                                   # (x, x) chain
+        docs.append("=" * n)                                                   # punctuation chain
+        docs.append(("th" * n)[:n])                                            # two-token period
+        docs.append("".join(rng.choice("一二三四五六七八九十") for _ in range(max(1, n // 3))))  # 3-byte letters
+        docs.append(" " + "".join(rng.choice("0123456789") for _ in range(n - 1)))  # attached space + digits
+    rng.shuffle(docs)
+    return docs
+
+
+@pytest.fixture(scope="module")
+def gpt2(gpt2_path):
+    with open(gpt2_path) as f:
+        obj = json.load(f)
+    return obj, Tokenizer.from_file(gpt2_path), ref_c.RefC(obj)
+
+
+def check(tok, rc, docs):
+    text, off = corpus.pack([d.encode() for d in docs])
+    assert_same(*tok.encode_packed(text, off, timing=True), *rc.encode_packed(text, off))
+    return tok.last_stats
+
+
+def test_tiers_gpt2(gpt2):
+    _, tok, rc = gpt2
+    st = check(tok, rc, tier_docs(1))
+    assert st["long_pieces"] > 0 and st["class_ids"][3] > 0
+
+
+def test_tiers_multilingual(multi_path):
+    with open(multi_path) as f:
+        obj = json.load(f)
+    check(Tokenizer.from_file(multi_path), ref_c.RefC(obj), tier_docs(2))
+
+
+def test_tiers_improper_table(gpt2):
+    obj, _, _ = gpt2
+    sh = toys.shuffled_merges(obj, seed=5)
+    check(Tokenizer.from_str(json.dumps(sh)), ref_c.RefC(sh), tier_docs(3))
+
+
+def test_tiers_many_docs_interleaved(gpt2):
+    """Tiers running side by side in one call (merge passes on the main stream, long tiers on the
+    side stream) over a C2 sample with long docs spliced in."""
+    _, tok, rc = gpt2
+    text, off = corpus.corpus_c2(20_000, seed=31)
+    docs = [d.decode() for d in corpus.unpack(text, off)]
+    extra = tier_docs(4)
+    for i, d in enumerate(extra):
+        docs.insert((i * 7919) % len(docs), d)
+    check(tok, rc, docs)
+
+
+def test_pieces_across_tile_ends(gpt2, multi_path):
+    """Pieces that start in the last bytes of a 3968-byte pre-tokenizer tile and end in the next
+    one: past the tile's look-ahead they go to the long list even when shorter than 64 bytes."""
+    tile = 3968
+    rng = random.Random(9)
+    docs, pos = [], 0
+    for delta in range(1, 80):
+        for n in (33, 60, 62, 63, 64, 65, 70, 130):
+            target = ((pos + 200) // tile + 1) * tile
+            filler = target - delta - pos
+            docs.append(("ab " * filler)[:filler])
+            alpha = "一二三四五" if n % 2 else "etaoinshr"
+            piece = "".join(rng.choice(alpha) for _ in range(n))
+            piece = piece.encode()[:n].decode("utf-8", "ignore")
+            docs.append(piece)
+            pos = target - delta + len(piece.encode())
+    _, tok, rc = gpt2
+    check(tok, rc, docs)
+    with open(multi_path) as f:
+        obj = json.load(f)
+    check(Tokenizer.from_file(multi_path), ref_c.RefC(obj), docs)
