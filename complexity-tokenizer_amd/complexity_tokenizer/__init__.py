@@ -23,7 +23,8 @@ import numpy as np
 from . import _native as _n
 
 __version__ = "0.3.3"
-__all__ = ["Tokenizer", "PanicException", "UnsupportedConfigError", "DeviceError", "__version__"]
+__all__ = ["Tokenizer", "Encoding", "BatchEncoding", "PanicException", "UnsupportedConfigError", "DeviceError",
+           "__version__"]
 
 
 class PanicException(BaseException):
@@ -78,6 +79,38 @@ def pack_texts(texts) -> tuple[np.ndarray, np.ndarray]:
     return buf, off
 
 
+def _as_str(t):
+    if not isinstance(t, str):
+        raise TypeError("'%s' object cannot be converted to 'PyString'" % type(t).__name__)
+    return t
+
+
+def _as_str_list(texts):
+    if isinstance(texts, (str, bytes)):
+        raise TypeError("Can't extract `str` to `Vec`")
+    return [_as_str(t) for t in texts]
+
+
+def _extract_str_list(v):
+    """PyO3 `extract::<Vec<String>>()` as a test: a non-str sequence of str, else None."""
+    if isinstance(v, (str, bytes)):
+        return None
+    try:
+        items = list(v)
+    except TypeError:
+        return None
+    return items if all(isinstance(x, str) for x in items) else None
+
+
+def _split_pairs(pairs):
+    a, b = [], []
+    for p in pairs:
+        x, y = p
+        a.append(_as_str(x))
+        b.append(_as_str(y))
+    return a, b
+
+
 def pack_ids(batch) -> tuple[np.ndarray, np.ndarray]:
     """list[list[int]] -> (uint32 ids, uint64 offsets[D+1]).  Mirrors the PyO3 `Vec<Vec<u32>>`
     extraction: a bare str is refused, elements must be ints in [0, 2**32)."""
@@ -114,6 +147,9 @@ def _split_lists(flat: np.ndarray, off: np.ndarray) -> list:
     finally:
         if was:
             gc.enable()
+
+
+from .encoding import BatchEncoding, Encoding  # noqa: E402
 
 
 class Tokenizer:
@@ -281,6 +317,275 @@ class Tokenizer:
         if not isinstance(text, str):
             raise TypeError("'%s' object cannot be converted to 'PyString'" % type(text).__name__)
         return self.encode_batch([text])[0]
+
+    # ------------------------------------------------------------------ padded encode / Encodings
+    # __call__, encode_to_encoding, encode_batch_with_padding, ...
+    # (src/bindings/tokenizer.rs:46-201, :256-371 -> src/huggingface/mod.rs:340-545).  The ids,
+    # post-processor, truncation, padding and the three masks come from the GPU
+    # (ctok_encode_padded); Encoding objects are assembled on the host from its rows.
+
+    @property
+    def model_max_length(self) -> int:
+        return int(_n.lib.ctok_model_max_length(self._h))
+
+    @property
+    def padding_side(self) -> str:
+        return "right"  # from_file / from_str (src/huggingface/mod.rs:325); setters are out of scope
+
+    @property
+    def is_fast(self) -> bool:
+        return True
+
+    def num_special_tokens_to_add(self, is_pair: bool = False) -> int:
+        """src/bindings/tokenizer.rs:248-251 -> src/huggingface/mod.rs:915-932."""
+        return int(_n.lib.ctok_num_special_tokens_to_add(self._h, 1 if is_pair else 0))
+
+    def _pad_id_token(self):
+        """(pad id, pad token) as chosen by the reference (src/huggingface/mod.rs:500-505)."""
+        pid = int(_n.lib.ctok_pad_id(self._h))
+        tok = self._tok_str(pid)
+        return pid, (tok if tok is not None else "<pad>")
+
+    def _tok_str(self, i):
+        """Vocab::get_token (model.vocab only), cached per id."""
+        cache = self.__dict__.setdefault("_tok_cache", {})
+        if i not in cache:
+            cache[i] = self.id_to_token(i)
+        return cache[i]
+
+    def get_special_tokens_mask(self, ids, already_has_special_tokens: bool = True) -> list:
+        """src/bindings/tokenizer.rs:243-246 -> src/huggingface/mod.rs:899-913."""
+        if not already_has_special_tokens:
+            return [0] * len(ids)
+        sp = self.special_tokens
+        return [1 if (self._tok_str(int(i)) is not None and self._tok_str(int(i)) in sp) else 0 for i in ids]
+
+    def encode_padded(self, texts, pairs=None, *, add_special_tokens: bool = True, truncation: bool = False,
+                      max_length: int | None = None, padding: str | None = None, pad_left: bool = False,
+                      pad_id: int | None = None, timing: bool = False, no_postprocess: bool = False) -> dict:
+        """Extension: the batch as [rows, width] uint32 arrays straight from the GPU --
+        input_ids, attention_mask, token_type_ids, special_tokens_mask, plus row_len (content +
+        padding).  padding: None, "longest" or "max_length"; pairs: a list of second texts (row r
+        = texts[r] + pairs[r]).  Semantics as encode_batch_with_padding / __call__ (include/ctok.h,
+        CTOK_P_*), without overflowing windows."""
+        if pairs is not None:
+            if len(pairs) != len(texts):
+                raise ValueError("pairs must have one entry per text")
+            docs = [x for ab in zip(texts, pairs) for x in ab]
+        else:
+            docs = list(texts)
+        text, off = pack_texts(docs)
+        rows = len(texts)
+        f = 0
+        if add_special_tokens:
+            f |= _n.CTOK_P_ADD_SPECIAL
+        if pairs is not None:
+            f |= _n.CTOK_P_PAIRS
+        if truncation:
+            f |= _n.CTOK_P_TRUNCATE
+        if padding == "longest":
+            f |= _n.CTOK_P_PAD_LONGEST
+        elif padding == "max_length":
+            f |= _n.CTOK_P_PAD_TO_MAX
+        elif padding is not None:
+            raise ValueError("padding must be None, 'longest' or 'max_length'")
+        if pad_left:
+            f |= _n.CTOK_P_PAD_LEFT
+        if pad_id is not None:
+            f |= _n.CTOK_P_PAD_ID
+        if no_postprocess:
+            f |= _n.CTOK_P_NO_POSTPROCESS
+        ml = int(max_length) if max_length is not None else self.model_max_length
+        opts = _n.PadOpts(f, int(pad_id or 0), ml)
+        # first guess of the width: ids <= bytes unless NFC grows the text (then the call reports
+        # the width it needs and runs again)
+        lens = np.diff(off.astype(np.int64))
+        if pairs is not None:
+            lens = lens.reshape(-1, 2).sum(axis=1) if rows else lens[:0]
+        items = self._pp_items() if (add_special_tokens and not no_postprocess) else None
+        n_a = items.count(_n.CTOK_PP_SEQUENCE) if items is not None else 1
+        n_s = len(items) - n_a if items is not None else 0
+        width = (int(lens.max()) * max(n_a, 1) + n_s + 1) if rows else 0
+        if truncation:
+            width = min(width, ml)
+        if padding == "max_length":
+            width = max(width, ml)
+        while True:
+            cap = max(rows * width, 1)
+            arrs = [np.empty(cap, dtype=np.uint32) for _ in range(4)]
+            row_len = np.empty(max(rows, 1), dtype=np.uint64)
+            wout = ctypes.c_uint64()
+            st = _n.Stats()
+            ex = _n.Exec(self.device, None, _n.CTOK_F_TIMING if timing else 0)
+            rc = _n.lib.ctok_encode_padded(self._h, text.ctypes.data, off.ctypes.data, len(docs), ctypes.byref(opts),
+                                           arrs[0].ctypes.data, arrs[1].ctypes.data, arrs[2].ctypes.data,
+                                           arrs[3].ctypes.data, cap, row_len.ctypes.data, ctypes.byref(wout),
+                                           ctypes.byref(ex), ctypes.byref(st))
+            if rc == _n.CTOK_E_CAPACITY and int(wout.value) > width:
+                width = int(wout.value)
+                continue
+            if rc != _n.CTOK_OK:
+                _raise(rc)
+            break
+        self.last_stats = st.as_dict()
+        w = int(wout.value)
+        shape = (rows, w)
+        out = {k: a[: rows * w].reshape(shape) for k, a in
+               zip(("input_ids", "attention_mask", "token_type_ids", "special_tokens_mask"), arrs)}
+        out["row_len"] = row_len[:rows].astype(np.int64)
+        return out
+
+    def _pp_items(self):
+        """The post-processor as items (CTOK_PP_SEQUENCE = the ids), None without one."""
+        n = ctypes.c_int64()
+        buf = (ctypes.c_uint32 * 64)()
+        rc = _n.lib.ctok_post_processor(self._h, buf, 64, ctypes.byref(n))
+        if rc != _n.CTOK_OK:
+            _raise(rc)
+        return None if n.value < 0 else list(buf[: n.value])
+
+    def _to_encodings(self, texts, pairs=None, add_special_tokens=True) -> list:
+        """Encodings before truncation / padding, from one GPU call (rows unpadded):
+        add_special_tokens -> encode_to_encoding / encode_pair_to_encoding
+        (src/huggingface/mod.rs:340-392), else Encoding::from_ids over encode() (+ merge for a
+        pair, src/bindings/tokenizer.rs:64-97)."""
+        r = self.encode_padded(texts, pairs, add_special_tokens=add_special_tokens)
+        items = self._pp_items() if add_special_tokens else None
+        seq = _n.CTOK_PP_SEQUENCE
+        orig_rows = None
+        if items is not None and seq not in items:  # the ids are not in the rows: fetch them apart
+            orig_rows = self.encode_padded(texts, pairs, add_special_tokens=True, no_postprocess=True)
+        n_a = items.count(seq) if items is not None else 0
+        n_s = len(items) - n_a if items is not None else 0
+        first_a = items.index(seq) if (items is not None and n_a) else 0
+        ids2d, att, typ, spc, rl = (r["input_ids"], r["attention_mask"], r["token_type_ids"],
+                                    r["special_tokens_mask"], r["row_len"])
+        encs = []
+        was = gc.isenabled()
+        gc.disable()
+        try:
+            for i in range(len(texts)):
+                L = int(rl[i])
+                ids = ids2d[i, :L].tolist()
+                types = typ[i, :L].tolist()
+                if add_special_tokens:
+                    if items is None:
+                        n, orig = L, ids
+                    elif n_a:
+                        n = (L - n_s) // n_a
+                        orig = ids[first_a: first_a + n]
+                    else:
+                        n = int(orig_rows["row_len"][i])
+                        orig = orig_rows["input_ids"][i, :n].tolist()
+                    # one token string per original id, "" outside model.vocab (mod.rs:410); the
+                    # post-processor adds no tokens (mod.rs:378-386)
+                    toks = [(self._tok_str(t) or "") for t in orig]
+                    na = types[:n].count(0)
+                    encs.append(Encoding(ids, types, toks, att[i, :L].tolist(), spc[i, :L].tolist(), None, None,
+                                         [0] * na + [1] * (n - na)))
+                else:
+                    toks = [t for t in (self._tok_str(x) for x in ids) if t is not None]
+                    na = types.count(0)
+                    encs.append(Encoding(ids, types, toks, att[i, :L].tolist(), spc[i, :L].tolist(), [], [],
+                                         [0] * na + [1] * (L - na)))
+        finally:
+            if was:
+                gc.enable()
+        return encs
+
+    def encode_to_encoding(self, text: str) -> Encoding:
+        """src/bindings/tokenizer.rs:298-300 -> src/huggingface/mod.rs:340-342."""
+        return self._to_encodings([_as_str(text)])[0]
+
+    def encode_plus(self, text: str) -> Encoding:
+        """src/bindings/tokenizer.rs:258-260."""
+        return self.encode_to_encoding(text)
+
+    def encode_pair_to_encoding(self, text: str, text_pair: str) -> Encoding:
+        """src/bindings/tokenizer.rs:302-304 -> src/huggingface/mod.rs:344-346."""
+        return self._to_encodings([_as_str(text)], [_as_str(text_pair)])[0]
+
+    def encode_with_truncation(self, text: str, text_pair: str | None = None, max_length: int = 512,
+                               stride: int = 0) -> Encoding:
+        """src/bindings/tokenizer.rs:306-318 -> src/huggingface/mod.rs:348-392: truncation
+        with stride (0 = plain windows) when longer than max_length."""
+        enc = (self.encode_pair_to_encoding(text, text_pair) if text_pair is not None
+               else self.encode_to_encoding(text))
+        if len(enc) > max_length:
+            enc.truncate_with_stride(max_length, stride)
+        return enc
+
+    def encode_batch_to_encoding(self, texts) -> list:
+        """src/bindings/tokenizer.rs:320-326 -> src/huggingface/mod.rs:483-485."""
+        return self._to_encodings(_as_str_list(texts))
+
+    def batch_encode_plus(self, texts) -> list:
+        """src/bindings/tokenizer.rs:262-269."""
+        return self.encode_batch_to_encoding(texts)
+
+    def encode_batch_pairs_to_encoding(self, pairs) -> list:
+        """src/bindings/tokenizer.rs:328-336 -> src/huggingface/mod.rs:487-491."""
+        a, b = _split_pairs(pairs)
+        return self._to_encodings(a, b)
+
+    def _pad_all(self, encs, max_length, pad_left):
+        target = max_length if max_length is not None else max((len(e) for e in encs), default=0)
+        pid, ptok = self._pad_id_token()
+        for e in encs:
+            e.pad(target, pid, ptok, pad_left)
+        return encs
+
+    def encode_batch_with_padding(self, texts, max_length: int | None = None, pad_left: bool = False) -> list:
+        """src/bindings/tokenizer.rs:338-350 -> src/huggingface/mod.rs:493-517 (no truncation:
+        a row longer than max_length stays longer)."""
+        return self._pad_all(self.encode_batch_to_encoding(texts), max_length, pad_left)
+
+    def encode_batch_pairs_with_padding(self, pairs, max_length: int | None = None, pad_left: bool = False) -> list:
+        """src/bindings/tokenizer.rs:352-367 -> src/huggingface/mod.rs:519-543."""
+        return self._pad_all(self.encode_batch_pairs_to_encoding(pairs), max_length, pad_left)
+
+    def __call__(self, text, text_pair=None, add_special_tokens: bool = True, padding: str | None = None,
+                 truncation: bool = False, max_length: int | None = None, stride: int = 0,
+                 return_attention_mask: bool = True, return_token_type_ids: bool = True,
+                 return_offsets_mapping: bool = False, return_special_tokens_mask: bool = False) -> BatchEncoding:
+        """src/bindings/tokenizer.rs:33-201."""
+        flags = (return_attention_mask, return_token_type_ids, return_offsets_mapping, return_special_tokens_mask)
+        max_len = max_length if max_length is not None else self.model_max_length
+        batch = _extract_str_list(text)
+        if batch is not None:
+            pairs = _extract_str_list(text_pair) if text_pair is not None else None
+            if pairs is not None:
+                m = min(len(batch), len(pairs))  # Iterator::zip
+                encs = self._to_encodings(batch[:m], pairs[:m], add_special_tokens)
+            else:
+                encs = self._to_encodings(batch, None, add_special_tokens)
+            longest = max((len(e) for e in encs), default=0)
+        elif isinstance(text, str):
+            pair = text_pair if isinstance(text_pair, str) else None
+            encs = self._to_encodings([text], [pair] if pair is not None else None, add_special_tokens)
+            longest = len(encs[0])
+        else:
+            raise TypeError("Expected str or List[str]")
+        if truncation:
+            for e in encs:
+                if len(e) > max_len:
+                    if stride > 0:
+                        e.truncate_with_stride(max_len, stride)
+                    else:
+                        e.truncate(max_len)
+            if batch is None:
+                longest = len(encs[0])
+        if padding is not None:
+            if batch is not None:
+                target = max_len if padding == "max_length" else max((len(e) for e in encs), default=0)
+            else:
+                target = max_len if padding == "max_length" else len(encs[0])
+            pid, ptok = self._pad_id_token()
+            left = padding == "left" or self.padding_side == "left"
+            for e in encs:
+                e.pad(target, pid, ptok, left)
+        del longest
+        return BatchEncoding(encs, *flags)
 
     # ------------------------------------------------------------------ decode
     def decode_packed(self, ids: np.ndarray, tok_off: np.ndarray, skip_special_tokens: bool = False,

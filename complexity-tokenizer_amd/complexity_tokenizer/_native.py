@@ -90,6 +90,21 @@ class DecodeStats(ctypes.Structure):
 CTOK_D_SKIP_SPECIAL = 1
 CTOK_D_CLEANUP = 2
 
+CTOK_P_ADD_SPECIAL = 1
+CTOK_P_PAIRS = 2
+CTOK_P_TRUNCATE = 4
+CTOK_P_PAD_LONGEST = 8
+CTOK_P_PAD_TO_MAX = 16
+CTOK_P_PAD_LEFT = 32
+CTOK_P_PAD_ID = 64
+CTOK_P_NO_POSTPROCESS = 128
+CTOK_PP_SEQUENCE = 0xFFFFFFFF
+
+
+class PadOpts(ctypes.Structure):
+    _fields_ = [("flags", ctypes.c_uint32), ("pad_id", ctypes.c_uint32), ("max_length", ctypes.c_uint64)]
+
+
 _p = ctypes.c_void_p
 _u64 = ctypes.c_uint64
 _u64p = ctypes.POINTER(ctypes.c_uint64)
@@ -112,6 +127,14 @@ SIGS = {
     "ctok_encode_batch_device": (ctypes.c_int, [_p, _p, _p, _u64, _u64, _p, _u64, _p, _u64p, ctypes.POINTER(Exec),
                                                 ctypes.POINTER(Stats)]),
     "ctok_device_count": (ctypes.c_int, []),
+    "ctok_encode_padded": (ctypes.c_int, [_p, _p, _p, _u64, ctypes.POINTER(PadOpts), _p, _p, _p, _p, _u64, _p, _u64p,
+                                          ctypes.POINTER(Exec), ctypes.POINTER(Stats)]),
+    "ctok_encode_padded_device": (ctypes.c_int, [_p, _p, _p, _u64, _u64, ctypes.POINTER(PadOpts), _p, _p, _p, _p, _u64, _p,
+                                                 _u64p, ctypes.POINTER(Exec), ctypes.POINTER(Stats)]),
+    "ctok_model_max_length": (_u64, [_p]),
+    "ctok_pad_id": (ctypes.c_uint32, [_p]),
+    "ctok_num_special_tokens_to_add": (_u64, [_p, ctypes.c_int]),
+    "ctok_post_processor": (ctypes.c_int, [_p, _u32p, _u64, ctypes.POINTER(ctypes.c_int64)]),
     "ctok_decode_batch": (ctypes.c_int, [_p, _p, _p, _u64, ctypes.c_uint32, _p, _u64, _p, ctypes.POINTER(Exec),
                                          ctypes.POINTER(DecodeStats)]),
     "ctok_decode_batch_device": (ctypes.c_int, [_p, _p, _p, _u64, _u64, ctypes.c_uint32, _p, _u64, _p, _u64p,

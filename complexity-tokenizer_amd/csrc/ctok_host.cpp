@@ -228,6 +228,10 @@ struct DeviceState {
   hipEvent_t dev_ev[8] = {};
   // host-API staging
   std::unique_ptr<HostPipe> pipe;
+  // padded encode: encoded ids, special ids, counters; host-API input / outputs
+  DevBuf<uint32_t> pad_ids, pad_special, pad_ctr, pad_out[4];
+  DevBuf<uint64_t> pad_tokoff, pad_rowlen, pad_in_off;
+  DevBuf<uint8_t> pad_in_text;
   ~DeviceState() {
     if (device >= 0) {
       (void)hipSetDevice(device);
@@ -285,6 +289,14 @@ struct ctok {
   std::string decoder_name;         // for the unsupported message
   std::vector<uint32_t> dec_ent;    // 2 u32 per id: byte offset, length | kDecNonAscii | kDecSpecial
   std::vector<uint8_t> dec_bytes;   // each id's bytes, 4-byte aligned, + 8 bytes of padding
+  // post-processor, compiled to the items of PostProcessor::process(ids, None)
+  // (src/postprocessors.rs:34-55): kPadItemA = the row's ids, else one special id
+  bool has_pp = false;
+  std::vector<uint32_t> pp_items;
+  int pp_kind = 0;                   // 1 TemplateProcessing, 2 RobertaProcessing, 3 BertProcessing
+  std::string pp_single, pp_pair;    // template strings (num_special_tokens_to_add)
+  bool pp_has_pair = false;
+  uint64_t model_max_length = 512;  // from_file / from_str: src/huggingface/mod.rs:243-245
   // per device
   std::mutex dev_mu;
   std::map<int, std::unique_ptr<DeviceState>> devs;
@@ -321,6 +333,137 @@ int parse_normalizer(const ctj::Value* v) {
     }
   }
   return 1;  // null, absent, or an object without "type": NFC (parsing.rs:89)
+}
+
+bool is_white_space(uint32_t c) {  // Unicode White_Space (Rust char::is_whitespace)
+  return (c >= 9 && c <= 13) || c == 32 || c == 0x85 || c == 0xA0 || c == 0x1680 || (c >= 0x2000 && c <= 0x200A) ||
+         c == 0x2028 || c == 0x2029 || c == 0x202F || c == 0x205F || c == 0x3000;
+}
+
+std::string encode_utf8(const std::vector<uint32_t>& cps, size_t a, size_t b) {
+  std::string s;
+  for (size_t i = a; i < b; i++) {
+    const uint32_t c = cps[i];
+    if (c < 0x80) {
+      s += (char)c;
+    } else if (c < 0x800) {
+      s += (char)(0xC0 | (c >> 6));
+      s += (char)(0x80 | (c & 63));
+    } else if (c < 0x10000) {
+      s += (char)(0xE0 | (c >> 12));
+      s += (char)(0x80 | ((c >> 6) & 63));
+      s += (char)(0x80 | (c & 63));
+    } else {
+      s += (char)(0xF0 | (c >> 18));
+      s += (char)(0x80 | ((c >> 12) & 63));
+      s += (char)(0x80 | ((c >> 6) & 63));
+      s += (char)(0x80 | (c & 63));
+    }
+  }
+  return s;
+}
+
+// parse_post_processor (src/huggingface/parsing.rs:193-253) and PostProcessor::process(ids, None)
+// (src/postprocessors.rs:34-147), compiled to a list of items: kPadItemA = the sequence's ids,
+// anything else = one special id.  The encode paths only ever call process(ids, None), so a
+// template's $B and the pair template are never used.  "Sequence" and other types -> None.
+void parse_post_processor(ctok* t, const ctj::Value* v) {
+  t->has_pp = false;
+  t->pp_items.clear();
+  t->pp_kind = 0;
+  if (!v || v->kind != ctj::Value::Object) return;
+  const ctj::Value* ty = v->get("type");
+  if (!ty) return;
+  const std::string kind = ty->kind == ctj::Value::String ? ty->s : "";
+  auto special = [&](const std::string& name, bool* found) -> uint32_t {
+    for (const auto& e : t->special)
+      if (e.first == name) {
+        *found = true;
+        return e.second;
+      }
+    *found = false;
+    return 0;
+  };
+  if (kind == "TemplateProcessing") {
+    std::string tpl = "<s> $A </s>";
+    const ctj::Value* single = v->get("single");
+    if (single && single->kind == ctj::Value::Array) {  // template_from_array (parsing.rs:236-253)
+      std::vector<std::string> parts;
+      for (const auto& item : single->arr) {
+        if (item.kind != ctj::Value::Object) continue;
+        if (const ctj::Value* sp = item.get("SpecialToken")) {
+          const ctj::Value* id = sp->get("id");
+          if (id && id->kind == ctj::Value::String) parts.push_back(id->s);
+          continue;
+        }
+        if (const ctj::Value* sq = item.get("Sequence")) {
+          const ctj::Value* id = sq->get("id");
+          if (id && id->kind == ctj::Value::String) parts.push_back("$" + id->s);
+        }
+      }
+      tpl.clear();
+      for (size_t i = 0; i < parts.size(); i++) tpl += (i ? " " : "") + parts[i];
+    }
+    t->pp_single = tpl;
+    if (const ctj::Value* pair = v->get("pair")) {
+      if (pair->kind == ctj::Value::Array) {
+        std::string ps;
+        bool first = true;
+        for (const auto& item : pair->arr) {
+          if (item.kind != ctj::Value::Object) continue;
+          std::string part;
+          bool ok = false;
+          if (const ctj::Value* sp = item.get("SpecialToken")) {
+            const ctj::Value* id = sp->get("id");
+            if (id && id->kind == ctj::Value::String) part = id->s, ok = true;
+          } else if (const ctj::Value* sq = item.get("Sequence")) {
+            const ctj::Value* id = sq->get("id");
+            if (id && id->kind == ctj::Value::String) part = "$" + id->s, ok = true;
+          }
+          if (ok) {
+            ps += (first ? "" : " ") + part;
+            first = false;
+          }
+        }
+        t->pp_pair = ps;
+        t->pp_has_pair = true;
+      }
+    }
+    t->pp_kind = 1;
+    std::vector<uint32_t> ch;
+    if (!decode_utf8(tpl, ch)) throw_err(CTOK_E_PARSE, "post_processor template is not valid UTF-8");
+    size_t i = 0;  // template_process's walk (postprocessors.rs:103-144)
+    while (i < ch.size()) {
+      if (ch[i] == '$' && i + 1 < ch.size()) {
+        if (ch[i + 1] == 'A') t->pp_items.push_back(kPadItemA);
+        if (ch[i + 1] == 'A' || ch[i + 1] == 'B') i += 2;  // $B: the pair, absent in process(ids, None)
+        else i += 1;
+      } else if (ch[i] == '<' || ch[i] == '[') {
+        const uint32_t end = ch[i] == '<' ? '>' : ']';
+        const size_t a = i;
+        while (i < ch.size() && ch[i] != end) i++;
+        if (i < ch.size()) i++;  // include the end char
+        size_t b = i;
+        while (b > a && is_white_space(ch[b - 1])) b--;  // str::trim (the start is '<' or '[')
+        bool found;
+        const uint32_t id = special(encode_utf8(ch, a, b), &found);
+        if (found) t->pp_items.push_back(id);
+      } else {
+        i++;
+      }
+    }
+    t->has_pp = true;
+  } else if (kind == "RobertaProcessing" || kind == "BertProcessing") {  // parsing.rs:221-236
+    const bool roberta = kind == "RobertaProcessing";
+    bool f;
+    uint32_t a = special(roberta ? "<s>" : "[CLS]", &f);
+    if (!f) a = roberta ? 0 : 101;
+    uint32_t b = special(roberta ? "</s>" : "[SEP]", &f);
+    if (!f) b = roberta ? 2 : 102;
+    t->pp_items = {a, kPadItemA, b};  // roberta_process / bert_process with no pair
+    t->has_pp = true;
+    t->pp_kind = roberta ? 2 : 3;
+  }
 }
 
 bool rust_regex_compiles(const std::string& p) {
@@ -730,6 +873,7 @@ void load(ctok* t, const char* buf, size_t len) {
   if (nbl != 1) throw_err(CTOK_E_UNSUPPORTED, "pre_tokenizer must contain exactly one ByteLevel");
 
   // decoder (parsing.rs:272-364) and the per-id decode table
+  parse_post_processor(t, root.get("post_processor"));
   t->decoder = parse_decoder(root.get("decoder"), t->decoder_name);
   build_decode_table(t);
 }
@@ -854,10 +998,14 @@ double now_ms() {
 // The pipeline on device-resident buffers.  Returns the token count.
 uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const uint64_t* d_off, uint64_t n_docs,
                        uint64_t n_bytes, uint32_t* d_ids, uint64_t ids_cap, uint64_t* d_tok_off, hipStream_t s,
-                       bool timing, ctok_stats* st) {
+                       bool timing, ctok_stats* st, bool split_added = true) {
   if (n_bytes >= 0xF0000000ull) throw_err(CTOK_E_ARG, "a single call is limited to < 3.75 GiB of text; split the batch");
   if (n_docs >= 0xF0000000ull) throw_err(CTOK_E_ARG, "too many documents in one call");
-  const Tables& tb = ds->t;
+  // split_added = false: encode_to_encoding's words go straight to BpeTokenizer::encode, with
+  // no added-token split (src/huggingface/mod.rs:395-420)
+  Tables tb_call = ds->t;
+  if (!split_added) tb_call.n_at = 0;
+  const Tables& tb = tb_call;
   // NFC speculation: when NFC is the only normalisation, run the pipeline on the raw text and
   // let k_segment flag any code point that NFC might change (NFC_QC != Yes or a non-zero
   // combining class; ASCII never is).  Only a flagged batch pays for the check + normalise
@@ -1636,6 +1784,188 @@ int ctok_encode_batch(const ctok* tc, const uint8_t* utf8_in, const uint64_t* do
       stats->tokens = total;
       stats->ms_total = now_ms() - t0;
     }
+  });
+}
+
+uint64_t ctok_model_max_length(const ctok* t) { return t ? t->model_max_length : 0; }
+
+int ctok_post_processor(const ctok* t, uint32_t* items, uint64_t cap, int64_t* n_items) {
+  if (!t || !n_items) return fail(CTOK_E_ARG, "null argument");
+  if (!t->has_pp) {
+    *n_items = -1;
+    return CTOK_OK;
+  }
+  *n_items = (int64_t)t->pp_items.size();
+  for (uint64_t i = 0; i < t->pp_items.size() && i < cap && items; i++) items[i] = t->pp_items[i];
+  return CTOK_OK;
+}
+
+// pad id: special_tokens["[PAD]"], else ["<pad>"], else 0 (src/huggingface/mod.rs:500-504)
+uint32_t ctok_pad_id(const ctok* t) {
+  if (!t) return 0;
+  for (const char* name : {"[PAD]", "<pad>"})
+    for (const auto& e : t->special)
+      if (e.first == name) return e.second;
+  return 0;
+}
+
+// src/huggingface/mod.rs:915-932
+uint64_t ctok_num_special_tokens_to_add(const ctok* t, int is_pair) {
+  if (!t) return 0;
+  if (t->pp_kind == 3) return is_pair ? 3 : 2;
+  if (t->pp_kind == 2) return is_pair ? 4 : 2;
+  if (t->pp_kind != 1) return 0;
+  const std::string& tpl = (is_pair && t->pp_has_pair) ? t->pp_pair : t->pp_single;
+  std::vector<uint32_t> ch;
+  if (!decode_utf8(tpl, ch)) return 0;
+  uint64_t n = 0;
+  size_t i = 0;
+  while (i < ch.size()) {  // split_whitespace, parts not starting with '$'
+    while (i < ch.size() && is_white_space(ch[i])) i++;
+    if (i >= ch.size()) break;
+    if (ch[i] != '$') n++;
+    while (i < ch.size() && !is_white_space(ch[i])) i++;
+  }
+  return n;
+}
+
+int ctok_encode_padded_device(const ctok* tc, const uint8_t* d_utf8, const uint64_t* d_doc_off, uint64_t n_docs,
+                              uint64_t n_bytes, const ctok_pad_opts* o, uint32_t* d_ids, uint32_t* d_attn,
+                              uint32_t* d_type, uint32_t* d_special, uint64_t cap, uint64_t* d_row_len,
+                              uint64_t* width_out, const ctok_exec* exec, ctok_stats* stats) {
+  if (!tc || !o || !d_doc_off || !d_row_len || !width_out || (n_bytes && !d_utf8))
+    return fail(CTOK_E_ARG, "null argument");
+  ctok* t = const_cast<ctok*>(tc);
+  return run([&] {
+    double t0 = now_ms();
+    const uint32_t f = o->flags;
+    const bool pairs = f & CTOK_P_PAIRS;
+    if (pairs && (n_docs & 1)) throw_err(CTOK_E_ARG, "CTOK_P_PAIRS needs an even number of documents");
+    const uint64_t rows = pairs ? n_docs / 2 : n_docs;
+    if (rows >= 0xFFFFFFFFull) throw_err(CTOK_E_ARG, "too many rows");
+    const bool add_special = f & CTOK_P_ADD_SPECIAL;
+    if (add_special && t->pp_items.size() > (size_t)kPadMaxItems)
+      throw_err(CTOK_E_UNSUPPORTED, "post-processor template with more than 16 items");
+    int dev = exec ? exec->device : 0;
+    DeviceState* ds = device_state(t, dev);
+    std::lock_guard<std::mutex> lk(ds->mu);
+    HIPTRY(hipSetDevice(dev));
+    hipStream_t s = exec && exec->stream ? (hipStream_t)exec->stream : ds->stream;
+    const bool timing = exec && (exec->flags & CTOK_F_TIMING);
+    // 1. encode (encode_to_encoding flavour: no added-token split)
+    const uint64_t cap_ids = ctok_ids_bound(t, n_bytes, n_docs);
+    ds->pad_ids.ensure(cap_ids);
+    ds->pad_tokoff.ensure(n_docs + 1);
+    ctok_stats st{};
+    encode_device(t, ds, d_utf8, d_doc_off, n_docs, n_bytes, ds->pad_ids.p, ds->pad_ids.cap, ds->pad_tokoff.p, s,
+                  timing, &st, !add_special);
+    // 2. row lengths and the longest row
+    std::vector<uint32_t> sp;
+    for (const auto& e : t->special) sp.push_back(e.second);
+    std::sort(sp.begin(), sp.end());
+    sp.erase(std::unique(sp.begin(), sp.end()), sp.end());
+    ds->pad_special.ensure(sp.size() + 1);
+    if (!sp.empty()) HIPTRY(hipMemcpyAsync(ds->pad_special.p, sp.data(), sp.size() * 4, hipMemcpyHostToDevice, s));
+    ds->pad_ctr.ensure(4);
+    HIPTRY(hipMemsetAsync(ds->pad_ctr.p, 0, 16, s));
+    PadWork w{};
+    w.ids = ds->pad_ids.p;
+    w.tok_off = ds->pad_tokoff.p;
+    w.n_rows = (uint32_t)rows;
+    w.pairs = pairs ? 1 : 0;
+    w.use_tpl = (add_special && t->has_pp && !(f & CTOK_P_NO_POSTPROCESS)) ? 1 : 0;
+    w.n_items = w.use_tpl ? (uint32_t)t->pp_items.size() : 0;
+    for (uint32_t k = 0; k < w.n_items; k++) w.items[k] = t->pp_items[k];
+    w.mark = (add_special && !(f & CTOK_P_NO_POSTPROCESS)) ? 1 : 0;
+    w.special_ids = ds->pad_special.p;
+    w.n_special = (uint32_t)sp.size();
+    w.truncate = (f & CTOK_P_TRUNCATE) ? 1 : 0;
+    w.max_len = o->max_length;
+    w.target = 0;
+    if (f & CTOK_P_PAD_TO_MAX) w.target = o->max_length;
+    w.pad_left = (f & CTOK_P_PAD_LEFT) ? 1 : 0;
+    w.pad_id = (f & CTOK_P_PAD_ID) ? o->pad_id : ctok_pad_id(t);
+    w.row_len = d_row_len;
+    w.counters = ds->pad_ctr.p;
+    HIPTRY(launch_pad_len(w, s));
+    HIPTRY(hipMemcpyAsync(ds->host, ds->pad_ctr.p, 16, hipMemcpyDeviceToHost, s));
+    spin_sync(ds, s);
+    const uint64_t longest = ((volatile uint64_t*)ds->host)[0];
+    const uint32_t dropped = ((volatile uint32_t*)ds->host)[2];
+    if (w.use_tpl && dropped)
+      throw_err(CTOK_E_PANIC, "attempt to subtract with overflow: the post-processor template drops ids (reference src/huggingface/mod.rs:378)");
+    if ((f & CTOK_P_PAD_LONGEST) && !(f & CTOK_P_PAD_TO_MAX)) {
+      w.target = longest;  // every row padded to the longest: row_len again
+      HIPTRY(launch_pad_len(w, s));
+    }
+    const uint64_t width = std::max<uint64_t>(longest, w.target);
+    *width_out = width;
+    w.width = width;
+    if (rows * width > cap) {
+      HIPTRY(hipStreamSynchronize(s));
+      throw_err(CTOK_E_CAPACITY, "cap too small: *width_out holds the row width needed");
+    }
+    if (rows * width && !d_ids) throw_err(CTOK_E_ARG, "null ids");
+    w.out_ids = d_ids;
+    w.out_attn = d_attn;
+    w.out_type = d_type;
+    w.out_special = d_special;
+    HIPTRY(launch_pad_rows(w, s));
+    spin_sync(ds, s);
+    if (stats) {
+      *stats = st;
+      stats->ms_total = now_ms() - t0;
+    }
+  });
+}
+
+int ctok_encode_padded(const ctok* tc, const uint8_t* utf8, const uint64_t* doc_off, uint64_t n_docs,
+                       const ctok_pad_opts* o, uint32_t* ids, uint32_t* attn, uint32_t* type, uint32_t* special,
+                       uint64_t cap, uint64_t* row_len, uint64_t* width_out, const ctok_exec* exec, ctok_stats* stats) {
+  if (!tc || !o || !doc_off || !row_len || !width_out) return fail(CTOK_E_ARG, "null argument");
+  ctok* t = const_cast<ctok*>(tc);
+  return run([&] {
+    if (doc_off[0] != 0) throw_err(CTOK_E_ARG, "doc_off[0] must be 0");
+    for (uint64_t d = 0; d < n_docs; d++)
+      if (doc_off[d + 1] < doc_off[d]) throw_err(CTOK_E_ARG, "doc_off must be non-decreasing");
+    const uint64_t B = doc_off[n_docs];
+    if (B && !utf8) throw_err(CTOK_E_ARG, "null text");
+    const uint64_t rows = (o->flags & CTOK_P_PAIRS) ? n_docs / 2 : n_docs;
+    int dev = exec ? exec->device : 0;
+    DeviceState* ds = device_state(t, dev);
+    hipStream_t s;
+    {
+      std::lock_guard<std::mutex> lk(ds->mu);
+      HIPTRY(hipSetDevice(dev));
+      s = exec && exec->stream ? (hipStream_t)exec->stream : ds->stream;
+      ds->pad_in_text.ensure(B + 16);
+      ds->pad_in_off.ensure(n_docs + 1);
+      ds->pad_rowlen.ensure(rows + 1);
+      for (auto& b : ds->pad_out) b.ensure(cap ? cap : 1);
+      if (B) HIPTRY(hipMemcpyAsync(ds->pad_in_text.p, utf8, B, hipMemcpyHostToDevice, s));
+      HIPTRY(hipMemsetAsync(ds->pad_in_text.p + B, 0, 16, s));
+      HIPTRY(hipMemcpyAsync(ds->pad_in_off.p, doc_off, (n_docs + 1) * 8, hipMemcpyHostToDevice, s));
+    }
+    ctok_exec ex = exec ? *exec : ctok_exec{};
+    ex.stream = s;
+    uint64_t width = 0;
+    const int rc = ctok_encode_padded_device(t, ds->pad_in_text.p, ds->pad_in_off.p, n_docs, B, o, ds->pad_out[0].p,
+                                             attn ? ds->pad_out[1].p : nullptr, type ? ds->pad_out[2].p : nullptr,
+                                             special ? ds->pad_out[3].p : nullptr, cap, ds->pad_rowlen.p, &width, &ex,
+                                             stats);
+    *width_out = width;
+    if (rc != CTOK_OK && rc != CTOK_E_CAPACITY) throw_err(rc, g_err);
+    std::lock_guard<std::mutex> lk(ds->mu);
+    HIPTRY(hipMemcpyAsync(row_len, ds->pad_rowlen.p, rows * 8, hipMemcpyDeviceToHost, s));
+    if (rc == CTOK_OK && rows * width) {
+      const size_t nb = rows * width * 4;
+      HIPTRY(hipMemcpyAsync(ids, ds->pad_out[0].p, nb, hipMemcpyDeviceToHost, s));
+      if (attn) HIPTRY(hipMemcpyAsync(attn, ds->pad_out[1].p, nb, hipMemcpyDeviceToHost, s));
+      if (type) HIPTRY(hipMemcpyAsync(type, ds->pad_out[2].p, nb, hipMemcpyDeviceToHost, s));
+      if (special) HIPTRY(hipMemcpyAsync(special, ds->pad_out[3].p, nb, hipMemcpyDeviceToHost, s));
+    }
+    HIPTRY(hipStreamSynchronize(s));
+    if (rc == CTOK_E_CAPACITY) throw_err(CTOK_E_CAPACITY, "cap too small: *width_out holds the row width needed");
   });
 }
 

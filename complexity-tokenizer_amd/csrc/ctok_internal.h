@@ -201,6 +201,41 @@ hipError_t launch_dec_prepare(const DecWork& w, hipStream_t s);  // clean-up: tr
 hipError_t launch_dec_count(const DecWork& w, uint32_t* tmp, uint64_t tmp_cap, hipStream_t s);
 hipError_t launch_dec_write(const DecWork& w, uint8_t* out, uint64_t* out_off, hipStream_t s);
 
+// ---- padded batch encode (pad.hip): Encoding rows as [rows, width] arrays -----------------
+// Row r = doc r (or docs 2r, 2r+1 merged as a pair).  Its n ids pass through the post-processor
+// items (kPadItemA = the n ids, else one special id), are cut to max_len when truncating, and
+// padded to `target` on the right or the left (src/encoding.rs:87-224, src/huggingface/mod.rs:
+// 340-392, src/bindings/tokenizer.rs:46-201).
+constexpr uint32_t kPadItemA = 0xFFFFFFFFu;
+constexpr int kPadMaxItems = 16;
+
+struct PadWork {
+  const uint32_t* ids;       // encoded ids of the docs
+  const uint64_t* tok_off;   // [n_docs + 1]
+  uint32_t n_rows;
+  uint32_t pairs;            // 1: row r = docs 2r (type 0) and 2r + 1 (type 1)
+  uint32_t use_tpl;          // apply the post-processor items
+  uint32_t n_items;
+  uint32_t items[kPadMaxItems];
+  uint32_t mark;             // special_tokens_mask |= id is a special token (mark_special_tokens)
+  const uint32_t* special_ids;  // sorted
+  uint32_t n_special;
+  uint32_t truncate;
+  uint64_t max_len;
+  uint64_t target;           // pad to this length (0: no padding)
+  uint32_t pad_left;
+  uint32_t pad_id;
+  uint64_t width;            // columns of the outputs
+  uint32_t* out_ids;         // [n_rows * width]; the three masks may be null
+  uint32_t* out_attn;
+  uint32_t* out_type;
+  uint32_t* out_special;
+  uint64_t* row_len;         // [n_rows] length of the row (content + padding)
+  uint32_t* counters;        // [0..1] longest content (u64, atomicMax), [2] a template dropped ids
+};
+hipError_t launch_pad_len(const PadWork& w, hipStream_t s);
+hipError_t launch_pad_rows(const PadWork& w, hipStream_t s);
+
 // ---- launchers (kernels.hip) -----------------------------------------------------------
 void upload_done();
 hipError_t launch_docstart(const Work& w, hipStream_t s);

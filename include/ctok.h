@@ -161,6 +161,60 @@ int ctok_decode_batch_device(const ctok* tok, const uint32_t* d_ids, const uint6
                              uint64_t* d_out_off, uint64_t* n_bytes_out, const ctok_exec* exec,
                              ctok_decode_stats* stats);
 
+/* ------------------------------------------------- padded batch encode (Encoding rows as arrays)
+ * Tokenizer.__call__ / encode_batch_with_padding / encode_batch_to_encoding / encode_to_encoding
+ * (src/bindings/tokenizer.rs:46-201, :298-371 -> src/huggingface/mod.rs:340-545,
+ * src/encoding.rs:45-253), computed on the GPU as [rows, width] u32 arrays:
+ *   - CTOK_P_ADD_SPECIAL: the encode_to_encoding flavour -- words go to BPE with no added-token
+ *     split (mod.rs:395-420), the post-processor's process(ids, None) is applied (a pair is
+ *     merged first, so the *single* template wraps both sequences, mod.rs:365-376), the masks
+ *     are extended by the added count and special tokens are marked (mod.rs:378-387).
+ *     Without it: Encoding::from_ids over Tokenizer.encode's ids (tokenizer.rs:88-97).
+ *   - CTOK_P_PAIRS: docs 2r and 2r+1 form row r; the second sequence's ids get type id 1.
+ *   - CTOK_P_TRUNCATE: rows cut to max_length (Encoding::truncate keeps the first max_length).
+ *   - CTOK_P_PAD_LONGEST / CTOK_P_PAD_TO_MAX: pad (Encoding::pad) to the longest row / to
+ *     max_length, on the left with CTOK_P_PAD_LEFT; pad id = opts->pad_id with CTOK_P_PAD_ID,
+ *     else the reference's choice (special "[PAD]", else "<pad>", else 0).  Padding cells:
+ *     attention 0, type 0, special 1.  A row longer than the target is not cut.
+ * Row r occupies ids[r*width .. r*width + row_len[r]); cells past row_len hold padding values.
+ * attention / type_ids / special_mask may be NULL.  cap = elements available in each array;
+ * rows * width > cap -> CTOK_E_CAPACITY with *width_out and row_len filled.  A template that
+ * drops ids (the reference's usize underflow at mod.rs:378) -> CTOK_E_PANIC. */
+#define CTOK_P_ADD_SPECIAL 1u
+#define CTOK_P_PAIRS 2u
+#define CTOK_P_TRUNCATE 4u
+#define CTOK_P_PAD_LONGEST 8u
+#define CTOK_P_PAD_TO_MAX 16u
+#define CTOK_P_PAD_LEFT 32u
+#define CTOK_P_PAD_ID 64u
+#define CTOK_P_NO_POSTPROCESS 128u  /* with CTOK_P_ADD_SPECIAL: skip the post-processor (ids, marks) */
+
+typedef struct ctok_pad_opts {
+  uint32_t flags;       /* CTOK_P_* */
+  uint32_t pad_id;      /* with CTOK_P_PAD_ID */
+  uint64_t max_length;  /* CTOK_P_TRUNCATE limit and CTOK_P_PAD_TO_MAX target */
+} ctok_pad_opts;
+
+int ctok_encode_padded(const ctok* tok, const uint8_t* utf8, const uint64_t* doc_off, uint64_t n_docs,
+                       const ctok_pad_opts* opts, uint32_t* ids, uint32_t* attention_mask, uint32_t* type_ids,
+                       uint32_t* special_mask, uint64_t cap, uint64_t* row_len, uint64_t* width_out,
+                       const ctok_exec* exec, ctok_stats* stats);
+/* Same on HBM-resident buffers (device pointers, work on exec->stream); n_bytes = doc_off[n_docs]. */
+int ctok_encode_padded_device(const ctok* tok, const uint8_t* d_utf8, const uint64_t* d_doc_off, uint64_t n_docs,
+                              uint64_t n_bytes, const ctok_pad_opts* opts, uint32_t* d_ids, uint32_t* d_attention,
+                              uint32_t* d_type_ids, uint32_t* d_special, uint64_t cap, uint64_t* d_row_len,
+                              uint64_t* width_out, const ctok_exec* exec, ctok_stats* stats);
+/* The model_max_length used when max_length is not given (512 for from_file / from_str,
+ * src/huggingface/mod.rs:243-245) and the pad id the reference picks (mod.rs:500-504). */
+uint64_t ctok_model_max_length(const ctok* tok);
+uint32_t ctok_pad_id(const ctok* tok);
+/* The post-processor as applied by the padded encode: *n_items items (at most cap written), each
+ * CTOK_PP_SEQUENCE (the sequence's ids, "$A") or a special id; *n_items = -1 without one. */
+#define CTOK_PP_SEQUENCE 0xFFFFFFFFu
+int ctok_post_processor(const ctok* tok, uint32_t* items, uint64_t cap, int64_t* n_items);
+/* Tokenizer.num_special_tokens_to_add(is_pair)  src/bindings/tokenizer.rs:248-251 -> mod.rs:915-932 */
+uint64_t ctok_num_special_tokens_to_add(const ctok* tok, int is_pair);
+
 /* Number of HIP devices visible to the library (0 when none; encode calls then fail with
  * CTOK_E_DEVICE -- there is no CPU fallback). */
 int ctok_device_count(void);

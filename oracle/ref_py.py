@@ -163,6 +163,8 @@ class RefTokenizer:
         self.byte_encoder = bytes_to_unicode()
         self.id_to_token_map = {v: k for k, v in vocab.items()}
         self.decoder = parse_decoder(obj.get("decoder"))
+        self.post_processor = parse_post_processor(obj.get("post_processor"), self.special_tokens)
+        self.model_max_length = 512  # from_tokenizer_json (src/huggingface/mod.rs:243-245)
 
     @classmethod
     def from_file(cls, path):
@@ -338,6 +340,74 @@ class RefTokenizer:
         """src/huggingface/mod.rs:771-785 (rayon par_iter, order-preserving)."""
         return [self.decode_with_options(ids, skip_special_tokens, clean_up_tokenization_spaces) for ids in batch]
 
+    # --------------------------------------------------------------------- Encoding path (SURVEY 8f rank 2)
+    def encode_single_to_encoding(self, text, type_id):
+        """src/huggingface/mod.rs:395-443 (ids only per word: no added-token split; offsets and
+        word ids are not restated -- the GPU path does not produce them)."""
+        words = self._pre_tokenize(self._normalize(text, self.normalizer), self.pre_tokenizer)
+        ids = []
+        for w in words:
+            ids.extend(self.bpe(w))
+        toks = [self.id_to_token_map.get(i, "") for i in ids]
+        n = len(ids)
+        return RefEncoding(ids, [type_id] * n, toks, [1] * n, [0] * n, [type_id] * n)
+
+    def encode_to_encoding(self, text, pair=None):
+        """encode_to_encoding_impl, src/huggingface/mod.rs:358-392 (max_length None)."""
+        enc = self.encode_single_to_encoding(text, 0)
+        if pair is not None:
+            enc.merge(self.encode_single_to_encoding(pair, 1), 1)
+        processed = process_post(self.post_processor, enc.ids) if self.post_processor else list(enc.ids)
+        added = len(processed) - len(enc.ids)
+        if added < 0:
+            raise PanicException("attempt to subtract with overflow")
+        enc.ids = processed
+        enc.attention_mask += [1] * added
+        enc.special_tokens_mask += [1] * added
+        enc.type_ids += [0] * added
+        sp = set(self.special_tokens.values())
+        enc.special_tokens_mask = [1 if i in sp else m for i, m in zip(enc.ids, enc.special_tokens_mask)]
+        return enc
+
+    def encode_from_ids(self, text, pair=None):
+        """Tokenizer.__call__ with add_special_tokens=False (src/bindings/tokenizer.rs:64-97)."""
+        def from_ids(ids):
+            toks = [self.id_to_token_map[i] for i in ids if i in self.id_to_token_map]
+            n = len(ids)
+            return RefEncoding(list(ids), [0] * n, toks, [1] * n, [0] * n, [0] * n)
+        enc = from_ids(self.encode(text))
+        if pair is not None:
+            enc.merge(from_ids(self.encode(pair)), 1)
+        return enc
+
+    def pad_id_token(self):
+        """src/huggingface/mod.rs:500-505."""
+        pid = self.special_tokens.get("[PAD]", self.special_tokens.get("<pad>", 0))
+        return pid, self.id_to_token_map.get(pid, "<pad>")
+
+    def call(self, texts, pairs=None, add_special_tokens=True, padding=None, truncation=False, max_length=None,
+             stride=0):
+        """Tokenizer.__call__ on a list (src/bindings/tokenizer.rs:59-133): encodings as dicts."""
+        if pairs is not None:
+            encs = [(self.encode_to_encoding(a, b) if add_special_tokens else self.encode_from_ids(a, b))
+                    for a, b in zip(texts, pairs)]
+        else:
+            encs = [(self.encode_to_encoding(t) if add_special_tokens else self.encode_from_ids(t)) for t in texts]
+        max_len = max_length if max_length is not None else self.model_max_length
+        if truncation:
+            for e in encs:
+                if len(e.ids) > max_len:
+                    if stride > 0:
+                        e.truncate_with_stride(max_len, stride)
+                    else:
+                        e.truncate(max_len)
+        if padding is not None:
+            target = max_len if padding == "max_length" else max((len(e.ids) for e in encs), default=0)
+            pid, ptok = self.pad_id_token()
+            for e in encs:
+                e.pad(target, pid, ptok, padding == "left")
+        return encs
+
     # convenience for tests: regex pieces as raw byte strings
     def pieces(self, text):
         if self.pre_tokenizer[0] == "ByteLevel" and self.pre_tokenizer[1] and text and not text.startswith(" "):
@@ -484,3 +554,148 @@ def clean_up_tokenization_spaces_(text: str) -> str:
     if cur:
         words.append("".join(cur))
     return " ".join(words)
+
+
+
+# ------------------------------------------------------------------------- post-processors, Encoding
+def parse_post_processor(value, special_tokens):
+    """parse_post_processor (src/huggingface/parsing.rs:193-253): ('template', str) |
+    ('bert', cls, sep) | ('roberta', bos, eos) | None."""
+    if not isinstance(value, dict) or "type" not in value:
+        return None
+    kind = value["type"] if isinstance(value["type"], str) else ""
+    if kind == "TemplateProcessing":
+        single = value.get("single")
+        tpl = _template_from_array(single) if isinstance(single, list) else "<s> $A </s>"
+        return ("template", tpl, dict(special_tokens))
+    if kind == "RobertaProcessing":
+        return ("roberta", special_tokens.get("<s>", 0), special_tokens.get("</s>", 2))
+    if kind == "BertProcessing":
+        return ("bert", special_tokens.get("[CLS]", 101), special_tokens.get("[SEP]", 102))
+    return None
+
+
+def _template_from_array(arr):
+    """src/huggingface/parsing.rs:236-253."""
+    parts = []
+    for item in arr:
+        if not isinstance(item, dict):
+            continue
+        if "SpecialToken" in item:
+            i = item["SpecialToken"].get("id") if isinstance(item["SpecialToken"], dict) else None
+            if isinstance(i, str):
+                parts.append(i)
+            continue
+        if "Sequence" in item:
+            i = item["Sequence"].get("id") if isinstance(item["Sequence"], dict) else None
+            if isinstance(i, str):
+                parts.append("$" + i)
+    return " ".join(parts)
+
+
+def process_post(pp, ids):
+    """PostProcessor::process(ids, None) (src/postprocessors.rs:34-147)."""
+    if pp[0] in ("bert", "roberta"):
+        return [pp[1]] + list(ids) + [pp[2]]
+    tpl, special = pp[1], pp[2]
+    out, i = [], 0
+    while i < len(tpl):
+        ch = tpl[i]
+        if ch == "$" and i + 1 < len(tpl):
+            if tpl[i + 1] == "A":
+                out.extend(ids)
+                i += 2
+            elif tpl[i + 1] == "B":
+                i += 2
+            else:
+                i += 1
+        elif ch in "<[":
+            end = ">" if ch == "<" else "]"
+            start = i
+            while i < len(tpl) and tpl[i] != end:
+                i += 1
+            if i < len(tpl):
+                i += 1
+            tok = tpl[start:i].strip()
+            if tok in special:
+                out.append(special[tok])
+        else:
+            i += 1
+    return out
+
+
+class RefEncoding:
+    """src/encoding.rs: the fields the GPU path produces (offsets / word ids left out)."""
+
+    def __init__(self, ids, type_ids, tokens, attention_mask, special_tokens_mask, sequence_ids):
+        self.ids, self.type_ids, self.tokens = ids, type_ids, tokens
+        self.attention_mask, self.special_tokens_mask, self.sequence_ids = attention_mask, special_tokens_mask, sequence_ids
+        self.overflowing = []
+
+    def merge(self, other, type_id):  # encoding.rs:240-255
+        n = len(other.ids)
+        self.ids = self.ids + other.ids
+        self.tokens = self.tokens + other.tokens
+        self.attention_mask = self.attention_mask + other.attention_mask
+        self.special_tokens_mask = self.special_tokens_mask + other.special_tokens_mask
+        self.type_ids = self.type_ids + [type_id] * n
+        self.sequence_ids = self.sequence_ids + [type_id] * n
+
+    def pad(self, target, pad_id, pad_token, left):  # encoding.rs:87-131
+        k = target - len(self.ids)
+        if k <= 0:
+            return
+        if left:
+            self.ids = [pad_id] * k + self.ids
+            self.type_ids = [0] * k + self.type_ids
+            self.tokens = [pad_token] * k + self.tokens
+            self.attention_mask = [0] * k + self.attention_mask
+            self.special_tokens_mask = [1] * k + self.special_tokens_mask
+            self.sequence_ids = [None] * k + self.sequence_ids
+        else:
+            self.ids += [pad_id] * k
+            self.type_ids += [0] * k
+            self.tokens += [pad_token] * k
+            self.attention_mask += [0] * k
+            self.special_tokens_mask += [1] * k
+            self.sequence_ids += [None] * k
+
+    @staticmethod
+    def _rs(v, a, b):  # Rust slice indexing
+        if a > b or b > len(v):
+            raise PanicException("slice index out of range")
+        return v[a:b]
+
+    def _cut(self, m):
+        for f in ("ids", "type_ids", "tokens", "attention_mask", "special_tokens_mask", "sequence_ids"):
+            setattr(self, f, getattr(self, f)[:m])
+
+    def truncate(self, m):  # encoding.rs:133-181
+        if len(self.ids) <= m:
+            return
+        r = self._rs
+        over = RefEncoding(r(self.ids, m, len(self.ids)), r(self.type_ids, m, len(self.type_ids)),
+                           r(self.tokens, m, len(self.tokens)), r(self.attention_mask, m, len(self.attention_mask)),
+                           r(self.special_tokens_mask, m, len(self.special_tokens_mask)),
+                           self.sequence_ids[m:] if len(self.sequence_ids) > m else [])
+        self.overflowing.append(over)
+        self._cut(m)
+
+    def truncate_with_stride(self, m, stride):  # encoding.rs:183-231
+        if len(self.ids) <= m:
+            return
+        pos, r = m, self._rs
+        while pos < len(self.ids):
+            start = max(0, pos - stride)
+            end = min(start + m, len(self.ids))
+            sq = self.sequence_ids[start:min(end, len(self.sequence_ids))] if len(self.sequence_ids) > start else []
+            self.overflowing.append(RefEncoding(r(self.ids, start, end), r(self.type_ids, start, end),
+                                                r(self.tokens, start, end), r(self.attention_mask, start, end),
+                                                r(self.special_tokens_mask, start, end), sq))
+            pos = end
+        self._cut(m)
+
+    def as_dict(self):
+        return {"ids": self.ids, "type_ids": self.type_ids, "tokens": self.tokens,
+                "attention_mask": self.attention_mask, "special_tokens_mask": self.special_tokens_mask,
+                "sequence_ids": self.sequence_ids, "overflowing": [o.as_dict() for o in self.overflowing]}
