@@ -1761,8 +1761,8 @@ hipError_t launch_bpe_long(const Work& w, const Tables& t, hipStream_t s) {
 // ------------------------------------------------------------------------------------------
 // emission.  tile_tok is scanned to each tile's first id; one workgroup per tile scans its
 // pieces' counts (blocked: 16 consecutive pieces per thread), copies each piece's ids from
-// scratch to ids[] (interleaved: coalesced writes), and leaves each piece's first id (within
-// the tile) in tcnt for k_tokoff.
+// scratch to ids[] (interleaved: coalesced writes), and leaves the first id (within the tile) of
+// each piece that starts a document in tcnt for k_tokoff (the only records it reads).
 
 __device__ __forceinline__ uint32_t rec_count(const Work& w, uint32_t v) {
   return (v & kRecHit) ? 1u : (v & kRecLong) ? w.long_cnt[v & ~kRecLong] : (v & 0xFFFFu);
@@ -1770,7 +1770,10 @@ __device__ __forceinline__ uint32_t rec_count(const Work& w, uint32_t v) {
 
 __global__ __launch_bounds__(256) void k_emit(Work w, uint32_t* __restrict__ ids, uint64_t ids_cap) {
   __shared__ uint32_t s_scan[17];
-  __shared__ uint32_t s_off[kTileSlots + 1];
+  // s_off[j + j / 16]: the padding makes the blocked writes (16 consecutive pieces per thread)
+  // conflict-free; the interleaved reads stay consecutive
+  __shared__ uint32_t s_off[kTileSlots + kTileSlots / 16 + 2];
+  auto so = [](uint32_t j) { return j + (j >> 4); };
   const uint32_t tile = blockIdx.x, tid = threadIdx.x;
   const uint32_t np = w.tile_np[tile];
   const uint64_t base = w.tile_tok[tile];
@@ -1799,10 +1802,10 @@ __global__ __launch_bounds__(256) void k_emit(Work w, uint32_t* __restrict__ ids
 #pragma unroll
   for (int k = 0; k < PER; k++) {
     pre[k] = o;
-    s_off[jb + k] = o;
+    s_off[so(jb + k)] = o;
     o += c[k];
   }
-  if (tid == 0) s_off[np] = total;
+  if (tid == 0) s_off[so(np)] = total;
   __syncthreads();
   // 2. copy, piece j = tid + 256 k: consecutive lanes write consecutive ids.  A whole-piece hit
   // carries its id in the record; other pieces read theirs from scratch, all first reads of a
@@ -1826,7 +1829,7 @@ __global__ __launch_bounds__(256) void k_emit(Work w, uint32_t* __restrict__ ids
   for (int k = 0; k < PER; k++) {
     const uint32_t j = tid + 256 * k;
     if (j >= np) break;
-    const uint32_t oj = s_off[j], cj = s_off[j + 1] - oj;
+    const uint32_t oj = s_off[so(j)], cj = s_off[so(j + 1)] - oj;
     const uint64_t dst = base + oj;
     if (cj > 0 && dst < ids_cap) ids[dst] = v0[k];
     for (uint32_t m = 1; m < cj; m += 4) {
@@ -1839,12 +1842,22 @@ __global__ __launch_bounds__(256) void k_emit(Work w, uint32_t* __restrict__ ids
         if (m + i < cj && dst + m + i < ids_cap) ids[dst + m + i] = x[i];  // the host reports CTOK_E_CAPACITY when short
     }
   }
-  __syncthreads();  // every record has been read: overwrite them with first ids
-  if (jb < np) {  // each piece's first id within the tile, for k_tokoff
-#pragma unroll
-    for (int k = 0; k < PER / 4; k++)
-      reinterpret_cast<uint4*>(tcnt + jb)[k] = make_uint4(pre[4 * k], pre[4 * k + 1], pre[4 * k + 2], pre[4 * k + 3]);
+  __syncthreads();  // every record has been read: doc-start pieces get their first id
+  if (tid < kTileWords) {  // lane = 64-byte word of the tile; its doc starts are piece starts
+    const uint32_t g = tile * kTileWords + tid;
+    if (2 * g < w.n_words) {
+      uint64_t m = (uint64_t)w.docbits[2 * g] | ((uint64_t)w.docbits[2 * g + 1] << 32);
+      const uint64_t P = (uint64_t)w.pbits[2 * g] | ((uint64_t)w.pbits[2 * g + 1] << 32);
+      const uint32_t j0 = w.wpref[(size_t)tile * 64 + tid];
+      while (m) {
+        const uint32_t b = (uint32_t)__builtin_ctzll(m);
+        m &= m - 1;
+        const uint32_t j = j0 + (uint32_t)__popcll(P & ((1ull << b) - 1));
+        tcnt[j] = s_off[so(j)];
+      }
+    }
   }
+  (void)pre;
 }
 
 // tok_off[d] = first id of the piece that starts at doc_off[d] (every non-empty doc starts a
