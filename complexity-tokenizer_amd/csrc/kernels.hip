@@ -320,24 +320,76 @@ __global__ __launch_bounds__(64 * kSegWaves) void k_segment(Work w, Tables t) {
   } else {
     s_text[(kTileWords + 1) * 16] = 0;
   }
-  if (m.NA) {  // non-ASCII code points: one class lookup per code point
+  if (m.NA) {  // non-ASCII code points: classes and NFC flags from the two-level tables
+    constexpr int kSegCp = 4;
     const uint32_t x0 = (uint32_t)(g * 64);
-    uint64_t todo = m.NA;
     bool nfc_bad = false;
-    while (todo) {
-      const uint32_t i = __builtin_ctzll(todo);
-      const uint32_t b0 = w.text[x0 + i];
-      const int cw = seg_cls_wide(w.text, B, x0 + i, t);
-      const int cl = cw & 3;
-      nfc_bad |= (cw & 4) != 0;
-      // a lead byte covers its continuation bytes within the word; a continuation byte at the
-      // start of the word (lead in the previous word) is classified on its own
-      const uint32_t len = (b0 & 0xC0) == 0x80 ? 1u : (uint32_t)u8len((uint8_t)b0);
-      const uint64_t bits = (len >= 64 - i ? ~0ull : ((1ull << len) - 1)) << i;
+    auto set_class = [&](int cl, uint64_t bits) {
       if (cl == 0) m.W |= bits & m.NA;
       else if (cl == 1) m.L |= bits & m.NA;
       else if (cl == 2) m.N |= bits & m.NA;
-      todo &= ~bits;
+    };
+    // continuation bytes (10xxxxxx), SWAR over the word's dwords
+    uint64_t cont = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k += 2) {
+      const uint32_t c0 = x[k] & ~(x[k] << 1) & seg::kHi, c1 = x[k + 1] & ~(x[k + 1] << 1) & seg::kHi;
+      cont |= (uint64_t)seg::pack8(c0, c1) << (4 * k);
+    }
+    cont &= m.NA;
+    const uint64_t lead_cont = cont & ~(cont + 1);  // continuation bytes at the start of the word
+    if (lead_cont) {  // a code point whose lead is in the previous word: classified on its own
+      const int cw = seg_cls_wide(w.text, B, x0, t);
+      nfc_bad |= (cw & 4) != 0;
+      set_class(cw & 3, lead_cont);
+    }
+    // every other code point starts at a lead byte in this word: decoded and looked up 8 at a
+    // time, so the byte loads, then both first-level table loads, then both second-level table
+    // loads of the 8 are in flight together (instead of a chain of dependent loads per code point)
+    uint64_t leads = m.NA & ~cont;
+    while (leads) {
+      uint32_t pos[kSegCp], cp[kSegCp], len[kSegCp];
+#pragma unroll
+      for (int k = 0; k < kSegCp; k++) {
+        pos[k] = leads ? (uint32_t)__builtin_ctzll(leads) : 64u;
+        leads &= leads ? leads - 1 : 0ull;
+      }
+#pragma unroll
+      for (int k = 0; k < kSegCp; k++) {
+        const uint32_t a = x0 + min(pos[k], 63u);
+        const uint32_t b0 = w.text[min(a, B - 1)];
+        const uint32_t b1 = w.text[min(a + 1, B - 1)] & 0x3Fu, b2 = w.text[min(a + 2, B - 1)] & 0x3Fu;
+        const uint32_t b3 = w.text[min(a + 3, B - 1)] & 0x3Fu;
+        const int l = u8len((uint8_t)b0);
+        len[k] = (uint32_t)l;
+        cp[k] = l == 2 ? ((b0 & 0x1Fu) << 6) | b1
+              : l == 3 ? ((b0 & 0x0Fu) << 12) | (b1 << 6) | b2
+              : l == 4 ? ((b0 & 0x07u) << 18) | (b1 << 12) | (b2 << 6) | b3 : b0;
+      }
+      uint32_t s1[kSegCp], n1[kSegCp];
+#pragma unroll
+      for (int k = 0; k < kSegCp; k++) {
+        const bool in = pos[k] < 64 && cp[k] < 0x110000;
+        s1[k] = in ? t.cls_s1[cp[k] >> 8] : 0u;
+        n1[k] = in ? t.nfc_s1[cp[k] >> 8] : 0u;
+      }
+#pragma unroll
+      for (int k = 0; k < kSegCp; k++) {
+        if (pos[k] >= 64) continue;
+        const uint32_t c = cp[k];
+        int cl = 3;
+        bool nf = false;
+        if (c < 0x80) {
+          cl = cls_ascii(c);
+        } else if (c < 0x110000) {
+          cl = (t.cls_s2[s1[k] * 64 + ((c & 255) >> 2)] >> ((c & 3) * 2)) & 3;
+          nf = t.nfc_s2[n1[k] * 256 + (c & 255)] != 0;
+        }
+        nfc_bad |= nf;
+        const uint32_t p = pos[k];
+        const uint64_t bits = (len[k] >= 64 - p ? ~0ull : ((1ull << len[k]) - 1)) << p;
+        set_class(cl, bits);
+      }
     }
     if (nfc_bad && w.nfc_watch) atomicOr(&w.counters[12], 1u);
   }
