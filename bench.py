@@ -152,12 +152,12 @@ def main():
     # Algorithmic bytes per launch (DESIGN.md "Measurement"):
     #   k_segment:      text read (B) + doc-start bitmap read (B/8) + piece-start bitmap written (B/8)
     #   merge passes:   text bytes of the pieces of their length classes + 4 B per id written
-    #                   (k_bpe_short: <= 16 B, k_bpe_mid: 17..64 B)
+    #                   (k_bpe_short: <= 16 B, k_bpe_mid: 17..32 B; 33..64 B run on the side stream)
     cb, ci = st["class_bytes"], st["class_ids"]
     kernels = {
         "k_segment": (avg("ms_segment"), 1.25 * B),
         "k_bpe_short": (avg("ms_bpe_lo"), cb[0] + cb[1] + 4 * (ci[0] + ci[1])),
-        "k_bpe_mid": (avg("ms_bpe_hi"), cb[2] + cb[3] + 4 * (ci[2] + ci[3])),
+        "k_bpe_mid": (avg("ms_bpe_hi"), cb[2] + 4 * ci[2]),
     }
     dom = max(kernels, key=lambda k: kernels[k][0])
     ms_dom, alg_dom = kernels[dom]

@@ -1104,7 +1104,7 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   w.scan_tmp_cap = ds->scan_tmp.cap * 2;
 
   // events (main stream s): 0 start | 7 segment start | 1 segment end | 2 <= 16 B merge pass end |
-  //   8, 9 around the 17..32 B pass | 5 side stream joined | 3 dropped-byte pass end | 6 emit end.
+  //   8, 10 around the 17..32 B pass | 9 after the 33..64 B pass (main instance) | 5 side stream joined | 3 dropped-byte pass end | 6 emit end.
   //   The side stream runs the long-piece pass, forked after k_segment (it reads only its output)
   //   and joined before the dropped-byte pass (fed by all merge passes) and k_emit.
   STEP("docstart", launch_docstart(w, s));
@@ -1119,6 +1119,8 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   if (timing) HIPTRY(hipEventRecord(ds->ev[2], s));
   if (timing) HIPTRY(hipEventRecord(ds->ev[8], s));
   STEP("bpe_mid", launch_bpe_class(w, tb, 2, s));
+  if (timing) HIPTRY(hipEventRecord(ds->ev[10], s));
+  STEP("bpe_c3", launch_bpe_class(w, tb, 4, s));
   if (timing) HIPTRY(hipEventRecord(ds->ev[9], s));
   HIPTRY(hipStreamWaitEvent(s, ds->ev_join, 0));
   if (timing) HIPTRY(hipEventRecord(ds->ev[5], s));
@@ -1162,8 +1164,8 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
       st->ms_pretok = el(0, 1);
       st->ms_segment = el(7, 1);
       st->ms_bpe_lo = el(1, 2);
-      st->ms_bpe_hi = el(8, 9);
-      st->ms_bpe_med = 0;  // classes 2 and 3 share k_bpe_mid (ms_bpe_hi)
+      st->ms_bpe_hi = el(8, 10);   // class 2
+      st->ms_bpe_med = el(10, 9);  // class 3, main-stream instance (the side instance overlaps)
       st->ms_bpe_short = el(1, 9);
       st->ms_bpe_long = el(9, 5);
       st->ms_emit = el(3, 6);

@@ -36,7 +36,8 @@ constexpr int kNumCounters = 32;
 // counters[] slots of class pass c: bytes merged / ids produced (statistics), next chunk
 __host__ __device__ constexpr int ctr_stat(int c) { return c < 3 ? 6 + 2 * c : 16; }
 __host__ __device__ constexpr int ctr_chunk(int c) { return c < 3 ? 13 + c : 18; }
-constexpr int kCtrAnyMid = 19;  // counters[19] != 0: some tile has a class-2 or class-3 piece
+constexpr int kCtrAnyMid = 19;  // counters[19] != 0: some tile has a class-2 piece
+constexpr int kCtrAnyC3 = 20;   // counters[20] != 0: some tile has a class-3 piece
 // List entry (u32): start within the tile [0,12), piece index within the tile [12,24), length [24,30).
 __host__ __device__ inline uint32_t list_entry(uint32_t sl, uint32_t j, uint32_t n) { return sl | (j << 12) | (n << 24); }
 
@@ -158,7 +159,7 @@ struct Work {              // device pointers, sized by the host for one call
   uint32_t* counters;      // [kNumCounters] [0] long count, [2] err, [3] nfc docs, [4] mid count,
                            // [5] pieces (stats), [ctr_stat(c)], [ctr_stat(c) + 1]: bytes merged /
                            // ids produced by class pass c (stats), [12] NFC speculation failed,
-                           // [ctr_chunk(c)] next chunk of class pass c, [kCtrAnyMid]
+                           // [ctr_chunk(c)] next chunk of class pass c, [kCtrAnyMid], [kCtrAnyC3]
   uint32_t* lw;            // long-piece workspace: 4 * n_bytes u32
   uint32_t* scan_tmp;      // scan partials
   uint64_t scan_tmp_cap;

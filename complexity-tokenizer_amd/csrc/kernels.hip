@@ -561,7 +561,8 @@ __global__ __launch_bounds__(64 * kSegWaves) void k_segment(Work w, Tables t) {
   }
   if (lane < kNumClasses)
     w.tcls[(size_t)lane * w.n_tiles + tile] = lane == 0 ? n0 : lane == 1 ? n1 : lane == 2 ? n2 : n3;
-  if (lane == 0 && (n2 | n3)) w.counters[kCtrAnyMid] = 1;  // plain store: every writer stores 1
+  if (lane == 0 && n2) w.counters[kCtrAnyMid] = 1;  // plain stores: every writer stores 1
+  if (lane == 0 && n3) w.counters[kCtrAnyC3] = 1;
 }
 
 hipError_t launch_segment(const Work& w, const Tables& t, hipStream_t s) {
@@ -1069,39 +1070,41 @@ __global__ __launch_bounds__(1024) void k_bpe_short(Work w, Tables t) {
   class_pass<16, COMPACT, true, 1024, kSortCap>(w, t, P, s_b2id, S, loaded, load);
 }
 
-// Pieces of 17..64 bytes (class 2, then class 3: e.g. runs of CJK letters, 3 bytes each) in one
-// kernel: 512-thread workgroups (two waves per SIMD at <= 256 VGPRs: 32 and 64 register slots
-// per thread) with the whole LDS image.  A workgroup moves on to class 3 when class 2 has no
-// chunk left, so the latency tail of the few long register pieces overlaps class-2 work.
-template <bool COMPACT>
+// Pieces of 17..32 bytes (CLS = 2, on the main stream after k_bpe_short) or 33..64 bytes (CLS = 3,
+// e.g. runs of CJK letters, 3 bytes each): 512-thread workgroups (two waves per SIMD at <= 256
+// VGPRs: 32 or 64 register slots per thread) with the whole LDS image.  One class per kernel:
+// the fully unrolled 64- and 32-slot loops together overflow the instruction cache.
+// Class 3 is launched twice, once on the side stream after the long-piece tiers and once on the
+// main stream after class 2; both instances take chunks from the same counter, so a handful of
+// class-3 pieces (long merge chains) is done by the side instance in the shadow of the main
+// stream's passes, and a large class 3 (multilingual text) is shared by both as CUs free up.
+template <bool COMPACT, int CLS>
 __global__ __launch_bounds__(512) void k_bpe_mid(Work w, Tables t) {
   extern __shared__ __attribute__((aligned(16))) uint4 s_img[];
   __shared__ int32_t s_b2id[256];
   __shared__ PassLds<kSortCap> S;
   // (the image is loaded up front: a lazy load pushes the 64-slot pass into scratch; the kernel
-  // returns at once when k_segment found no piece of either class)
-  if (w.counters[kCtrAnyMid] == 0) return;
+  // returns at once when k_segment found no piece of its class)
+  if (w.counters[CLS == 2 ? kCtrAnyMid : kCtrAnyC3] == 0) return;
+  if (CLS == 3 && __atomic_load_n(&w.counters[ctr_chunk(3)], __ATOMIC_RELAXED) * 64ull >= w.n_tiles) return;
   const uint32_t tid = threadIdx.x;
   for (uint32_t i = tid; i < kLdsImageBytes / 16; i += 512) s_img[i] = t.lds_image[i];
   for (uint32_t i = tid; i < 256; i += 512) s_b2id[i] = t.byte2id[i];
   bool loaded = true;
   const PairLds P{(const lds_u64*)s_img, (const lds_u32*)(s_img + kHotBuckets)};
-  // class 3 first: its pieces have the longest merge chains, so their latency tail overlaps the
-  // class-2 work of the other workgroups instead of ending the kernel
-  class_pass<64, COMPACT, true, 512, kSortCap>(w, t, P, s_b2id, S, loaded, [] {});
-  class_pass<32, COMPACT, true, 512, kSortCap>(w, t, P, s_b2id, S, loaded, [] {});
+  class_pass<CLS == 2 ? 32 : 64, COMPACT, true, 512, kSortCap>(w, t, P, s_b2id, S, loaded, [] {});
 }
 
-template <bool C>
+template <bool C, int CLS>
 static hipError_t launch_mid(const Work& w, const Tables& t, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
-    HIPCHK(hipFuncSetAttribute((const void*)k_bpe_mid<C>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    HIPCHK(hipFuncSetAttribute((const void*)k_bpe_mid<C, CLS>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)kLdsImageBytes));
     attr = true;
   }
   if (!w.n_tiles) return hipSuccess;
-  k_bpe_mid<C><<<min((w.n_tiles + 63) / 64, w.n_cus), 512, kLdsImageBytes, s>>>(w, t);
+  k_bpe_mid<C, CLS><<<min((w.n_tiles + 63) / 64, w.n_cus), 512, kLdsImageBytes, s>>>(w, t);
   return hipGetLastError();
 }
 
@@ -1125,7 +1128,8 @@ hipError_t launch_bpe_class(const Work& w, const Tables& t, int cls, hipStream_t
   }
   switch (cls) {
     case 0: return t.compact ? launch_short<true>(w, t, s) : launch_short<false>(w, t, s);  // classes 0 and 1
-    case 2: return t.compact ? launch_mid<true>(w, t, s) : launch_mid<false>(w, t, s);  // classes 2 and 3
+    case 2: return t.compact ? launch_mid<true, 2>(w, t, s) : launch_mid<false, 2>(w, t, s);
+    case 4: return t.compact ? launch_mid<true, 3>(w, t, s) : launch_mid<false, 3>(w, t, s);  // main-stream instance
     case 3:  // pieces with dropped bytes, found by the merge passes
       k_bpe_generic<true><<<64, 128, 0, s>>>(w, t);
       return hipGetLastError();
@@ -1807,7 +1811,9 @@ hipError_t launch_bpe_long(const Work& w, const Tables& t, hipStream_t s) {
     HIPCHK((launch_wave<64, 1024, 1, true, true>(w, t, w.n_cus, s)));
   }
   k_bpe_long<true><<<128, 256, 0, s>>>(w, t);
-  return hipGetLastError();
+  HIPCHK(hipGetLastError());
+  // 33..64 B register pass, side-stream instance (see k_bpe_mid)
+  return t.compact ? launch_mid<true, 3>(w, t, s) : launch_mid<false, 3>(w, t, s);
 }
 
 // ------------------------------------------------------------------------------------------

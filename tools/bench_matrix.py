@@ -150,7 +150,8 @@ def run_config(name, args, torch, dev):
                      "ms_device": round(statistics.median(devs), 3),
                      "MBps_device": round(n_bytes / (statistics.median(devs) * 1e-3) / 1e6, 1),
                      "ms_segment": round(st["ms_segment"], 4), "ms_bpe_short": round(st["ms_bpe_short"], 4),
-                     "ms_bpe_le16": round(st["ms_bpe_lo"], 4), "ms_bpe_17_64": round(st["ms_bpe_hi"], 4),
+                     "ms_bpe_le16": round(st["ms_bpe_lo"], 4), "ms_bpe_17_32": round(st["ms_bpe_hi"], 4),
+                     "ms_bpe_33_64_main": round(st["ms_bpe_med"], 4),
                      "class_bytes": st["class_bytes"],
                      "class_ids": st["class_ids"],
                      "ms_bpe_long": round(st["ms_bpe_long"], 4), "ms_emit": round(st["ms_emit"], 4),
