@@ -970,19 +970,48 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
       }
       __syncthreads();
     }
-    for (uint32_t i = tid; i < E; i += NT) {
+    // software pipeline over a thread's pieces i, i + NT, ...: the list entry is loaded two pieces
+    // ahead and the piece's text words one piece ahead, so the merges of one piece hide the two
+    // dependent global loads of the next
+    auto entry = [&](uint32_t i, uint32_t& kt) {
       const uint32_t q = sorted ? (uint32_t)S.perm[i] : i;
-      const uint32_t kt = tile_of<K>(S.pre, q);
+      kt = tile_of<K>(S.pre, q);
+      return list[(size_t)(c0 + kt) * LC::cap + (q - S.pre[kt])];
+    };
+    auto start_of = [&](uint32_t e, uint32_t kt) { return (c0 + kt) * kTile + (e & 0xFFFu); };
+    // (64 slots: no registers to spare, no pipeline)
+    constexpr bool kPf = N <= 32;
+    constexpr int kPw = kPf ? N / 4 : 1;
+    uint32_t e0 = 0, kt0 = 0, e1 = 0, kt1 = 0;
+    uint32_t wv0[kPw];
+    if (kPf && tid < E) {
+      e0 = entry(tid, kt0);
+      load_words<kPw>(w.text, start_of(e0, kt0), w.n_bytes, wv0);
+    }
+    if (kPf && tid + NT < E) e1 = entry(tid + NT, kt1);
+    for (uint32_t i = tid; i < E; i += NT) {
+      uint32_t e, kt;
+      uint32_t wv[N / 4];
+      if constexpr (kPf) {
+        e = e0;
+        kt = kt0;
+#pragma unroll
+        for (int k = 0; k < N / 4; k++) wv[k] = wv0[k];
+        e0 = e1;
+        kt0 = kt1;
+        if (i + NT < E) load_words<kPw>(w.text, start_of(e0, kt0), w.n_bytes, wv0);
+        if (i + 2 * NT < E) e1 = entry(i + 2 * NT, kt1);
+      } else {
+        e = entry(i, kt);
+        load_words<N / 4>(w.text, start_of(e, kt), w.n_bytes, wv);
+      }
       const uint32_t tile = c0 + kt;
-      const uint32_t e = list[(size_t)tile * LC::cap + (q - S.pre[kt])];
       const uint32_t s = tile * kTile + (e & 0xFFFu);
       const uint32_t j = (e >> 12) & 0xFFFu;
       const uint32_t n = e >> 24;
       uint32_t tk[N], rk[N];
       bool missing = false;
-      uint32_t wv[N / 4];
       {
-        load_words<N / 4>(w.text, s, w.n_bytes, wv);
 #pragma unroll
         for (int k = 0; k < N; k++) {
           const int32_t id = s_b2id[byte_of(wv[k >> 2], k)];
