@@ -1,14 +1,15 @@
 #!/bin/bash
 # A/B of two builds of libctok.so on the same GPU box: bench.py alternately with each library
 # (CTOK_LIB), three times each, printing throughput and the per-kernel times.
-#   usage: bash tools/ab.sh LIB_A LIB_B [bench args]
+#   usage: bash tools/ab.sh LIB_A[,VAR=VAL] LIB_B[,VAR=VAL] [bench args]
 set -e
 A=$1; B=$2; shift 2
 mkdir -p gpurun_out/ab
 for i in 1 2 3; do
   for v in A B; do
-    lib=$A; [ $v = B ] && lib=$B
-    CTOK_LIB=$lib timeout -k 10 120 python -u bench.py --no-cpu-baseline --no-parity --steps 30 "$@" \
+    spec=$A; [ $v = B ] && spec=$B
+    lib=${spec%%,*}; envs=""; [ "$spec" != "$lib" ] && envs=${spec#*,}
+    env CTOK_LIB=$lib $envs timeout -k 10 120 python -u bench.py --no-cpu-baseline --no-parity --steps 30 "$@" \
       > gpurun_out/ab/$v$i.json 2> gpurun_out/ab/$v$i.log
     python3 -c "
 import json,sys
