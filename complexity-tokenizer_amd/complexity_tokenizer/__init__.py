@@ -435,6 +435,38 @@ class Tokenizer:
         out["row_len"] = row_len[:rows].astype(np.int64)
         return out
 
+    def encode_offsets(self, texts):
+        """Per text: (ids, offsets, word_ids) of encode_single_to_encoding
+        (src/huggingface/mod.rs:395-480) -- ids from the GPU encode without the added-token
+        split, each token's approximate (start, end) byte range in its text and its word index,
+        placed by the C ABI's host walk (ctok_encode_offsets).  Raises PanicException where the
+        reference's text slicing panics."""
+        docs = _as_str_list(texts)
+        text, off = pack_texts(docs)
+        n = len(docs)
+        cap = max(int(off[-1]) + n, 1)
+        while True:
+            ids = np.empty(cap, dtype=np.uint32)
+            offs = np.empty(2 * cap, dtype=np.uint64)
+            wids = np.empty(cap, dtype=np.uint32)
+            tok_off = np.empty(n + 1, dtype=np.uint64)
+            ex = _n.Exec(self.device, None, 0)
+            rc = _n.lib.ctok_encode_offsets(self._h, text.ctypes.data, off.ctypes.data, n, ids.ctypes.data,
+                                            offs.ctypes.data, wids.ctypes.data, cap, tok_off.ctypes.data,
+                                            ctypes.byref(ex))
+            if rc == _n.CTOK_E_CAPACITY and int(tok_off[n]) > cap:
+                cap = int(tok_off[n])
+                continue
+            if rc != _n.CTOK_OK:
+                _raise(rc)
+            break
+        pairs = offs[: 2 * int(tok_off[n])].reshape(-1, 2).tolist()
+        res = []
+        for d in range(n):
+            a, b = int(tok_off[d]), int(tok_off[d + 1])
+            res.append((ids[a:b].tolist(), [tuple(x) for x in pairs[a:b]], wids[a:b].tolist()))
+        return res
+
     def _pp_items(self):
         """The post-processor as items (CTOK_PP_SEQUENCE = the ids), None without one."""
         n = ctypes.c_int64()
@@ -460,6 +492,10 @@ class Tokenizer:
         first_a = items.index(seq) if (items is not None and n_a) else 0
         ids2d, att, typ, spc, rl = (r["input_ids"], r["attention_mask"], r["token_type_ids"],
                                     r["special_tokens_mask"], r["row_len"])
+        offs_a = offs_b = None
+        if add_special_tokens:  # offsets / word ids of encode_single_to_encoding, per sequence
+            offs_a = self.encode_offsets(texts)
+            offs_b = self.encode_offsets(pairs) if pairs is not None else None
         encs = []
         was = gc.isenabled()
         gc.disable()
@@ -481,7 +517,15 @@ class Tokenizer:
                     # post-processor adds no tokens (mod.rs:378-386)
                     toks = [(self._tok_str(t) or "") for t in orig]
                     na = types[:n].count(0)
-                    encs.append(Encoding(ids, types, toks, att[i, :L].tolist(), spc[i, :L].tolist(), None, None,
+                    # offsets / word ids: the sequences' own, merged (encoding.rs:240-255); the
+                    # post-processor does not extend them (mod.rs:378-386)
+                    offs, wids = list(offs_a[i][1]), list(offs_a[i][2])
+                    if offs_b is not None:
+                        offs += offs_b[i][1]
+                        wids += offs_b[i][2]
+                    if len(offs) != n:
+                        raise RuntimeError("offsets: %d tokens for %d ids" % (len(offs), n))
+                    encs.append(Encoding(ids, types, toks, att[i, :L].tolist(), spc[i, :L].tolist(), offs, wids,
                                          [0] * na + [1] * (n - na)))
                 else:
                     toks = [t for t in (self._tok_str(x) for x in ids) if t is not None]

@@ -135,6 +135,7 @@ SIGS = {
     "ctok_pad_id": (ctypes.c_uint32, [_p]),
     "ctok_num_special_tokens_to_add": (_u64, [_p, ctypes.c_int]),
     "ctok_post_processor": (ctypes.c_int, [_p, _u32p, _u64, ctypes.POINTER(ctypes.c_int64)]),
+    "ctok_encode_offsets": (ctypes.c_int, [_p, _p, _p, _u64, _p, _p, _p, _u64, _p, ctypes.POINTER(Exec)]),
     "ctok_decode_batch": (ctypes.c_int, [_p, _p, _p, _u64, ctypes.c_uint32, _p, _u64, _p, ctypes.POINTER(Exec),
                                          ctypes.POINTER(DecodeStats)]),
     "ctok_decode_batch_device": (ctypes.c_int, [_p, _p, _p, _u64, _u64, ctypes.c_uint32, _p, _u64, _p, _u64p,

@@ -9,21 +9,22 @@ host-side list operations, restated from src/encoding.rs with the reference's qu
   * `pad` extends ids / type_ids / tokens / attention / special / sequence_ids, not offsets or
     word_ids (encoding.rs:87-131).
 
-`offsets` and `word_ids` of encode_to_encoding's encodings (approximate character offsets found
-by `str::find` of each pre-tokenized word, mod.rs:395-480) are not produced by the GPU path yet:
-reading them raises NotImplementedError rather than returning different values.  Encodings made
-by Encoding.from_ids have empty offsets / word_ids, as in the reference.
+`offsets` and `word_ids` of encode_to_encoding's encodings are the reference's approximate byte
+ranges (`str::find` of each pre-tokenized word, mod.rs:395-480), computed by ctok_encode_offsets
+from the GPU encode's pieces.  Encodings made by Encoding.from_ids have empty offsets / word_ids,
+as in the reference.  An Encoding built without them (offsets=None) raises NotImplementedError
+on access rather than returning different values.
 """
 from __future__ import annotations
 
 import numpy as np
 
-_UNKNOWN = None  # offsets / word_ids not produced (see the module docstring)
+_UNKNOWN = None  # offsets / word_ids not given (see the module docstring)
 
 
 def _need(v, what):
     if v is _UNKNOWN:
-        raise NotImplementedError("%s of encode_to_encoding results are not produced by the GPU path" % what)
+        raise NotImplementedError("%s were not computed for this Encoding" % what)
     return v
 
 

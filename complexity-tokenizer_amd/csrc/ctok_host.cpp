@@ -23,6 +23,7 @@
 #include <sstream>
 #include <thread>
 #include <string>
+#include <string_view>
 #include <unordered_map>
 #include <unordered_set>
 #include <vector>
@@ -217,6 +218,8 @@ struct DeviceState {
   DevBuf<uint32_t> doc_flag, ncp;
   DevBuf<uint64_t> norm_off;
   DevBuf<uint8_t> norm_text;
+  bool last_norm = false;  // the last encode ran on norm_text / norm_off (last_B bytes)
+  uint64_t last_B = 0;
   // decode: tables (uploaded on first use), workspace, events
   bool dec_ready = false;
   DevBuf<uint32_t> dec_ent;
@@ -1053,6 +1056,8 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
     B = nb;
   }
   if (B > 0 && ((uintptr_t)text & 15)) throw_err(CTOK_E_ARG, "device text buffer must be 16-byte aligned");
+  ds->last_norm = norm;
+  ds->last_B = B;
 
   Work w{};
   w.text = text;
@@ -1968,6 +1973,136 @@ int ctok_encode_padded(const ctok* tc, const uint8_t* utf8, const uint64_t* doc_
     }
     HIPTRY(hipStreamSynchronize(s));
     if (rc == CTOK_E_CAPACITY) throw_err(CTOK_E_CAPACITY, "cap too small: *width_out holds the row width needed");
+  });
+}
+
+// Offsets and word ids of encode_to_encoding (src/huggingface/mod.rs:395-480).  The ids and the
+// piece starts (the pre-tokenizer's words) come from the GPU encode; the walk that places each
+// word in the original text by str::find and each token inside its word is a sequential host
+// pass per document, as in the reference.  A word's ids are the ids whose token strings (one
+// char per non-dropped byte) add up to the word's non-dropped bytes.
+int ctok_encode_offsets(const ctok* tc, const uint8_t* utf8, const uint64_t* doc_off, uint64_t n_docs,
+                        uint32_t* ids, uint64_t* offsets, uint32_t* word_ids, uint64_t cap, uint64_t* tok_off,
+                        const ctok_exec* exec) {
+  if (!tc || !doc_off || !tok_off) return fail(CTOK_E_ARG, "null argument");
+  ctok* t = const_cast<ctok*>(tc);
+  return run([&] {
+    if (doc_off[0] != 0) throw_err(CTOK_E_ARG, "doc_off[0] must be 0");
+    for (uint64_t d = 0; d < n_docs; d++)
+      if (doc_off[d + 1] < doc_off[d]) throw_err(CTOK_E_ARG, "doc_off must be non-decreasing");
+    const uint64_t n_in = doc_off[n_docs];
+    if (n_in && !utf8) throw_err(CTOK_E_ARG, "null text");
+    const int dev = exec ? exec->device : 0;
+    DeviceState* ds = device_state(t, dev);
+    std::lock_guard<std::mutex> lk(ds->mu);
+    HIPTRY(hipSetDevice(dev));
+    hipStream_t s = exec && exec->stream ? (hipStream_t)exec->stream : ds->stream;
+    ds->pad_in_text.ensure(n_in + 16);
+    ds->pad_in_off.ensure(n_docs + 1);
+    if (n_in) HIPTRY(hipMemcpyAsync(ds->pad_in_text.p, utf8, n_in, hipMemcpyHostToDevice, s));
+    HIPTRY(hipMemsetAsync(ds->pad_in_text.p + n_in, 0, 16, s));
+    HIPTRY(hipMemcpyAsync(ds->pad_in_off.p, doc_off, (n_docs + 1) * 8, hipMemcpyHostToDevice, s));
+    ds->pad_ids.ensure(ctok_ids_bound(t, n_in, n_docs));
+    ds->pad_tokoff.ensure(n_docs + 1);
+    const uint64_t ntok = encode_device(t, ds, ds->pad_in_text.p, ds->pad_in_off.p, n_docs, n_in, ds->pad_ids.p,
+                                        ds->pad_ids.cap, ds->pad_tokoff.p, s, false, nullptr, false);
+    const uint64_t B = ds->last_B;
+    const bool norm = ds->last_norm;
+    std::vector<uint32_t> hid(ntok), pb((B + 31) / 32);
+    std::vector<uint64_t> toff(n_docs + 1), noff;
+    std::vector<uint8_t> ntext;
+    HIPTRY(hipMemcpyAsync(toff.data(), ds->pad_tokoff.p, (n_docs + 1) * 8, hipMemcpyDeviceToHost, s));
+    if (ntok) HIPTRY(hipMemcpyAsync(hid.data(), ds->pad_ids.p, ntok * 4, hipMemcpyDeviceToHost, s));
+    if (!pb.empty()) HIPTRY(hipMemcpyAsync(pb.data(), ds->pbits.p, pb.size() * 4, hipMemcpyDeviceToHost, s));
+    if (norm) {
+      ntext.resize(B + 1);
+      noff.resize(n_docs + 1);
+      if (B) HIPTRY(hipMemcpyAsync(ntext.data(), ds->norm_text.p, B, hipMemcpyDeviceToHost, s));
+      HIPTRY(hipMemcpyAsync(noff.data(), ds->norm_off.p, (n_docs + 1) * 8, hipMemcpyDeviceToHost, s));
+    }
+    HIPTRY(hipStreamSynchronize(s));
+    for (uint64_t d = 0; d <= n_docs; d++) tok_off[d] = toff[d];
+    if (ntok > cap) throw_err(CTOK_E_CAPACITY, "cap too small: tok_off[n_docs] holds the number of ids needed");
+    if (ntok && (!ids || !offsets || !word_ids)) throw_err(CTOK_E_ARG, "null output");
+    std::memcpy(ids, hid.data(), ntok * 4);
+    // bytes_to_unicode (src/pretokenizers.rs:130-153): the UTF-8 of each byte's char
+    std::string benc[256];
+    {
+      int n = 0;
+      for (int b = 0; b < 256; b++) {
+        const bool keep = (b >= 0x21 && b <= 0x7E) || (b >= 0xA1 && b <= 0xAC) || (b >= 0xAE && b <= 0xFF);
+        const std::vector<uint32_t> cp{keep ? (uint32_t)b : 256u + (uint32_t)n++};
+        benc[b] = encode_utf8(cp, 0, 1);
+      }
+    }
+    std::unordered_map<uint32_t, std::pair<uint32_t, uint32_t>> tlen;  // id -> (bytes, chars) of its token string
+    auto token_len = [&](uint32_t id) {
+      auto it = tlen.find(id);
+      if (it != tlen.end()) return it->second;
+      auto jt = t->id_to_token.find(id);
+      uint32_t nb = 0, nc = 0;
+      if (jt != t->id_to_token.end()) {
+        nb = (uint32_t)jt->second.size();
+        for (unsigned char c : jt->second) nc += (c & 0xC0) != 0x80;
+      }
+      return tlen.emplace(id, std::make_pair(nb, nc)).first->second;
+    };
+    auto is_start = [&](uint64_t g) { return (pb[g >> 5] >> (g & 31)) & 1u; };
+    std::string word;
+    for (uint64_t d = 0; d < n_docs; d++) {
+      const uint8_t* o = utf8 + doc_off[d];
+      const uint64_t olen = doc_off[d + 1] - doc_off[d];
+      const uint64_t g0 = norm ? noff[d] : doc_off[d], g1 = norm ? noff[d + 1] : doc_off[d + 1];
+      const uint8_t* nt = norm ? ntext.data() + g0 : o;
+      const std::string_view orig((const char*)o, olen);
+      uint64_t search = 0, k = toff[d], widx = 0;
+      for (uint64_t p = g0; p < g1;) {
+        uint64_t q = p + 1;
+        while (q < g1 && !is_start(q)) q++;
+        word.clear();
+        uint64_t kept = 0;  // bytes whose char is in the vocab (the others are dropped, src/bpe.rs:94-97)
+        for (uint64_t i = p; i < q; i++) {
+          const uint8_t b = nt[i - g0];
+          word += benc[b];
+          kept += t->byte2id[b] >= 0;
+        }
+        size_t lead = 0;  // trim_start_matches('Ġ' | '▁')
+        while (true) {
+          if (word.compare(lead, 2, "\xC4\xA0") == 0) lead += 2;
+          else if (word.compare(lead, 3, "\xE2\x96\x81") == 0) lead += 3;
+          else break;
+        }
+        const std::string_view find = lead < word.size() ? std::string_view(word).substr(lead) : std::string_view(word);
+        if (search < olen && (o[search] & 0xC0) == 0x80)
+          throw_err(CTOK_E_PANIC, "byte index " + std::to_string(search) +
+                                      " is not a char boundary (reference src/huggingface/mod.rs:464 slices the text there)");
+        const size_t pos = orig.substr(search).find(find);
+        uint64_t ws, we;
+        if (pos != std::string_view::npos) {
+          ws = search + pos;
+          we = ws + find.size();
+        } else {
+          ws = search;
+          we = std::min<uint64_t>(ws + word.size(), olen);
+        }
+        search = we;
+        uint64_t at = ws;
+        for (uint64_t got = 0; got < kept; k++) {
+          if (k >= toff[d + 1]) throw_err(CTOK_E_DEVICE, "offsets: ids and words disagree");
+          const auto L = token_len(hid[k]);
+          if (L.second == 0) throw_err(CTOK_E_UNSUPPORTED, "offsets: an id without a token string");
+          const uint64_t e = std::min<uint64_t>(at + L.first, we);
+          offsets[2 * k] = at;
+          offsets[2 * k + 1] = e;
+          word_ids[k] = (uint32_t)widx;
+          at = e;
+          got += L.second;
+        }
+        widx++;
+        p = q;
+      }
+      if (k != toff[d + 1]) throw_err(CTOK_E_DEVICE, "offsets: ids and words disagree");
+    }
   });
 }
 

@@ -215,6 +215,20 @@ int ctok_post_processor(const ctok* tok, uint32_t* items, uint64_t cap, int64_t*
 /* Tokenizer.num_special_tokens_to_add(is_pair)  src/bindings/tokenizer.rs:248-251 -> mod.rs:915-932 */
 uint64_t ctok_num_special_tokens_to_add(const ctok* tok, int is_pair);
 
+/* Offsets and word ids of encode_to_encoding, before the post-processor
+ * (encode_single_to_encoding + pre_tokenize_with_offsets, src/huggingface/mod.rs:395-480; replaces
+ * the per-text Encoding.offsets / Encoding.word_ids of src/bindings/encoding.rs).  Each document
+ * is encoded on the GPU without the added-token split (ids[tok_off[d] .. tok_off[d+1])); token k's
+ * byte range in its document is offsets[2k] .. offsets[2k+1] and word_ids[k] is the index of its
+ * pre-tokenized word.  The reference's approximations are kept (each word found with str::find
+ * from the previous word's end, falling back to the word's byte-level length; each token's range
+ * is its token string's byte length, clipped to the word).  A fallback that ends inside a UTF-8
+ * character makes the reference panic on the next word: CTOK_E_PANIC.  cap too small ->
+ * CTOK_E_CAPACITY with tok_off filled. */
+int ctok_encode_offsets(const ctok* tok, const uint8_t* utf8, const uint64_t* doc_off, uint64_t n_docs,
+                        uint32_t* ids, uint64_t* offsets, uint32_t* word_ids, uint64_t cap, uint64_t* tok_off,
+                        const ctok_exec* exec);
+
 /* Number of HIP devices visible to the library (0 when none; encode calls then fail with
  * CTOK_E_DEVICE -- there is no CPU fallback). */
 int ctok_device_count(void);

@@ -341,16 +341,46 @@ class RefTokenizer:
         return [self.decode_with_options(ids, skip_special_tokens, clean_up_tokenization_spaces) for ids in batch]
 
     # --------------------------------------------------------------------- Encoding path
-    def encode_single_to_encoding(self, text, type_id):
-        """src/huggingface/mod.rs:395-443 (ids only per word: no added-token split; offsets and
-        word ids are not restated -- the GPU path does not produce them)."""
-        words = self._pre_tokenize(self._normalize(text, self.normalizer), self.pre_tokenizer)
-        ids = []
+    @staticmethod
+    def words_with_offsets(words, original):
+        """pre_tokenize_with_offsets, src/huggingface/mod.rs:448-480, on UTF-8 bytes (Rust str
+        indices are byte offsets): each word, its leading 'Ġ' / '▁' trimmed, is searched for with
+        str::find from where the previous word ended; a miss falls back to the word's own byte
+        length, clipped to the text.  `&original[search_start..]` panics when search_start is not
+        a char boundary (a fallback end inside a multi-byte character)."""
+        o = original.encode("utf-8")
+        res, search = [], 0
         for w in words:
-            ids.extend(self.bpe(w))
+            trimmed = w.lstrip("\u0120\u2581")
+            find = (trimmed if trimmed else w).encode("utf-8")
+            if search < len(o) and 0x80 <= o[search] < 0xC0:
+                raise PanicException("byte index %d is not a char boundary" % search)
+            pos = o.find(find, search)
+            if pos >= 0:
+                start, end = pos, pos + len(find)
+            else:
+                start, end = search, min(search + len(w.encode("utf-8")), len(o))
+            res.append((w, start, end))
+            search = end
+        return res
+
+    def encode_single_to_encoding(self, text, type_id):
+        """src/huggingface/mod.rs:395-443 (ids per word: no added-token split), with the
+        approximate per-token offsets (token string byte length from the word's start, clipped to
+        the word's end) and word indices."""
+        words = self._pre_tokenize(self._normalize(text, self.normalizer), self.pre_tokenizer)
+        ids, offsets, word_ids = [], [], []
+        for wi, (w, ws, we) in enumerate(self.words_with_offsets(words, text)):
+            pos = ws
+            for i in self.bpe(w):
+                ids.append(i)
+                end = min(pos + len(self.id_to_token_map.get(i, "").encode("utf-8")), we)
+                offsets.append((pos, end))
+                pos = end
+                word_ids.append(wi)
         toks = [self.id_to_token_map.get(i, "") for i in ids]
         n = len(ids)
-        return RefEncoding(ids, [type_id] * n, toks, [1] * n, [0] * n, [type_id] * n)
+        return RefEncoding(ids, [type_id] * n, toks, [1] * n, [0] * n, [type_id] * n, offsets, word_ids)
 
     def encode_to_encoding(self, text, pair=None):
         """encode_to_encoding_impl, src/huggingface/mod.rs:358-392 (max_length None)."""
@@ -374,7 +404,7 @@ class RefTokenizer:
         def from_ids(ids):
             toks = [self.id_to_token_map[i] for i in ids if i in self.id_to_token_map]
             n = len(ids)
-            return RefEncoding(list(ids), [0] * n, toks, [1] * n, [0] * n, [0] * n)
+            return RefEncoding(list(ids), [0] * n, toks, [1] * n, [0] * n, [0] * n, [], [])
         enc = from_ids(self.encode(text))
         if pair is not None:
             enc.merge(from_ids(self.encode(pair)), 1)
@@ -625,17 +655,22 @@ def process_post(pp, ids):
 
 
 class RefEncoding:
-    """src/encoding.rs: the fields the GPU path produces (offsets / word ids left out)."""
+    """src/encoding.rs: the Encoding fields (word ids as plain ints: they are always Some here)."""
 
-    def __init__(self, ids, type_ids, tokens, attention_mask, special_tokens_mask, sequence_ids):
+    def __init__(self, ids, type_ids, tokens, attention_mask, special_tokens_mask, sequence_ids, offsets=None,
+                 word_ids=None):
         self.ids, self.type_ids, self.tokens = ids, type_ids, tokens
         self.attention_mask, self.special_tokens_mask, self.sequence_ids = attention_mask, special_tokens_mask, sequence_ids
+        self.offsets = list(offsets) if offsets is not None else []
+        self.word_ids = list(word_ids) if word_ids is not None else []
         self.overflowing = []
 
     def merge(self, other, type_id):  # encoding.rs:240-255
         n = len(other.ids)
         self.ids = self.ids + other.ids
         self.tokens = self.tokens + other.tokens
+        self.offsets = self.offsets + other.offsets
+        self.word_ids = self.word_ids + other.word_ids
         self.attention_mask = self.attention_mask + other.attention_mask
         self.special_tokens_mask = self.special_tokens_mask + other.special_tokens_mask
         self.type_ids = self.type_ids + [type_id] * n
@@ -667,7 +702,8 @@ class RefEncoding:
         return v[a:b]
 
     def _cut(self, m):
-        for f in ("ids", "type_ids", "tokens", "attention_mask", "special_tokens_mask", "sequence_ids"):
+        for f in ("ids", "type_ids", "tokens", "attention_mask", "special_tokens_mask", "sequence_ids", "offsets",
+                  "word_ids"):
             setattr(self, f, getattr(self, f)[:m])
 
     def truncate(self, m):  # encoding.rs:133-181
@@ -677,7 +713,9 @@ class RefEncoding:
         over = RefEncoding(r(self.ids, m, len(self.ids)), r(self.type_ids, m, len(self.type_ids)),
                            r(self.tokens, m, len(self.tokens)), r(self.attention_mask, m, len(self.attention_mask)),
                            r(self.special_tokens_mask, m, len(self.special_tokens_mask)),
-                           self.sequence_ids[m:] if len(self.sequence_ids) > m else [])
+                           self.sequence_ids[m:] if len(self.sequence_ids) > m else [],
+                           self.offsets[m:] if len(self.offsets) > m else [],
+                           self.word_ids[m:] if len(self.word_ids) > m else [])
         self.overflowing.append(over)
         self._cut(m)
 
@@ -688,14 +726,17 @@ class RefEncoding:
         while pos < len(self.ids):
             start = max(0, pos - stride)
             end = min(start + m, len(self.ids))
-            sq = self.sequence_ids[start:min(end, len(self.sequence_ids))] if len(self.sequence_ids) > start else []
+            def opt(v):
+                return v[start:min(end, len(v))] if len(v) > start else []
             self.overflowing.append(RefEncoding(r(self.ids, start, end), r(self.type_ids, start, end),
                                                 r(self.tokens, start, end), r(self.attention_mask, start, end),
-                                                r(self.special_tokens_mask, start, end), sq))
+                                                r(self.special_tokens_mask, start, end), opt(self.sequence_ids),
+                                                opt(self.offsets), opt(self.word_ids)))
             pos = end
         self._cut(m)
 
     def as_dict(self):
         return {"ids": self.ids, "type_ids": self.type_ids, "tokens": self.tokens,
                 "attention_mask": self.attention_mask, "special_tokens_mask": self.special_tokens_mask,
-                "sequence_ids": self.sequence_ids, "overflowing": [o.as_dict() for o in self.overflowing]}
+                "sequence_ids": self.sequence_ids, "offsets": [tuple(x) for x in self.offsets],
+                "word_ids": list(self.word_ids), "overflowing": [o.as_dict() for o in self.overflowing]}

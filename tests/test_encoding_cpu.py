@@ -105,3 +105,15 @@ def test_loader_post_processor(gpt2_path, kind, items, n_single):
     assert tok.model_max_length == 512
     ref = ref_py.RefTokenizer(obj)
     assert tok._pad_id_token()[0] == ref.pad_id_token()[0]
+
+
+def test_kat_words_with_offsets():
+    """pre_tokenize_with_offsets (src/huggingface/mod.rs:448-480) on hand-checked cases: find after
+    the leading 'Ġ' is trimmed, the byte-length fallback for words not in the text, the panic on a
+    fallback that ends inside a UTF-8 character."""
+    w = ref_py.RefTokenizer.words_with_offsets
+    assert [x[1:] for x in w(["hello", "\u0120world"], "hello world")] == [(0, 5), (6, 11)]
+    # '\n' -> 'Ċ' (2 bytes) is not in the text: start at the search point, end clipped
+    assert [x[1:] for x in w(["a", "\u010a", "b"], "a\nb")] == [(0, 1), (1, 3), (3, 3)]
+    with pytest.raises(ref_py.PanicException):
+        w(["\u00c3\u00a9", "\u00e2\u0082\u00ac"], "\u00e9\u20ac")

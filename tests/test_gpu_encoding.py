@@ -29,7 +29,7 @@ def pair_of(obj):
 def enc_dict(e):
     return {"ids": e.ids, "type_ids": e.type_ids, "tokens": e.tokens, "attention_mask": e.attention_mask,
             "special_tokens_mask": e.special_tokens_mask, "sequence_ids": e.sequence_ids,
-            "overflowing": [enc_dict(o) for o in e.overflowing]}
+            "offsets": e.offsets, "word_ids": e.word_ids, "overflowing": [enc_dict(o) for o in e.overflowing]}
 
 
 def same(got, want, what):
@@ -155,3 +155,59 @@ def test_special_mask_helpers(base):
     assert tok.get_special_tokens_mask(ids, already_has_special_tokens=False) == [0] * len(ids)
     arr = tok.encode_padded(["a b", "c"], padding="longest")
     assert arr["input_ids"].dtype == np.uint32 and arr["input_ids"].shape[0] == 2
+
+
+def _offset_texts():
+    """Texts for the offsets walk: the Encoding cases, whitespace runs (words whose byte-level form
+    is not in the text: the fallback), accents, CJK, emoji, and seeded random mixes."""
+    import random
+    out = encoding_cases.texts() + ["hello world\tfoo\nbar  baz", "  leading", "trailing   ", "a\n\n\nb",
+                                    "caf\u00e9 na\u00efve", "\u4f60\u597d\u4e16\u754c", "emoji \U0001F600 here",
+                                    "x\u00e9y", "\u00e9 x", "'s 're it's", "1,234.56 %"]
+    rng = random.Random(5)
+    alphabet = ["a", "b", " ", "  ", "\n", "\t", "\u00e9", "\u4e16", "\U0001F600", "1", "!", "'s", "\u20ac", "x y"]
+    out += ["".join(rng.choice(alphabet) for _ in range(rng.randrange(1, 12))) for _ in range(300)]
+    return out
+
+
+@pytest.mark.parametrize("variant", ["plain", "prefix_space", "nfc"])
+def test_offsets_and_word_ids(base, variant):
+    """ctok_encode_offsets vs the oracle's encode_single_to_encoding: ids, per-token byte ranges
+    and word indices equal, texts whose walk panics in the reference raise PanicException."""
+    obj = json.loads(json.dumps(base))
+    if variant == "prefix_space":
+        obj["pre_tokenizer"]["add_prefix_space"] = True
+    if variant == "nfc":
+        obj["normalizer"] = {"type": "NFC"}
+    tok, ref = pair_of(obj)
+    ok, bad = [], []
+    texts = _offset_texts() + (["e\u0301 x \u00e9\u0301", "A\u030a\u0301b", "n\u0303o"] if variant == "nfc" else [])
+    for t in texts:
+        try:
+            ok.append((t, ref.encode_single_to_encoding(t, 0)))
+        except ref_py.PanicException:
+            bad.append(t)
+    got = tok.encode_offsets([t for t, _ in ok])
+    for (t, want), (ids, offs, wids) in zip(ok, got):
+        assert ids == want.ids, repr(t)
+        assert offs == want.offsets, repr(t)
+        assert wids == want.word_ids, repr(t)
+    assert len(bad) > 0 or variant != "plain"  # the random mixes reach the reference's panic
+    for t in bad[:5]:
+        with pytest.raises(PanicException):
+            tok.encode_offsets([t])
+        with pytest.raises(PanicException):
+            tok.encode_to_encoding(t)
+
+
+def test_offsets_lookups(base):
+    """char / word lookups over the GPU offsets, as the reference computes them."""
+    tok, ref = pair_of(encoding_cases.with_post_processor(base, "bert"))
+    e = tok.encode_to_encoding("hello world foo")
+    w = ref.encode_to_encoding("hello world foo")
+    assert e.offsets == w.offsets and e.word_ids == w.word_ids
+    assert e.char_to_token(0) == 0 and e.token_to_word(0) == 0
+    assert e.word_to_tokens(1) is not None and e.n_words == 3
+    p = tok.encode_pair_to_encoding("ab cd", "ef")
+    q = ref.encode_to_encoding("ab cd", "ef")
+    assert p.offsets == q.offsets and p.word_ids == q.word_ids
