@@ -590,12 +590,22 @@ void build_decode_table(ctok* t) {
 }
 
 void load(ctok* t, const char* buf, size_t len) {
+  // CTOK_LOAD_TIMING=1: per-phase load times on stderr
+  const bool lt = getenv("CTOK_LOAD_TIMING") != nullptr;
+  auto lt0 = std::chrono::steady_clock::now();
+  auto lap = [&](const char* what) {
+    if (!lt) return;
+    const auto now = std::chrono::steady_clock::now();
+    fprintf(stderr, "[ctok load] %-12s %8.1f ms\n", what, std::chrono::duration<double, std::milli>(now - lt0).count());
+    lt0 = now;
+  };
   ctj::Value root;
   try {
     root = ctj::parse(buf, len);
   } catch (const ctj::ParseError& e) {
     throw_err(CTOK_E_PARSE, e.what());
   }
+  lap("json");
   if (root.kind != ctj::Value::Object) throw_err(CTOK_E_PARSE, "invalid type: expected struct TokenizerJson");
   const ctj::Value* model = root.get("model");
   if (!model) throw_err(CTOK_E_PARSE, "missing field `model`");
@@ -604,20 +614,21 @@ void load(ctok* t, const char* buf, size_t len) {
   if (!vocab) throw_err(CTOK_E_PARSE, "missing field `vocab`");
   if (vocab->kind != ctj::Value::Object) throw_err(CTOK_E_PARSE, "invalid type for `vocab`, expected a map");
   t->vocab.reserve(vocab->obj.size() * 2);
+  std::vector<const std::string*> first_keys;  // first occurrence of each key, in file order
+  first_keys.reserve(vocab->obj.size());
   for (const auto& m : vocab->obj) {
     if (!m.second.is_u32()) throw_err(CTOK_E_PARSE, "invalid value for vocab entry `" + m.first + "`, expected u32");
-    t->vocab[m.first] = (uint32_t)m.second.u;  // HashMap insert: a later duplicate key wins
+    auto ins = t->vocab.try_emplace(m.first, (uint32_t)m.second.u);
+    if (ins.second) first_keys.push_back(&m.first);
+    else ins.first->second = (uint32_t)m.second.u;  // HashMap insert: a later duplicate key wins
   }
   // Vocab::id_to_token (src/vocab.rs:47-52).  Several tokens sharing one id make the reference's
   // choice depend on HashMap order; here the later entry of the file wins (first occurrence of a
   // key, final value) -- parity for such files is unpinned.
-  {
-    std::unordered_set<std::string> seen;
-    seen.reserve(vocab->obj.size() * 2);
-    for (const auto& m : vocab->obj)
-      if (seen.insert(m.first).second) t->id_to_token[t->vocab[m.first]] = m.first;
-  }
+  t->id_to_token.reserve(first_keys.size() * 2);
+  for (const std::string* k : first_keys) t->id_to_token[t->vocab.find(*k)->second] = *k;
 
+  lap("vocab");
   // merges: deserialize_merges (mod.rs:56-101) then split(' ') == 2 parts (mod.rs:252-264)
   std::vector<std::pair<std::string, std::string>> merges;
   if (const ctj::Value* mv = model->get("merges")) {
@@ -647,6 +658,7 @@ void load(ctok* t, const char* buf, size_t len) {
     ranks[((uint64_t)ia->second << 32) | ib->second] = (uint32_t)r;
     valid_new.push_back(in->second);
   }
+  lap("ranks");
   if (merges.size() >= (size_t)kNoRank - 2) throw_err(CTOK_E_UNSUPPORTED, "more than 4M merges");
   t->rank_newid = valid_new;
   // compact table: values are the new ids themselves when new id is strictly increasing in rank
@@ -677,6 +689,7 @@ void load(ctok* t, const char* buf, size_t len) {
   }
   for (uint32_t id : valid_new)
     if (id > kMaxId) throw_err(CTOK_E_UNSUPPORTED, "token ids above 2^21-2 are not supported by the device merge table");
+  lap("merge_tab");
   // byte-level initial ids: vocab[bytes_to_unicode[b]] (src/bpe.rs:94-97), -1 = dropped
   std::vector<uint32_t> bm = byte_map();
   for (int b = 0; b < 256; b++) {
@@ -725,25 +738,23 @@ void load(ctok* t, const char* buf, size_t len) {
     }
     t->hot_entries = placed;
   }
+  lap("lds_image");
   // rank monotonicity ("proper"): every merge consuming z ranks after every merge producing z
   {
-    std::unordered_map<uint32_t, uint32_t> maxprod, mincons;
+    // per id (ids <= kMaxId, checked above): the latest rank producing it, the earliest consuming it
+    constexpr uint32_t kUnset = UINT32_MAX;
+    std::vector<uint32_t> maxprod(kMaxId + 2, kUnset), mincons(kMaxId + 2, kUnset);
     for (const auto& kv : ranks) {
       uint32_t r = kv.second;
       if (r >= valid_new.size()) continue;  // panics on lookup anyway
       uint32_t z = valid_new[r];
-      auto it = maxprod.find(z);
-      if (it == maxprod.end() || it->second < r) maxprod[z] = r;
-      for (uint32_t c : {(uint32_t)(kv.first >> 32), (uint32_t)kv.first}) {
-        auto jt = mincons.find(c);
-        if (jt == mincons.end() || jt->second > r) mincons[c] = r;
-      }
+      if (maxprod[z] == kUnset || maxprod[z] < r) maxprod[z] = r;
+      for (uint32_t c : {(uint32_t)(kv.first >> 32), (uint32_t)kv.first})
+        if (mincons[c] == kUnset || mincons[c] > r) mincons[c] = r;
     }
     t->proper = true;
-    for (const auto& kv : maxprod) {
-      auto jt = mincons.find(kv.first);
-      if (jt != mincons.end() && jt->second <= kv.second) { t->proper = false; break; }
-    }
+    for (size_t z = 0; z < maxprod.size(); z++)
+      if (maxprod[z] != kUnset && mincons[z] != kUnset && mincons[z] <= maxprod[z]) { t->proper = false; break; }
   }
 
 
@@ -759,44 +770,73 @@ void load(ctok* t, const char* buf, size_t len) {
       t->pair0[a * 256 + b] = t->compact ? (r < valid_new.size() ? valid_new[r] : kPanicVal) : r;
     }
 
+  lap("proper+pair0");
   // whole-piece table: every vocab entry of <= 8 raw bytes whose own BPE is that single token
   {
-    std::unordered_map<uint32_t, int> inv0;  // mapped code point -> byte
+    std::vector<int> inv0(0x144, -1);  // mapped code point (< U+0144) -> byte
     for (int b = 0; b < 256; b++) inv0[bm[b]] = b;
-    std::vector<std::pair<std::string, uint32_t>> ents;
-    std::vector<uint32_t> cps, tk;
-    for (const auto& kv : t->vocab) {
-      if (!decode_utf8(kv.first, cps) || cps.empty() || cps.size() > 8) continue;
-      std::string raw;
-      bool ok = true;
-      for (uint32_t c : cps) {
-        auto it = inv0.find(c);
-        if (it == inv0.end()) { ok = false; break; }
-        raw += (char)it->second;
+    // the merge table probed as the kernels probe it: value = rank, or (compact) the new id,
+    // both increasing in rank; kPanicVal / a rank past the valid merges would panic
+    auto tab_value = [&](uint32_t a, uint32_t b) -> uint64_t {
+      const uint64_t key = ((uint64_t)a << kIdBits) | b;
+      for (uint32_t h = mhash(a, b) & t->merge_mask;; h = (h + 1) & t->merge_mask) {
+        const uint64_t e = t->merge_tab[h];
+        if (e == kEmpty) return UINT64_MAX;
+        if ((e & ((1ull << 42) - 1)) == key) return e >> 42;
       }
-      if (!ok) continue;
-      // the reference merge loop (src/bpe.rs:88-153) on these bytes
-      tk.clear();
-      for (unsigned char c : raw) {
-        if (t->byte2id[c] < 0) { ok = false; break; }
-        tk.push_back((uint32_t)t->byte2id[c]);
-      }
-      if (!ok) continue;
-      for (;;) {
-        size_t bi = 0;
-        uint32_t best = UINT32_MAX;
-        for (size_t i = 0; i + 1 < tk.size(); i++) {
-          auto r = ranks.find(((uint64_t)tk[i] << 32) | tk[i + 1]);
-          if (r == ranks.end()) continue;
-          if (r->second >= valid_new.size()) { ok = false; break; }  // would panic: leave to the kernels
-          if (r->second < best) { best = r->second; bi = i; }
+    };
+    const uint64_t n_valid = valid_new.size();
+    auto panics = [&](uint64_t v) { return t->compact ? v == kPanicVal : v >= n_valid; };
+    std::vector<std::pair<const std::string*, uint32_t>> items;
+    items.reserve(t->vocab.size());
+    for (const auto& kv : t->vocab) items.push_back({&kv.first, kv.second});
+    // the reference merge loop (src/bpe.rs:88-153) on each entry's bytes, vocab split over threads
+    const unsigned nth = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<std::vector<std::pair<std::string, uint32_t>>> part(nth);
+    auto work = [&](unsigned w) {
+      std::vector<uint32_t> cps, tk;
+      for (size_t i = w; i < items.size(); i += nth) {
+        const std::string& key = *items[i].first;
+        if (!decode_utf8(key, cps) || cps.empty() || cps.size() > 8) continue;
+        std::string raw;
+        bool ok = true;
+        for (uint32_t c : cps) {
+          if (c >= inv0.size() || inv0[c] < 0) { ok = false; break; }
+          raw += (char)inv0[c];
         }
-        if (!ok || best == UINT32_MAX) break;
-        tk[bi] = valid_new[best];
-        tk.erase(tk.begin() + bi + 1);
+        if (!ok) continue;
+        tk.clear();
+        for (unsigned char c : raw) {
+          if (t->byte2id[c] < 0) { ok = false; break; }
+          tk.push_back((uint32_t)t->byte2id[c]);
+        }
+        if (!ok) continue;
+        for (;;) {
+          size_t bi = 0;
+          uint64_t best = UINT64_MAX;
+          for (size_t j = 0; j + 1 < tk.size(); j++) {
+            const uint64_t v = tab_value(tk[j], tk[j + 1]);
+            if (v == UINT64_MAX) continue;
+            if (panics(v)) { ok = false; break; }  // would panic: leave to the kernels
+            if (v < best) { best = v; bi = j; }
+          }
+          if (!ok || best == UINT64_MAX) break;
+          tk[bi] = t->compact ? (uint32_t)best : valid_new[best];
+          tk.erase(tk.begin() + bi + 1);
+        }
+        if (ok && tk.size() == 1 && tk[0] == items[i].second) part[w].push_back({raw, items[i].second});
       }
-      if (ok && tk.size() == 1 && tk[0] == kv.second) ents.push_back({raw, kv.second});
+    };
+    {
+      std::vector<std::thread> th;
+      for (unsigned w = 1; w < nth; w++) th.emplace_back(work, w);
+      work(0);
+      for (auto& x : th) x.join();
     }
+    std::vector<std::pair<std::string, uint32_t>> ents;
+    for (auto& p : part)
+      for (auto& e : p) ents.push_back(std::move(e));
+    std::sort(ents.begin(), ents.end(), [](const auto& x, const auto& y) { return x.second < y.second; });
     size_t pcap = 1024;
     while (pcap < ents.size() * 2 + 16) pcap <<= 1;
     t->piece_tab.assign((pcap + 1) * 4, 0);  // + one slot that stays empty (k_segment's no-probe lanes)
@@ -815,6 +855,7 @@ void load(ctok* t, const char* buf, size_t len) {
     if (getenv("CTOK_NO_PIECE_TABLE")) std::fill(t->piece_tab.begin(), t->piece_tab.end(), 0u);
   }
 
+  lap("piece_tab");
   // added tokens (mod.rs:103-116 schema, :274-305 maps)
   std::vector<std::pair<std::string, std::pair<uint32_t, uint8_t>>> added;  // content -> (id, flags)
   if (const ctj::Value* at = root.get("added_tokens")) {
@@ -879,6 +920,7 @@ void load(ctok* t, const char* buf, size_t len) {
   parse_post_processor(t, root.get("post_processor"));
   t->decoder = parse_decoder(root.get("decoder"), t->decoder_name);
   build_decode_table(t);
+  lap("rest");
 }
 
 template <typename T>
