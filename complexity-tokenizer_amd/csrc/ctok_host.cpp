@@ -677,7 +677,14 @@ void load(ctok* t, const char* buf, size_t len) {
   while (cap < ranks.size() * 2 + 16) cap <<= 1;
   t->merge_tab.assign(cap, kEmpty);
   t->merge_mask = (uint32_t)(cap - 1);
-  for (const auto& kv : ranks) {
+  // inserted in rank order: the low-rank (frequent) pairs sit in their home slots, so their
+  // lookups end at the first probe (the same reason the whole-piece table is filled in id order)
+  std::vector<std::pair<uint32_t, uint64_t>> by_rank_key;
+  by_rank_key.reserve(ranks.size());
+  for (const auto& kv : ranks) by_rank_key.push_back({kv.second, kv.first});
+  std::sort(by_rank_key.begin(), by_rank_key.end());
+  for (const auto& rk : by_rank_key) {
+    const std::pair<uint64_t, uint32_t> kv{rk.second, rk.first};
     uint32_t a = (uint32_t)(kv.first >> 32), b = (uint32_t)kv.first;
     if (a > kMaxId || b > kMaxId) throw_err(CTOK_E_UNSUPPORTED, "token ids above 2^21-2 are not supported by the device merge table");
     uint64_t val = kv.second;
@@ -836,6 +843,9 @@ void load(ctok* t, const char* buf, size_t len) {
     std::vector<std::pair<std::string, uint32_t>> ents;
     for (auto& p : part)
       for (auto& e : p) ents.push_back(std::move(e));
+    // id order (BPE ids grow with merge order, roughly inverse frequency): frequent pieces are
+    // inserted first and sit in their home slots -- k_segment's probes mostly end at the first
+    // slot (C2 k_segment 0.42 -> 0.32 ms against the hash-map order used before)
     std::sort(ents.begin(), ents.end(), [](const auto& x, const auto& y) { return x.second < y.second; });
     size_t pcap = 1024;
     while (pcap < ents.size() * 2 + 16) pcap <<= 1;

@@ -1115,7 +1115,7 @@ __global__ __launch_bounds__(512) void k_bpe_mid(Work w, Tables t) {
   // (the image is loaded up front: a lazy load pushes the 64-slot pass into scratch; the kernel
   // returns at once when k_segment found no piece of its class)
   if (w.counters[CLS == 2 ? kCtrAnyMid : kCtrAnyC3] == 0) return;
-  if (CLS == 3 && __atomic_load_n(&w.counters[ctr_chunk(3)], __ATOMIC_RELAXED) * 64ull >= w.n_tiles) return;
+  if (__atomic_load_n(&w.counters[ctr_chunk(CLS)], __ATOMIC_RELAXED) * 64ull >= w.n_tiles) return;
   const uint32_t tid = threadIdx.x;
   for (uint32_t i = tid; i < kLdsImageBytes / 16; i += 512) s_img[i] = t.lds_image[i];
   for (uint32_t i = tid; i < 256; i += 512) s_b2id[i] = t.byte2id[i];
