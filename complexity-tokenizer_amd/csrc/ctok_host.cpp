@@ -714,36 +714,45 @@ void load(ctok* t, const char* buf, size_t len) {
     std::vector<uint8_t> is_byte_tok(kMaxId + 2, 0);
     for (int b = 0; b < 256; b++)
       if (t->byte2id[b] >= 0 && (uint32_t)t->byte2id[b] <= kMaxId) is_byte_tok[t->byte2id[b]] = 1;
-    t->lds_image.assign(kLdsImageBytes / 8, 0);
+    // image = hot table | Bloom filter of the pairs not in the hot table (the merge passes ask
+    // the filter only after a hot-table miss), then, outside the image, the Bloom filter of all
+    // pairs for the kernels that load the filter alone (k_bpe_wave without HOT)
+    t->lds_image.assign(kLdsImageBytes / 8 + kBloomWords / 2, 0);
     uint64_t* hot = t->lds_image.data();
     std::fill(hot, hot + kHotU64, kEmpty);
     uint32_t* bloom = reinterpret_cast<uint32_t*>(hot + kHotU64);
+    uint32_t* bloom_all = reinterpret_cast<uint32_t*>(t->lds_image.data() + kLdsImageBytes / 8);
     std::vector<std::pair<uint32_t, uint64_t>> by_rank;  // (rank, entry)
     by_rank.reserve(ranks.size());
     for (uint64_t e : t->merge_tab) {
       if (e == kEmpty) continue;
       const uint32_t a = (uint32_t)((e >> kIdBits) & ((1u << kIdBits) - 1)), b = (uint32_t)(e & ((1u << kIdBits) - 1));
       if (is_byte_tok[a] && is_byte_tok[b]) continue;
-      const uint32_t h1 = mhash(a, b), h2 = mhash2(h1);
-      const uint32_t b1 = (h1 >> 12) & (kBloomBits - 1), b2 = (h2 >> 12) & (kBloomBits - 1);
-      bloom[b1 >> 5] |= 1u << (b1 & 31);
-      bloom[b2 >> 5] |= 1u << (b2 & 31);
-      const uint32_t r = ranks.at(((uint64_t)a << 32) | b);
-      if (r < valid_new.size()) by_rank.push_back({r, e});  // never cache an entry that panics
+      by_rank.push_back({ranks.at(((uint64_t)a << 32) | b), e});
     }
     std::sort(by_rank.begin(), by_rank.end());
     size_t placed = 0;
-    if (!getenv("CTOK_NO_HOT_TABLE")) {
-      for (const auto& re : by_rank) {
-        const uint64_t e = re.second;
-        const uint32_t a = (uint32_t)((e >> kIdBits) & ((1u << kIdBits) - 1)), b = (uint32_t)(e & ((1u << kIdBits) - 1));
-        const uint32_t c1 = mhash(a, b) & (kHotBuckets - 1), c2 = mhash2(mhash(a, b)) & (kHotBuckets - 1);
-        uint64_t* slot = nullptr;
-        for (uint32_t c : {c1, c2})
+    const bool use_hot = !getenv("CTOK_NO_HOT_TABLE");
+    for (const auto& re : by_rank) {
+      const uint64_t e = re.second;
+      const uint32_t a = (uint32_t)((e >> kIdBits) & ((1u << kIdBits) - 1)), b = (uint32_t)(e & ((1u << kIdBits) - 1));
+      const uint32_t h1 = mhash(a, b), h2 = mhash2(h1);
+      const uint32_t b1 = (h1 >> 12) & (kBloomBits - 1), b2 = (h2 >> 12) & (kBloomBits - 1);
+      bloom_all[b1 >> 5] |= 1u << (b1 & 31);
+      bloom_all[b2 >> 5] |= 1u << (b2 & 31);
+      uint64_t* slot = nullptr;
+      if (use_hot && re.first < valid_new.size()) {  // never cache an entry that panics
+        for (uint32_t c : {h1 & (kHotBuckets - 1), h2 & (kHotBuckets - 1)})
           for (int k = 0; k < 2 && !slot; k++)
             if (hot[2 * c + k] == kEmpty) slot = &hot[2 * c + k];
-        if (slot) { *slot = e; placed++; }
       }
+      if (slot) {
+        *slot = e;
+        placed++;
+        continue;  // a hot pair is found in the hot table before the filter is asked
+      }
+      bloom[b1 >> 5] |= 1u << (b1 & 31);
+      bloom[b2 >> 5] |= 1u << (b2 & 31);
     }
     t->hot_entries = placed;
   }

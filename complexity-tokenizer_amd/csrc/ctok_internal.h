@@ -76,9 +76,10 @@ __host__ __device__ inline uint32_t mhash2(uint32_t h1) {
 
 // LDS image for the merge passes (loaded once per workgroup): a hot table of the lowest-rank
 // mergeable pairs, kHotBuckets buckets of two merge-table entries, a pair in bucket
-// mhash & mask or mhash2 & mask; and a Bloom filter over every merge-table entry (bits
-// (mhash >> 12) and (mhash2 >> 12) mod kBloomBits).  A pair found in neither LDS structure goes
-// to the global table only when both Bloom bits are set.
+// mhash & mask or mhash2 & mask; and a Bloom filter over the merge-table entries that are not in
+// the hot table (bits (mhash >> 12) and (mhash2 >> 12) mod kBloomBits).  A pair found in neither
+// LDS structure goes to the global table only when both Bloom bits are set.  A second filter over
+// every entry follows the image in memory, for the kernels that load the filter alone.
 constexpr uint32_t kHotBuckets = 4096;                 // 64 KiB
 constexpr uint32_t kBloomBits = 1u << 18;              // 32 KiB
 constexpr uint32_t kHotU64 = 2 * kHotBuckets;
@@ -99,7 +100,8 @@ __host__ __device__ inline uint32_t piece_hash(uint32_t lo, uint32_t hi, uint32_
 struct Tables {            // device pointers, owned by the host runtime
   const uint64_t* merge_tab;
   uint32_t merge_mask;     // capacity - 1 (power of two)
-  const uint4* lds_image;  // hot table + Bloom filter (kLdsImageBytes), copied to LDS by the merge passes
+  const uint4* lds_image;  // hot table + Bloom filter (kLdsImageBytes), copied to LDS by the merge passes;
+                           // then the Bloom filter of all pairs (kBloomWords u32)
   const uint32_t* pair0;   // [256 * 256] merge-table value of the byte pair (a, b), kNoRank if none
   const uint4* piece_tab;  // whole-piece table (see piece_hash), piece_mask + 2 slots (the last stays empty)
   uint32_t piece_mask;

@@ -1776,7 +1776,9 @@ __global__ __launch_bounds__(64 * NW) void k_bpe_wave(Work w, Tables t) {
   }
   __syncthreads();
   if (s_any == 0) return;
-  const uint4* img = HOT ? t.lds_image : t.lds_image + kHotBuckets;
+  // (HOT: hot table + the filter of the other pairs; else the filter of all pairs, stored after
+  // the image)
+  const uint4* img = HOT ? t.lds_image : t.lds_image + kLdsImageBytes / 16;
   for (uint32_t i = tid; i < kImg; i += 64 * NW) s_dyn[i] = img[i];
   for (uint32_t i = tid; i < 256; i += 64 * NW) s_b2id[i] = t.byte2id[i];
   __syncthreads();
