@@ -15,6 +15,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstring>
+#include <exception>
 #include <fstream>
 #include <functional>
 #include <map>
@@ -2098,6 +2099,9 @@ int ctok_encode_offsets(const ctok* tc, const uint8_t* utf8, const uint64_t* doc
         benc[b] = encode_utf8(cp, 0, 1);
       }
     }
+    auto is_start = [&](uint64_t g) { return (pb[g >> 5] >> (g & 31)) & 1u; };
+    // documents are independent: contiguous ranges over host threads, each with its own cache
+    auto walk = [&](uint64_t d_begin, uint64_t d_end) {
     std::unordered_map<uint32_t, std::pair<uint32_t, uint32_t>> tlen;  // id -> (bytes, chars) of its token string
     auto token_len = [&](uint32_t id) {
       auto it = tlen.find(id);
@@ -2110,9 +2114,8 @@ int ctok_encode_offsets(const ctok* tc, const uint8_t* utf8, const uint64_t* doc
       }
       return tlen.emplace(id, std::make_pair(nb, nc)).first->second;
     };
-    auto is_start = [&](uint64_t g) { return (pb[g >> 5] >> (g & 31)) & 1u; };
     std::string word;
-    for (uint64_t d = 0; d < n_docs; d++) {
+    for (uint64_t d = d_begin; d < d_end; d++) {
       const uint8_t* o = utf8 + doc_off[d];
       const uint64_t olen = doc_off[d + 1] - doc_off[d];
       const uint64_t g0 = norm ? noff[d] : doc_off[d], g1 = norm ? noff[d + 1] : doc_off[d + 1];
@@ -2166,6 +2169,25 @@ int ctok_encode_offsets(const ctok* tc, const uint8_t* utf8, const uint64_t* doc
       }
       if (k != toff[d + 1]) throw_err(CTOK_E_DEVICE, "offsets: ids and words disagree");
     }
+    };
+    const unsigned nth = n_docs < 256 ? 1u : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<std::exception_ptr> errs(nth);
+    std::vector<std::thread> th;
+    for (unsigned w = 0; w < nth; w++) {
+      const uint64_t a = n_docs * w / nth, b = n_docs * (w + 1) / nth;
+      auto job = [&, w, a, b] {
+        try {
+          walk(a, b);
+        } catch (...) {
+          errs[w] = std::current_exception();
+        }
+      };
+      if (w + 1 < nth) th.emplace_back(job);
+      else job();
+    }
+    for (auto& x : th) x.join();
+    for (auto& e : errs)  // the error of the lowest document range
+      if (e) std::rethrow_exception(e);
   });
 }
 
