@@ -249,6 +249,10 @@ class Tokenizer:
             out[buf.raw[:n.value].decode("utf-8")] = int(tid.value)
         return out
 
+    def num_piece_added_tokens(self) -> int:
+        """Extension (diagnostic): added tokens the GPU split runs on (include/ctok.h)."""
+        return int(_n.lib.ctok_num_piece_added_tokens(self._h))
+
     # ------------------------------------------------------------------ encode
     def encode_packed(self, text: np.ndarray, off: np.ndarray, timing: bool = False):
         """Extension: encode a packed batch (uint8 UTF-8 buffer, uint64 offsets[D+1]) and return

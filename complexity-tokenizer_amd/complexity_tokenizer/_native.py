@@ -123,6 +123,8 @@ SIGS = {
     "ctok_num_special_tokens": (_u64, [_p]),
     "ctok_special_token": (ctypes.c_int, [_p, _u64, ctypes.c_char_p, _sz, ctypes.POINTER(_sz), _u32p]),
     "ctok_ids_bound": (_u64, [_p, _u64, _u64]),
+    "ctok_num_piece_added_tokens": (_u64, [_p]),
+    "ctok_piece_can_contain": (ctypes.c_int, [ctypes.c_char_p, _sz]),
     "ctok_encode_batch": (ctypes.c_int, [_p, _p, _p, _u64, _p, _u64, _p, ctypes.POINTER(Exec), ctypes.POINTER(Stats)]),
     "ctok_encode_batch_device": (ctypes.c_int, [_p, _p, _p, _u64, _u64, _p, _u64, _p, _u64p, ctypes.POINTER(Exec),
                                                 ctypes.POINTER(Stats)]),

@@ -1617,6 +1617,13 @@ int ctok_special_token(const ctok* t, uint64_t i, char* buf, size_t cap, size_t*
   return CTOK_OK;
 }
 
+uint64_t ctok_num_piece_added_tokens(const ctok* t) { return t ? t->at_id.size() : 0; }
+
+int ctok_piece_can_contain(const uint8_t* raw, size_t len) {
+  if (!raw && len) return fail(CTOK_E_ARG, "null argument");
+  return can_occur_in_piece(std::string((const char*)raw, len)) ? 1 : 0;
+}
+
 uint64_t ctok_ids_bound(const ctok*, uint64_t n_bytes, uint64_t n_docs) { return 3 * n_bytes + n_docs + 16; }
 
 int ctok_device_count(void) {

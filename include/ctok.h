@@ -58,6 +58,17 @@ int ctok_id_to_token(const ctok* tok, uint32_t id, char* buf, size_t cap, size_t
 uint64_t ctok_num_special_tokens(const ctok* tok);
 int ctok_special_token(const ctok* tok, uint64_t i, char* buf, size_t cap, size_t* len, uint32_t* id);
 
+/* Diagnostics of the added-token split (src/huggingface/mod.rs:566-675).  The reference tries
+ * every added token on every pre-tokenized word; tokens that provably never occur inside one
+ * GPT2_PATTERN piece (e.g. "<|endoftext|>", which the regex always cuts apart) cannot change
+ * the result and are left out of the device tables at load.
+ *   ctok_num_piece_added_tokens: how many added tokens the encode kernels split on (0 = the
+ *     fast paths without the split run);
+ *   ctok_piece_can_contain: 1 if the raw byte string can occur inside one piece (the load-time
+ *     predicate; conservative: 1 unless provably impossible), 0 if not, < 0 on error. */
+uint64_t ctok_num_piece_added_tokens(const ctok* tok);
+int ctok_piece_can_contain(const uint8_t* raw, size_t len);
+
 /* Execution / measurement options for one encode call. */
 typedef struct ctok_exec {
   int device;       /* HIP device ordinal the work runs on                              */
@@ -86,10 +97,10 @@ typedef struct ctok_stats {
   uint64_t docs, pieces, long_pieces, tokens, nfc_docs;
   double ms_segment;      /* k_segment alone: piece starts + whole-piece probes/routing */
   double ms_bpe_lo;       /* k_bpe_short: pieces of <= 16 bytes (classes 0 and 1)        */
-  double ms_bpe_hi;       /* k_bpe_mid: pieces of 17..64 bytes                           */
+  double ms_bpe_hi;       /* k_bpe_mid<2>: pieces of 17..32 bytes                        */
   uint64_t class_bytes[4];  /* text bytes merged per length class (<= 8, 9..16, 17..32, 33..64 B) */
   uint64_t class_ids[4];    /* ids produced per length class                             */
-  double ms_bpe_med;      /* reserved (0): classes 2 and 3 share k_bpe_mid               */
+  double ms_bpe_med;      /* k_bpe_mid<3>, main-stream instance: pieces of 33..64 bytes    */
 } ctok_stats;
 
 /* Upper bound on the ids of a batch whose docs total `n_bytes` bytes (ids <= 3*bytes + docs:
