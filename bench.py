@@ -2,20 +2,33 @@
 """Benchmark: MB/s of raw UTF-8 encoded by the MI355X batch ByteLevel-BPE encode path.
 
 Metric (BASELINE.json): "MB/s raw UTF-8 encoded (encode_batch), 50k ByteLevel BPE, 1/2/4/8 MI355X".
-Workload per GPU = config C2 (BASELINE.json configs[1]): 1,000,000 synthetic English-like ASCII
-docs of 96-160 bytes (~128 MB), GPT-2-shaped 50,257-token ByteLevel BPE (synthetic merges, no
-network).  A step = one `ctok_encode_batch_device` call over the whole batch, inputs already
-resident in HBM (pre-tokenize + routing, BPE merge passes, id emission + token offsets, ending
-with the host reading the token count).  N > 1: one process per GPU (torch.distributed.run), every rank encodes its own
-1M-doc shard (seed 2 + 1000*rank): weak scaling, no data-path collective (gloo only for the
-barrier and the max-over-ranks timing).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--cpu-seconds S]
+Workload (default, --config c4): BASELINE.json configs[3], the config the 1/2/4/8 curve is quoted
+on -- 10,000,000 synthetic English-like ASCII docs of 96-160 B (1.28 GB, the C2 generator in
+independent 1M-doc blocks, datagen/corpus.py), GPT-2-shaped 50,257-token ByteLevel BPE
+(synthetic merges, no network).  The batch is cut into N contiguous byte-balanced doc shards
+(complexity_tokenizer.parallel.shard_bounds), one per GPU: strong scaling, no data-path
+collective (gloo only for the barrier, the max-over-ranks time and the parity vote).  At N = 1
+the whole 1.28 GB is one call on one GPU.  --config c2 runs configs[1] instead (1M docs per GPU,
+weak scaling).
+
+A step = one `ctok_encode_batch_device` call over the rank's shard with its inputs already
+resident in HBM (pre-tokenize + routing, BPE merge passes, id emission + token offsets, ending
+with the host reading the token count).  `value` = bytes of all shards x steps / max-over-ranks
+wall time of the K timed steps.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4|c2] [--cpu-seconds S]
+
+With --gpus N > 1 and no WORLD_SIZE in the environment, N child processes (one per GPU) are
+started before anything touches the GPU; under torch.distributed.run the ranks come from
+RANK / LOCAL_RANK / WORLD_SIZE.
 """
 import argparse
 import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -39,27 +52,104 @@ def digest(ids, tok_off):
     return h.hexdigest()
 
 
-def cpu_baseline(tok_path, text, off, seconds, threads):
-    """The reference's algorithm as a faithful C port (oracle/ctok_ref.c) on the host cores,
-    on a bounded sample (the first docs of this rank's batch)."""
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def cpu_share():
+    """CPUs the cgroup lets this process use (cpu.max quota), or None when unlimited."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+        return None if q == "max" else round(int(q) / int(p), 2)
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline(tok_path, text, off, seconds):
+    """The reference's algorithm as a faithful C port (oracle/ctok_ref.c) on the host cores, on
+    a bounded sample (the first docs of this rank's shard): rayon's default thread count (every
+    CPU of the affinity mask, reference src/huggingface/mod.rs:695) and one thread."""
     from oracle import ref_c
     rc = ref_c.RefC.from_file(tok_path)
+    # rayon's default pool size is std::thread::available_parallelism(): the affinity mask,
+    # capped by the cgroup v2 CPU quota on Linux
+    threads = len(os.sched_getaffinity(0))
+    quota = cpu_share()
+    if quota:
+        threads = max(1, min(threads, int(quota)))
     n_docs = len(off) - 1
-    n0 = min(20_000, n_docs)
+
+    def timed(n, th):
+        t = time.perf_counter()
+        rc.encode_packed(text[: int(off[n])], off[: n + 1], th)
+        return int(off[n]) / max(time.perf_counter() - t, 1e-9)
+
+    def sized(rate, secs):  # docs for about `secs` of work at `rate` bytes/s
+        return max(1000, min(n_docs, int(np.searchsorted(off.astype(np.int64), int(rate * secs)))))
+
+    r1 = timed(min(2000, n_docs), 1)
+    n1 = sized(r1, 0.25 * seconds)
+    r1 = timed(n1, 1)
+    rn = timed(min(20_000, n_docs), threads)
+    nn = sized(rn, 0.75 * seconds)
     t = time.perf_counter()
-    rc.encode_packed(text[: int(off[n0])], off[: n0 + 1], threads)
-    rate = int(off[n0]) / max(time.perf_counter() - t, 1e-9)  # bytes/s
-    n = n_docs
-    if int(off[-1]) / rate > seconds:
-        n = int(np.searchsorted(off.astype(np.int64), int(rate * seconds)))
-        n = max(n0, min(n, n_docs))
-    t = time.perf_counter()
-    rc.encode_packed(text[: int(off[n])], off[: n + 1], threads)
+    rc.encode_packed(text[: int(off[nn])], off[: nn + 1], threads)
     dt = time.perf_counter() - t
-    return {"value": round(int(off[n]) / dt / 1e6, 3), "unit": "MB/s", "cores": threads, "kind": "port",
-            "sample": "first %d docs (%.1f MB) of the rank-0 C2 batch, %.1f s, oracle/ctok_ref.c (faithful C "
+    return {"value": round(int(off[nn]) / dt / 1e6, 3), "unit": "MB/s", "cores": threads, "kind": "port",
+            "value_1thread": round(r1 / 1e6, 3), "cpu_model": cpu_model(), "cgroup_cpus": cpu_share(),
+            "sample": "first %d docs (%.1f MB) of the rank-0 shard, %.1f s on %d threads (rayon default: every CPU "
+                      "of the affinity mask, capped by the cgroup CPU quota); 1-thread figure on the first %d docs; oracle/ctok_ref.c (faithful C "
                       "restatement of the Rust reference: per-doc NFC + byte-map rebuild, O(n^2) merge rescans, "
-                      "rayon-like doc threads)" % (n, int(off[n]) / 1e6, dt)}
+                      "rayon-like doc threads)" % (nn, int(off[nn]) / 1e6, dt, threads, n1)}
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n):
+    """One child per GPU (RANK / LOCAL_RANK / WORLD_SIZE set), started before any GPU call in
+    this process; returns the worst exit status."""
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    return next((c for c in rcs if c != 0), 0)
+
+
+def workload(args, rank, world):
+    """(text, off, description dict) of this rank's shard."""
+    from datagen import corpus
+    from complexity_tokenizer.parallel import shard_bounds
+    if args.config == "c2":
+        n = args.docs or 1_000_000
+        text, off = corpus.corpus_c2(n, seed=2 + 1000 * rank)
+        return text, off, {"workload": "C2: %d docs x 96-160 B ASCII per GPU, GPT-2-shaped 50,257-token ByteLevel "
+                                       "BPE (weak scaling)" % n, "docs_total": n * world}, None
+    n = args.docs or corpus.C4_DOCS
+    full = corpus.c4_offsets(n)
+    d0, d1 = shard_bounds(full, world, rank)
+    cpus = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
+    text, off = corpus.corpus_c4_range(d0, d1, n, workers=max(1, min(8, cpus // world)))
+    desc = {"workload": "C4: %d docs x 96-160 B ASCII (%.2f GB), GPT-2-shaped 50,257-token ByteLevel BPE, "
+                        "byte-balanced doc shards over %d GPU(s)" % (n, int(full[-1]) / 1e9, world),
+            "docs_total": n, "bytes_total": int(full[-1])}
+    return text, off, desc, ("%d/%d" % (rank, world), d0, d1, n)
 
 
 def main():
@@ -67,33 +157,44 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--docs", type=int, default=1_000_000)
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--config", choices=["c4", "c2"], default="c4")
+    ap.add_argument("--docs", type=int, default=0, help="override the doc count (tests; parity needs the default)")
+    ap.add_argument("--cpu-seconds", type=float, default=16.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     args = ap.parse_args()
 
-    import torch
-    rank = int(os.environ.get("RANK", "0"))
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        log("[bench] --gpus %d but WORLD_SIZE=%d: run one process per GPU (torch.distributed.run "
+            "--nproc-per-node %d) or let bench.py start them" % (args.gpus, world, args.gpus))
+        sys.exit(2)
+    rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
     dist = None
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group(backend="gloo")
 
     from complexity_tokenizer import Tokenizer
-    from datagen import corpus
     from datagen.build_tokenizers import fixture_path
 
     tmp = os.path.join("/tmp", "ctok_bench_%d" % os.getpid())
     os.makedirs(tmp, exist_ok=True)
     tok_path = fixture_path("gpt2_50k", tmp)
     t0 = time.time()
-    text, off = corpus.corpus_c2(args.docs, seed=2 + 1000 * rank)
+    text, off, desc, shard = workload(args, rank, world)
     n_docs, n_bytes = len(off) - 1, int(off[-1])
-    log("[bench] rank %d: corpus %d docs %.1f MB in %.1fs" % (rank, n_docs, n_bytes / 1e6, time.time() - t0))
+    log("[bench] rank %d: shard %d docs %.1f MB built in %.1fs" % (rank, n_docs, n_bytes / 1e6, time.time() - t0))
 
+    n_dev = max(1, torch.cuda.device_count())
+    if local >= n_dev:  # a rehearsal of N ranks on fewer GPUs: ranks share devices
+        log("[bench] rank %d: LOCAL_RANK %d >= %d visible GPU(s), sharing device %d" % (rank, local, n_dev, local % n_dev))
+    local = local % n_dev
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     tok = Tokenizer.from_file(tok_path)
@@ -112,15 +213,36 @@ def main():
     for _ in range(args.warmup):
         ntok = step(False)
 
-    parity = None
-    if rank == 0 and not args.no_parity and args.docs == 1_000_000:
-        gold = json.load(open(os.path.join(ROOT, "tests", "golden", "digests.json"))).get("C2")
-        ids = d_ids[:ntok].cpu().numpy().view(np.uint32)
-        toff = d_tok_off.cpu().numpy().view(np.uint64)
-        ok = gold is not None and digest(ids, toff) == gold["sha256"]
-        parity = ("bit-exact: sha256(tok_off, ids) of all %d docs == C-oracle golden (tests/golden/digests.json)"
-                  % n_docs) if ok else "MISMATCH vs golden digest"
-        log("[bench] parity:", parity)
+    # parity (outside the timed region): this rank's (tok_off, ids) against the C-oracle digest
+    # of its shard (tests/golden/digests.json), one vote per rank
+    parity, bad = None, 0
+    if not args.no_parity:
+        gold = json.load(open(os.path.join(ROOT, "tests", "golden", "digests.json")))
+        want = None
+        if args.config == "c4" and shard[3] == gold["C4"]["docs"]:
+            want = gold["C4"]["shards"].get(shard[0], {}).get("sha256")
+        elif args.config == "c2" and rank == 0 and n_docs == gold["C2"]["docs"]:
+            want = gold["C2"]["sha256"]
+        if want is not None:
+            ids = d_ids[:ntok].cpu().numpy().view(np.uint32)
+            toff = d_tok_off.cpu().numpy().view(np.uint64)
+            bad = 0 if digest(ids, toff) == want else 1
+            del ids, toff
+        else:
+            bad = -1  # no golden digest for this shape
+    votes = torch.tensor([1.0 if bad == 0 else 0.0, 1.0 if bad == 1 else 0.0], dtype=torch.float64)
+    if dist:
+        dist.all_reduce(votes, op=dist.ReduceOp.SUM)
+    if not args.no_parity:
+        if votes[1] > 0:
+            parity = "MISMATCH vs golden digest on %d of %d rank(s)" % (int(votes[1]), world)
+        elif votes[0] == world:
+            parity = ("bit-exact: sha256(tok_off, ids) of every rank's shard == C-oracle golden "
+                      "(tests/golden/digests.json, %s)" % ("C4 shards of %d" % world if args.config == "c4" else "C2"))
+        else:
+            parity = "unchecked on %d rank(s): no golden digest for this shape" % (world - int(votes[0]))
+        if rank == 0:
+            log("[bench] parity:", parity)
 
     # timed region: K steps bracketed by barrier + synchronize
     if dist:
@@ -149,15 +271,16 @@ def main():
     st = stats[-1]
     P, T, B, D = st["pieces"], st["tokens"], st["bytes_norm"], st["docs"]
     # Per-kernel rooflines (HIP events on the encode stream, averaged over the timed steps).
-    # Algorithmic bytes per launch (DESIGN.md "Measurement"):
+    # Algorithmic bytes per launch:
     #   k_segment:      text read (B) + doc-start bitmap read (B/8) + piece-start bitmap written (B/8)
-    #   merge passes:   text bytes of the pieces of their length classes + 4 B per id written
-    #                   (k_bpe_short: <= 16 B, k_bpe_mid: 17..32 B; 33..64 B run on the side stream)
+    #   k_bpe_short:    text bytes of the <= 16 B pieces left to merge + 4 B per id written
+    #   k_bpe_mid<2>:   the same for the 17..32 B pieces (33..64 B: k_bpe_mid<3>, main + side stream)
     cb, ci = st["class_bytes"], st["class_ids"]
     kernels = {
         "k_segment": (avg("ms_segment"), 1.25 * B),
         "k_bpe_short": (avg("ms_bpe_lo"), cb[0] + cb[1] + 4 * (ci[0] + ci[1])),
         "k_bpe_mid": (avg("ms_bpe_hi"), cb[2] + 4 * ci[2]),
+        "k_emit": (avg("ms_emit"), 8 * T + 16 * (D + 1)),  # + tile scan, k_tokoff: ids read + written, offsets
     }
     dom = max(kernels, key=lambda k: kernels[k][0])
     ms_dom, alg_dom = kernels[dom]
@@ -169,15 +292,19 @@ def main():
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            threads = min(16, os.cpu_count() or 1)
-            cpu = cpu_baseline(tok_path, text, off, args.cpu_seconds, threads)
+            cpu = cpu_baseline(tok_path, text, off, args.cpu_seconds)
         traffic = None  # HBM bytes per launch of the dominant kernel from the committed PMC passes
         tr_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(tr_path):
-            per = json.load(open(tr_path)).get("hbm_bytes_per_launch", {})
-            hits = [v for k, v in per.items() if k.split("<")[0] == dom]
-            traffic = hits[0] if len(hits) == 1 else None
+            tr = json.load(open(tr_path))
+            if tr.get("workload") == "%s/%d" % (args.config, n_docs):
+                per = tr.get("hbm_bytes_per_launch", {})
+                hits = [v for k, v in per.items() if k.split("<")[0] == dom]
+                traffic = hits[0] if len(hits) == 1 else None
         ms_step = elapsed_max / args.steps * 1e3
+        cfg = dict(desc)
+        cfg.update({"docs_per_gpu": n_docs, "bytes_per_gpu": n_bytes, "tokens_per_gpu": int(T),
+                    "parallelism": "doc-sharded x%d, no collectives" % world})
         out = {
             "metric": METRIC,
             "value": round(total_bytes * args.steps / elapsed_max / 1e6, 2),
@@ -187,14 +314,11 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_step, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.config == "c4" else "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic (datagen/corpus.py C2 generator, seed 2+1000*rank; synthetic GPT-2-shaped tokenizer)",
-            "config": {"workload": "C2: %d docs x 96-160 B ASCII per GPU (%.1f MB), GPT-2-shaped 50,257-token "
-                                   "ByteLevel BPE" % (n_docs, n_bytes / 1e6),
-                       "docs_per_gpu": n_docs, "bytes_per_gpu": n_bytes, "tokens_per_gpu": int(T),
-                       "parallelism": "doc-sharded x%d, no collectives" % world},
+            "data": "synthetic (datagen/corpus.py %s generator; synthetic GPT-2-shaped tokenizer)" % args.config.upper(),
+            "config": cfg,
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(ach, 2), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 5), "traffic": traffic,
                          "alg_bytes_per_launch": int(alg_dom), "ms_per_launch": round(ms_dom, 4),

@@ -1425,7 +1425,10 @@ RangeOut encode_host_range(ctok* t, DeviceState* ds, const uint8_t* text, const 
   double ms_h2d = 0, ms_d2h = 0, ms_dev = 0, ms_pre = 0, ms_bs = 0, ms_bl = 0, ms_em = 0, ms_seg = 0, ms_lo = 0, ms_hi = 0;
   double ms_med = 0;
 
+  // stage / drain run on helper threads: each makes the shard's device current first (the HIP
+  // current device is per thread)
   auto stage = [&](size_t c) {
+    HIPTRY(hipSetDevice(ds->device));
     const int k = (int)(c & 1);
     const uint64_t a = cut[c], b = cut[c + 1], n = b - a, B = off[b] - off[a];
     HIPTRY(hipEventSynchronize(P->ev_h2d[k]));  // chunk c - 2's H2D from these pinned buffers
@@ -1441,6 +1444,7 @@ RangeOut encode_host_range(ctok* t, DeviceState* ds, const uint8_t* text, const 
     HIPTRY(hipEventRecord(P->ev_h2d[k], P->up));
   };
   auto drain = [&](size_t c) {
+    HIPTRY(hipSetDevice(ds->device));
     const int k = (int)(c & 1);
     const uint64_t a = cut[c], n = cut[c + 1] - a;
     HIPTRY(hipEventSynchronize(P->ev_d2h[k]));

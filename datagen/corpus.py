@@ -7,7 +7,7 @@ Configs:
   C1  1,000 docs, uniform 1-64 B, ASCII English-like                         seed 1
   C2  1,000,000 docs, uniform 96-160 B (mean 128), ASCII English-like          seed 2
   C3  100,000 docs, log-uniform 16 B-4 KiB, ASCII + Latin-1; 1% carry >=1 KiB letter/digit runs  seed 3
-  C4  10,000,000 docs as C2 (sharded over GPUs)                                seed 4
+  C4  10,000,000 docs as C2, in independent 1M-doc blocks (sharded over GPUs)  seed 4
   C5  1,000,000 docs, uniform 64-512 B: 40% CJK/kana/Hangul, 20% emoji, 40% ASCII   seed 5
 """
 from __future__ import annotations
@@ -171,8 +171,55 @@ def corpus_c2(n_docs: int = 1_000_000, seed: int = 2):
     return _docs_from_lengths(g.stream, lengths, False)
 
 
-def corpus_c4(n_docs: int = 10_000_000, seed: int = 4):
-    return corpus_c2(n_docs, seed)
+# C4: 10M C2-style docs, built in blocks of C4_BLOCK docs so that any doc range (a rank's shard)
+# is generated without the rest: the doc lengths of the whole corpus come from one cheap RNG
+# stream (seed), block b's text from the C2 generator re-seeded with (seed, b).  Blocks are
+# independent, so they are built by a process pool.
+C4_DOCS = 10_000_000
+C4_BLOCK = 1_000_000
+
+
+def c4_lengths(n_docs: int = C4_DOCS, seed: int = 4) -> np.ndarray:
+    return np.random.default_rng([seed, 0x4C454E]).integers(96, 161, size=n_docs)
+
+
+def c4_offsets(n_docs: int = C4_DOCS, seed: int = 4) -> np.ndarray:
+    """Byte offsets[D+1] of the whole C4 corpus (what parallel.shard_bounds cuts)."""
+    return np.concatenate([[0], np.cumsum(c4_lengths(n_docs, seed))]).astype(np.uint64)
+
+
+_C4_GEN = {}
+
+
+def _c4_block(args):
+    seed, b, lengths = args
+    g = _C4_GEN.get(seed)
+    if g is None:
+        g = _C4_GEN[seed] = EnglishGen(seed)  # lexicon and surfaces shared by every block
+    g.rng = np.random.default_rng([seed, b])
+    return _docs_from_lengths(g.stream, lengths, False)[0]
+
+
+def corpus_c4_range(d0: int, d1: int, n_docs: int = C4_DOCS, seed: int = 4, workers: int = 1):
+    """Docs [d0, d1) of C4 as (text, offsets rebased to 0)."""
+    lengths = c4_lengths(n_docs, seed)
+    off = np.concatenate([[0], np.cumsum(lengths)]).astype(np.int64)
+    b0, b1 = d0 // C4_BLOCK, (max(d1, d0 + 1) - 1) // C4_BLOCK + 1
+    jobs = [(seed, b, lengths[b * C4_BLOCK: min((b + 1) * C4_BLOCK, n_docs)]) for b in range(b0, b1) if d1 > d0]
+    if workers > 1 and len(jobs) > 1:
+        import multiprocessing as mp
+        with mp.get_context("fork").Pool(min(workers, len(jobs))) as pool:
+            parts = pool.map(_c4_block, jobs)
+    else:
+        parts = [_c4_block(j) for j in jobs]
+    text = np.concatenate(parts) if parts else np.zeros(0, np.uint8)
+    base = int(off[b0 * C4_BLOCK]) if jobs else 0
+    a, z = int(off[d0]) - base, int(off[d1]) - base
+    return text[a:z].copy(), (off[d0:d1 + 1] - off[d0]).astype(np.uint64)
+
+
+def corpus_c4(n_docs: int = C4_DOCS, seed: int = 4, workers: int = 1):
+    return corpus_c4_range(0, n_docs, n_docs, seed, workers)
 
 
 def corpus_c3(n_docs: int = 100_000, seed: int = 3):

@@ -8,7 +8,7 @@
                       computed with the C oracle (ctok_ref.c), itself checked against ref_py on a
                       sample of the same corpus first.  Also digests of the first 100k docs (CPU tests).
 
-Usage: python tests/golden/make_golden.py [c1 edge c2 c3 c5]
+Usage: python tests/golden/make_golden.py [c1 edge c2 c3 c4 c5]
 """
 import hashlib
 import json
@@ -20,7 +20,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
-sys.path.insert(0, ROOT)
+sys.path[:0] = [ROOT, os.path.join(ROOT, "complexity-tokenizer_amd")]
 
 from datagen import corpus  # noqa: E402
 from datagen.build_tokenizers import fixture_path  # noqa: E402
@@ -103,6 +103,51 @@ def big(name):
         json.dump(d, f, indent=1, sort_keys=True)
 
 
+def c4_shard_digests(counts, ids_blocks, worlds=(1, 2, 4, 8)):
+    """sha256 of (tok_off, ids) of every rank's shard (parallel.shard_bounds over C4's byte
+    offsets) for each world size: what bench.py checks per rank."""
+    from complexity_tokenizer.parallel import shard_bounds
+    off = corpus.c4_offsets()
+    tok_off = np.concatenate([[0], np.cumsum(counts)]).astype(np.uint64)
+    ids = np.concatenate(ids_blocks)
+    out = {}
+    for w in worlds:
+        for r in range(w):
+            d0, d1 = shard_bounds(off, w, r)
+            t0, t1 = int(tok_off[d0]), int(tok_off[d1])
+            out["%d/%d" % (r, w)] = {"docs": [d0, d1], "bytes": int(off[d1] - off[d0]), "tokens": t1 - t0,
+                                     "sha256": digest(ids[t0:t1], tok_off[d0:d1 + 1] - np.uint64(t0))}
+    return out
+
+
+def c4():
+    """C4 (10M docs, 1.28 GB) block by block through the C oracle; digests per shard."""
+    obj = load("gpt2_50k")
+    rc = ref_c.RefC(obj)
+    py = ref_py.RefTokenizer(obj)
+    n = corpus.C4_DOCS
+    counts = np.zeros(n, dtype=np.int64)
+    blocks = []
+    t = time.time()
+    for b in range(0, n, corpus.C4_BLOCK):
+        e = min(n, b + corpus.C4_BLOCK)
+        text, off = corpus.corpus_c4_range(b, e)
+        if b == 0:  # pin the C oracle against ref_py on a sample of this corpus
+            ns = 2000
+            docs = [d.decode() for d in corpus.unpack(text[: int(off[ns])], off[: ns + 1])]
+            assert py.encode_batch(docs) == rc.encode_batch(docs), "C4: C oracle disagrees with ref_py"
+        ids, tok_off = rc.encode_packed(text, off)
+        counts[b:e] = np.diff(tok_off.astype(np.int64))
+        blocks.append(ids)
+        print("C4 block %d: %d ids, %.1fs" % (b // corpus.C4_BLOCK, len(ids), time.time() - t), flush=True)
+    path = os.path.join(HERE, "digests.json")
+    d = json.load(open(path)) if os.path.exists(path) else {}
+    d["C4"] = {"tokenizer": "gpt2_50k", "docs": n, "bytes": int(corpus.c4_offsets()[-1]),
+               "tokens": int(counts.sum()), "shards": c4_shard_digests(counts, blocks)}
+    with open(path, "w") as f:
+        json.dump(d, f, indent=1, sort_keys=True)
+
+
 def main(args):
     os.makedirs(TMP, exist_ok=True)
     for a in args or ["c1", "edge", "c2", "c3", "c5"]:
@@ -110,6 +155,8 @@ def main(args):
             c1()
         elif a == "edge":
             edge()
+        elif a == "c4":
+            c4()
         else:
             big(a.upper())
 

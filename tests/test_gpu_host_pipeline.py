@@ -107,3 +107,15 @@ def test_capacity_error_reports_size(gpt2, c2):
                                       len(exact), out_off.ctypes.data, ctypes.byref(ex), None)
         assert rc == _n.CTOK_OK
         assert np.array_equal(exact, ids) and np.array_equal(out_off, toff)
+
+
+def test_shards_over_every_visible_device(gpt2, c2):
+    """ctok_exec.devices = every visible device (one shard per GPU, one host thread each, each
+    thread making its device current); on a 1-GPU box this is one shard, on a node all of them."""
+    tok, rc = gpt2
+    text, off = c2
+    n = _n.lib.ctok_device_count()
+    assert n >= 1
+    devs = list(range(n))
+    assert_same(*run(tok, text, off, devices=devs, chunk_mb=4), *rc.encode_packed(text, off))
+    assert_same(*run(tok, text, off, devices=devs + devs, chunk_mb=4), *rc.encode_packed(text, off))
