@@ -145,7 +145,21 @@ def workload(args, rank, world):
     full = corpus.c4_offsets(n)
     d0, d1 = shard_bounds(full, world, rank)
     cpus = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
-    text, off = corpus.corpus_c4_range(d0, d1, n, workers=max(1, min(8, cpus // world)))
+    # shards are cached under /tmp: a profiled rerun (rocprofv3 --pmc initialises the GPU before
+    # main) must not fork a corpus pool, so it reads what the unprofiled run built
+    cache = os.path.join(os.environ.get("TMPDIR", "/tmp"), "ctok_corpus", "c4_%d_%d_%d.npz" % (n, d0, d1))
+    if os.path.exists(cache):
+        z = np.load(cache)
+        text, off = z["text"], z["off"]
+    else:
+        text, off = corpus.corpus_c4_range(d0, d1, n, workers=1 if args.corpus_workers == 1 else
+                                           max(1, min(8, cpus // world)))
+        try:
+            os.makedirs(os.path.dirname(cache), exist_ok=True)
+            np.savez(cache + ".tmp.npz", text=text, off=off)
+            os.replace(cache + ".tmp.npz", cache)
+        except OSError:
+            pass
     desc = {"workload": "C4: %d docs x 96-160 B ASCII (%.2f GB), GPT-2-shaped 50,257-token ByteLevel BPE, "
                         "byte-balanced doc shards over %d GPU(s)" % (n, int(full[-1]) / 1e9, world),
             "docs_total": n, "bytes_total": int(full[-1])}
@@ -162,6 +176,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=16.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--corpus-workers", type=int, default=0, help="1: build the corpus without a process pool")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:

@@ -212,7 +212,8 @@ struct DeviceState {
   DevBuf<uint64_t> comp_key;
   Tables t{};
   // workspace
-  DevBuf<uint32_t> docbits, pbits, tile_np, tile_tok, tcls, list0, list1, list2, list3, tcnt, scratch, counters, lw;
+  DevBuf<uint32_t> docbits, pbits, tile_np, tile_tok, tcls, list0, list1, list2, list3, tcnt, scratch, lscratch, counters, lw;
+  DevBuf<uint64_t> tregion;
   DevBuf<uint16_t> wpref;
   DevBuf<uint32_t> long_cnt;
   DevBuf<uint64_t> long_list, mid_list, scan_tmp;
@@ -1146,7 +1147,9 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
     ds->list3.ensure(nt * kCap3 + 8);
   }
   ds->tcnt.ensure(nt * kTileSlots + 8);
-  ds->scratch.ensure(nt * kTile + 8);  // whole tiles: k_emit gathers unconditionally
+  ds->scratch.ensure(nt * kTileSlots + 8);  // per tile: the class regions of the register passes
+  ds->lscratch.ensure(B + 64);             // long / generic-pass pieces, by text offset
+  ds->tregion.ensure(nt + 8);
   ds->long_list.ensure(B / kShortMax + nt + 8);
   ds->long_cnt.ensure(B / kShortMax + nt + 8);
   ds->mid_list.ensure(B / 2 + 8);
@@ -1165,6 +1168,8 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   w.long_cnt = ds->long_cnt.p;
   w.tcnt = ds->tcnt.p;
   w.scratch = ds->scratch.p;
+  w.lscratch = ds->lscratch.p;
+  w.tregion = (uint2*)ds->tregion.p;
   w.long_list = ds->long_list.p;
   w.mid_list = ds->mid_list.p;
   w.counters = ds->counters.p;

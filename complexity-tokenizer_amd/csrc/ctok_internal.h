@@ -38,15 +38,32 @@ __host__ __device__ constexpr int ctr_stat(int c) { return c < 3 ? 6 + 2 * c : 1
 __host__ __device__ constexpr int ctr_chunk(int c) { return c < 3 ? 13 + c : 18; }
 constexpr int kCtrAnyMid = 19;  // counters[19] != 0: some tile has a class-2 piece
 constexpr int kCtrAnyC3 = 20;   // counters[20] != 0: some tile has a class-3 piece
-// List entry (u32): start within the tile [0,12), piece index within the tile [12,24), length [24,30).
+// List entry (u32): start within the tile [0,12), piece index within the tile [12,24), length [24,31)
+// (<= kMedMax = 64), kEntDoc: the piece starts a document.
+constexpr uint32_t kEntDoc = 1u << 31;
 __host__ __device__ inline uint32_t list_entry(uint32_t sl, uint32_t j, uint32_t n) { return sl | (j << 12) | (n << 24); }
+__host__ __device__ inline uint32_t ent_len(uint32_t e) { return (e >> 24) & 127u; }
+__host__ __device__ inline uint32_t ent_j(uint32_t e) { return (e >> 12) & 0xFFFu; }
+// long_list entry (u64): start byte | j << 32 | kLongDoc; mid_list entry: start | j << 32 |
+// kMidDoc | n << 48.
+constexpr uint64_t kLongDoc = 1ull << 63, kMidDoc = 1ull << 44;
 
 // Piece record (tcnt[tile][j], u32), written by whichever pass finishes piece j:
 //   kRecHit | id            one id, the whole-piece probe's (no scratch entry)
 //   kRecLong | li           long piece li: count long_cnt[li], ids at scratch[(u32)long_list[li] ..]
-//   count | start << 16     merged piece (<= 32 B): ids at scratch[tile start + start ..]
-// k_emit turns the records into each piece's first id within the tile (for k_tokoff).
-constexpr uint32_t kRecHit = 0x80000000u, kRecLong = 0x40000000u;
+//   count | pos << 16       merged piece (<= 64 B, register passes): ids at scratch[tile * kTileSlots + pos ..]
+//                           (pos: a slot of the tile's region for the piece's length class, see tregion)
+//   kRecAlt | count | start << 16   piece of the generic pass: ids at lscratch[tile * kTile + start ..]
+// | kRecDoc when the piece starts a document: k_emit then leaves the piece's first id within the
+// tile in its slot (for k_tokoff).
+constexpr uint32_t kRecHit = 0x80000000u, kRecLong = 0x40000000u, kRecDoc = 0x20000000u, kRecAlt = 0x10000000u;
+constexpr uint32_t kRecIdMask = (1u << kIdBits) - 1u, kRecLongMask = kRecDoc - 1u;
+// Per-tile id regions of the register merge passes in scratch (kTileSlots u32 per tile): class c
+// (c = 0..3) starts at the total bytes of the tile's class lists < c (ids <= bytes), packed as
+// tregion[tile] = {R1 | R2 << 16, R3}.
+__host__ __device__ inline uint32_t region_base(uint2 r, int cls) {
+  return cls <= 0 ? 0u : cls == 1 ? (r.x & 0xFFFFu) : cls == 2 ? (r.x >> 16) : r.y;
+}
 __host__ __device__ inline uint32_t rec_short(uint32_t count, uint32_t sl) { return count | (sl << 16); }
 
 // 24-bit multiply (v_mul_u32_u24: full rate; a 32-bit v_mul_lo_u32 is quarter rate on CDNA)
@@ -154,7 +171,9 @@ struct Work {              // device pointers, sized by the host for one call
   uint32_t* tcnt;          // [n_tiles * kTileSlots] record of piece j (see kRecHit), then (k_emit) its
                            // first id within the tile
   uint32_t* long_cnt;      // ids of long piece li
-  uint32_t* scratch;       // [n_bytes] ids of the piece starting at byte s at scratch[s ..]
+  uint32_t* scratch;       // [n_tiles * kTileSlots] ids of the register passes' pieces, per tile and class region
+  uint32_t* lscratch;      // [n_bytes + 64] ids of a long / generic-pass piece starting at byte s at lscratch[s ..]
+  uint2* tregion;          // [n_tiles] class region bases of the tile in scratch (region_base)
   uint64_t* long_list;     // pieces > kMedMax B (> kShortMax B in generic mode), or of unknown length
                            // at a tile end: s | j << 32
   uint64_t* mid_list;      // pieces with dropped bytes for the generic kernel: s | j << 32 | n << 48

@@ -270,6 +270,7 @@ __device__ __forceinline__ uint32_t select_bit(uint64_t x, uint32_t k) {
 __global__ __launch_bounds__(64 * kSegWaves) void k_segment(Work w, Tables t) {
   __shared__ uint16_t s_pos_all[kSegWaves][64 * kSegUnroll + 8];  // one round's piece starts
   __shared__ uint32_t s_text_all[kSegWaves][(kTileWords + 1) * 16 + 4];  // the tile + look-ahead word
+  __shared__ uint64_t s_D_all[kSegWaves][64];  // doc starts per word (piece records carry kRecDoc)
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wid = uni(threadIdx.x >> 6);
   const uint32_t tile = uni(blockIdx.x * kSegWaves + wid);
@@ -312,6 +313,7 @@ __global__ __launch_bounds__(64 * kSegWaves) void k_segment(Work w, Tables t) {
     }
   }
   seg::Masks m = seg::ascii_masks(x);
+  s_D_all[wid][lane] = D;
   uint32_t* s_text = s_text_all[wid];
   if (!first) {  // the tile's bytes (and the look-ahead word) for the whole-piece probes
 #pragma unroll
@@ -449,6 +451,7 @@ __global__ __launch_bounds__(64 * kSegWaves) void k_segment(Work w, Tables t) {
   uint32_t* tcnt = w.tcnt + (size_t)tile * kTileSlots;
   uint32_t hits = 0;
   uint32_t n0 = 0, n1 = 0, n2 = 0, n3 = 0;  // class-list lengths (wave-uniform)
+  uint32_t by0 = 0, by1 = 0, by2 = 0;        // this lane's bytes in class lists 0..2 (id regions)
   constexpr int U = kSegUnroll;
   constexpr uint32_t W = 64 * U;  // pieces per round
   for (uint32_t j0 = 0; j0 < np; j0 += W) {
@@ -465,15 +468,17 @@ __global__ __launch_bounds__(64 * kSegWaves) void k_segment(Work w, Tables t) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    uint32_t sl[U], n[U], cls[U], plo[U], phi[U], h[U];
+    uint32_t sl[U], n[U], cls[U], plo[U], phi[U], h[U], doc[U];
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const uint32_t j = j0 + 64 * u + lane;
       sl[u] = 0;
       n[u] = 0;
+      doc[u] = 0;
       cls[u] = 4;  // 0..2 class lists, 3 long, 4 done (or inactive), 5 probe, 6 class list 3
       if (j < np) {
         sl[u] = s_pos[64 * u + lane];
+        doc[u] = (uint32_t)(s_D_all[wid][(sl[u] >> 6) + 1] >> (sl[u] & 63)) & 1u;
         const uint32_t el = s_pos[64 * u + lane + 1];
         if (el == 0xFFFFu || el - sl[u] > (generic ? (uint32_t)kShortMax : (uint32_t)kMedMax)) {
           cls[u] = 3;
@@ -514,7 +519,7 @@ __global__ __launch_bounds__(64 * kSegWaves) void k_segment(Work w, Tables t) {
       // miscompiled by this hipcc in the unrolled loop)
       if (cls[u] == 5) {
         const bool hit = hitv[u] != kNone;
-        rec = hit ? kRecHit | hitv[u] : 0u;
+        rec = hit ? kRecHit | hitv[u] | (doc[u] ? kRecDoc : 0u) : 0u;
         hits += hit ? 1u : 0u;
         cls[u] = hit ? 4u : 0u;
       }
@@ -523,7 +528,7 @@ __global__ __launch_bounds__(64 * kSegWaves) void k_segment(Work w, Tables t) {
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const uint32_t j = j0 + 64 * u + lane;
-      const uint32_t e = list_entry(sl[u], j, n[u]);
+      const uint32_t e = list_entry(sl[u], j, n[u]) | (doc[u] ? kEntDoc : 0u);
       {  // the wave owns its tile's lists: running counts in scalar registers, no atomics
         const uint64_t m0 = __ballot(cls[u] == 0), m1 = __ballot(cls[u] == 1), m2 = __ballot(cls[u] == 2);
         const uint64_t m3 = __ballot(cls[u] == 6);
@@ -532,6 +537,9 @@ __global__ __launch_bounds__(64 * kSegWaves) void k_segment(Work w, Tables t) {
         if (cls[u] == 1) w.list1[(size_t)tile * kCap1 + n1 + __popcll(m1 & below)] = e;
         if (cls[u] == 2) w.list2[(size_t)tile * kCap2 + n2 + __popcll(m2 & below)] = e;
         if (cls[u] == 6) w.list3[(size_t)tile * kCap3 + n3 + __popcll(m3 & below)] = e;
+        by0 += cls[u] == 0 ? n[u] : 0u;
+        by1 += cls[u] == 1 ? n[u] : 0u;
+        by2 += cls[u] == 2 ? n[u] : 0u;
         n0 += __popcll(m0);
         n1 += __popcll(m1);
         n2 += __popcll(m2);
@@ -543,7 +551,9 @@ __global__ __launch_bounds__(64 * kSegWaves) void k_segment(Work w, Tables t) {
         uint32_t b = 0;
         if (lane == leader) b = atomicAdd(&w.counters[0], (uint32_t)__popcll(lm));
         b = (uint32_t)__shfl((int)b, (int)leader, 64);
-        if (cls[u] == 3) w.long_list[b + __popcll(lm & lanemask_lt())] = (uint64_t)(t0 + sl[u]) | ((uint64_t)j << 32);
+        if (cls[u] == 3)
+          w.long_list[b + __popcll(lm & lanemask_lt())] =
+              (uint64_t)(t0 + sl[u]) | ((uint64_t)j << 32) | (doc[u] ? kLongDoc : 0ull);
       }
     }
     // every lane has read this round's s_pos before the next round's expansion overwrites it
@@ -552,12 +562,20 @@ __global__ __launch_bounds__(64 * kSegWaves) void k_segment(Work w, Tables t) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) hits += (uint32_t)__shfl_xor((int)hits, o, 64);
+  for (int o = 32; o > 0; o >>= 1) {
+    hits += (uint32_t)__shfl_xor((int)hits, o, 64);
+    by0 += (uint32_t)__shfl_xor((int)by0, o, 64);
+    by1 += (uint32_t)__shfl_xor((int)by1, o, 64);
+    by2 += (uint32_t)__shfl_xor((int)by2, o, 64);
+  }
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   __builtin_amdgcn_wave_barrier();
   if (lane == 0) {
     w.tile_tok[tile] = hits;  // initial token count (the merge passes add theirs atomically)
     w.tile_np[tile] = np;
+    // id regions of the register passes (ids <= bytes per piece; all four fit in kTileSlots:
+    // the lists hold pieces that start in the tile and end within its 62-byte look-ahead)
+    w.tregion[tile] = make_uint2(by0 | ((by0 + by1) << 16), by0 + by1 + by2);
   }
   if (lane < kNumClasses)
     w.tcls[(size_t)lane * w.n_tiles + tile] = lane == 0 ? n0 : lane == 1 ? n1 : lane == 2 ? n2 : n3;
@@ -660,17 +678,24 @@ __device__ __forceinline__ uint32_t bpe_short(const Tables& t, const uint8_t* by
 // binary search over those K offsets.  Token counts are summed per tile in LDS and added to
 // tile_tok with one atomic per (workgroup, tile); no two workgroups share a (class, tile).
 
+// s_tsum[l] starts at tile t0 + l's region base for class cls (tregion, cls >= 0) or at 0: the
+// merge passes allocate their ids from it (and add the difference to tile_tok at the flush).
 template <int K>
 __device__ __forceinline__ uint32_t tile_share_init(const uint32_t* counts, uint32_t n_tiles, uint32_t t0,
-                                                    uint32_t* s_pre, uint32_t* s_tsum) {
+                                                    uint32_t* s_pre, uint32_t* s_tsum, const uint2* tregion = nullptr,
+                                                    int cls = -1, uint32_t* s_tbase = nullptr) {
   static_assert(K >= 1 && K <= 64 && (K & (K - 1)) == 0, "K: power of two <= 64");
   if (threadIdx.x < 64) {
     const uint32_t l = threadIdx.x;
-    const uint32_t c = (l < K && t0 + l < n_tiles) ? counts[t0 + l] : 0u;
+    const bool in = l < K && t0 + l < n_tiles;
+    const uint32_t c = in ? counts[t0 + l] : 0u;
     const uint32_t inc = wave_incl_scan(c);
     if (l < K) {
       s_pre[l] = inc - c;
-      s_tsum[l] = 0;
+      uint32_t b0 = 0;
+      if (cls > 0 && in) b0 = region_base(tregion[t0 + l], cls);
+      s_tsum[l] = b0;
+      if (s_tbase) s_tbase[l] = b0;
     }
     if (l == 63) s_pre[K] = inc;
   }
@@ -688,10 +713,13 @@ __device__ __forceinline__ uint32_t tile_of(const uint32_t* s_pre, uint32_t q) {
 }
 
 template <int K>
-__device__ __forceinline__ void tile_share_flush(const Work& w, uint32_t t0, const uint32_t* s_tsum) {
+__device__ __forceinline__ void tile_share_flush(const Work& w, uint32_t t0, const uint32_t* s_tsum,
+                                                 const uint32_t* s_tbase = nullptr) {
   __syncthreads();
-  if (threadIdx.x < K && t0 + threadIdx.x < w.n_tiles && s_tsum[threadIdx.x])
-    atomicAdd(&w.tile_tok[t0 + threadIdx.x], s_tsum[threadIdx.x]);
+  if (threadIdx.x < K && t0 + threadIdx.x < w.n_tiles) {
+    const uint32_t v = s_tsum[threadIdx.x] - (s_tbase ? s_tbase[threadIdx.x] : 0u);
+    if (v) atomicAdd(&w.tile_tok[t0 + threadIdx.x], v);
+  }
 }
 
 constexpr int kTilesGeneric = 2;  // tiles per workgroup, generic pass over list0
@@ -722,23 +750,25 @@ __global__ __launch_bounds__(MID ? 128 : 256) void k_bpe_generic(Work w, Tables 
   }
   const uint32_t stride = MID ? gridDim.x * NT : NT;
   for (uint32_t q = (MID ? blockIdx.x * NT : 0) + tid; q < E; q += stride) {
-    uint32_t s, j, n, tile, kt = 0;
+    uint32_t s, j, n, tile, kt = 0, doc;
     if (MID) {
       const uint64_t e = w.mid_list[q];
       s = (uint32_t)e;
-      j = (uint32_t)(e >> 32) & 0xFFFFu;
+      j = (uint32_t)(e >> 32) & 0xFFFu;
       n = (uint32_t)(e >> 48);
+      doc = (e & kMidDoc) ? kRecDoc : 0u;
       tile = s / kTile;
     } else {
       kt = tile_of<kTilesGeneric>(s_pre, q);
       tile = t0 + kt;
       const uint32_t e = w.list0[(size_t)tile * kCap0 + (q - s_pre[kt])];
       s = tile * kTile + (e & 0xFFFu);
-      j = (e >> 12) & 0xFFFu;
-      n = e >> 24;
+      j = ent_j(e);
+      n = ent_len(e);
+      doc = (e & kEntDoc) ? kRecDoc : 0u;
     }
     const uint8_t* bytes = w.text + s;
-    uint32_t* out = w.scratch + s;
+    uint32_t* out = w.lscratch + s;
     uint32_t cnt = 0;
     if (t.n_at == 0) {
       cnt = bpe_short<NT>(t, bytes, n, s_b2id, s_tok, s_rk, tid, out, err);
@@ -762,7 +792,7 @@ __global__ __launch_bounds__(MID ? 128 : 256) void k_bpe_generic(Work w, Tables 
         pos += nxt;
       }
     }
-    w.tcnt[(size_t)tile * kTileSlots + j] = rec_short(cnt, s - tile * kTile);
+    w.tcnt[(size_t)tile * kTileSlots + j] = rec_short(cnt, s - tile * kTile) | doc | kRecAlt;
     if (MID) atomicAdd(&w.tile_tok[tile], cnt);
     else atomicAdd(&s_tsum[kt], cnt);
   }
@@ -895,7 +925,7 @@ __device__ __forceinline__ bool merge_slots(const Tables& t, const PairLds& P, u
 // Workgroup-shared scratch of a merge pass.
 template <uint32_t SORTCAP>
 struct PassLds {
-  uint32_t pre[65], tsum[64], stat[2], bcnt[4], bfill[4], chunk;
+  uint32_t pre[65], tsum[64], tbase[64], stat[2], bcnt[4], bfill[4], chunk;
   uint16_t perm[SORTCAP];  // the chunk's entries ordered by length bucket
 };
 
@@ -930,7 +960,7 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
     const uint32_t c0 = S.chunk * K;
     if (c0 >= w.n_tiles) break;
     const uint32_t tb1 = min(w.n_tiles, c0 + K);
-    const uint32_t E = tile_share_init<K>(counts, tb1, c0, S.pre, S.tsum);
+    const uint32_t E = tile_share_init<K>(counts, tb1, c0, S.pre, S.tsum, w.tregion, LC::cls, S.tbase);
     if (E && !loaded) {  // E is workgroup-uniform (read from LDS after a barrier)
       load();
       loaded = true;
@@ -942,7 +972,7 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
       __syncthreads();
       for (uint32_t q = tid; q < E; q += NT) {  // bucket sizes (one LDS add per wave and bucket)
         const uint32_t kt = tile_of<K>(S.pre, q);
-        const uint32_t b = bucket(list[(size_t)(c0 + kt) * LC::cap + (q - S.pre[kt])] >> 24);
+        const uint32_t b = bucket(ent_len(list[(size_t)(c0 + kt) * LC::cap + (q - S.pre[kt])]));
 #pragma unroll
         for (uint32_t bb = 0; bb < 4; bb++) {
           const uint64_t m = __ballot(b == bb);
@@ -961,7 +991,7 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
       __syncthreads();
       for (uint32_t q = tid; q < E; q += NT) {  // scatter entry numbers into bucket order
         const uint32_t kt = tile_of<K>(S.pre, q);
-        const uint32_t b = bucket(list[(size_t)(c0 + kt) * LC::cap + (q - S.pre[kt])] >> 24);
+        const uint32_t b = bucket(ent_len(list[(size_t)(c0 + kt) * LC::cap + (q - S.pre[kt])]));
 #pragma unroll
         for (uint32_t bb = 0; bb < 4; bb++) {
           const uint32_t slot = wave_append(&S.bfill[bb], b == bb);
@@ -1007,8 +1037,8 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
       }
       const uint32_t tile = c0 + kt;
       const uint32_t s = tile * kTile + (e & 0xFFFu);
-      const uint32_t j = (e >> 12) & 0xFFFu;
-      const uint32_t n = e >> 24;
+      const uint32_t j = ent_j(e);
+      const uint32_t n = ent_len(e);
       uint32_t tk[N], rk[N];
       bool missing = false;
       {
@@ -1020,7 +1050,8 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
         }
       }
       if (missing) {  // a byte char absent from the vocab is dropped: generic path
-        w.mid_list[atomicAdd(&w.counters[4], 1u)] = (uint64_t)s | ((uint64_t)j << 32) | ((uint64_t)n << 48);
+        w.mid_list[atomicAdd(&w.counters[4], 1u)] =
+            (uint64_t)s | ((uint64_t)j << 32) | ((uint64_t)n << 48) | ((e & kEntDoc) ? kMidDoc : 0ull);
         continue;
       }
       // initial pair ranks: every initial pair is a byte pair, one load each from the 256 x 256
@@ -1050,16 +1081,18 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
         if (more) more = merge_slots<16, COMPACT, HOT>(t, P, tk, rk, m, 8, err);
       }
       if (more) merge_slots<8, COMPACT, HOT>(t, P, tk, rk, m, 0, err);
-      uint32_t* out = w.scratch + s;
+      // ids go to the next free slots of the tile's region for this class (dense: a wave's
+      // stores fill whole lines), the record points at them
+      const uint32_t pos = atomicAdd(&S.tsum[kt], m);
+      uint32_t* out = w.scratch + (size_t)tile * kTileSlots + pos;
 #pragma unroll
       for (int k = 0; k < N; k++)
         if ((uint32_t)k < m) out[k] = tk[k];
-      w.tcnt[(size_t)tile * kTileSlots + j] = rec_short(m, e & 0xFFFu);
-      atomicAdd(&S.tsum[kt], m);
+      w.tcnt[(size_t)tile * kTileSlots + j] = rec_short(m, pos) | ((e & kEntDoc) ? kRecDoc : 0u);
       st_bytes += n;
       st_ids += m;
     }
-    tile_share_flush<K>(w, c0, S.tsum);
+    tile_share_flush<K>(w, c0, S.tsum, S.tbase);
     __syncthreads();
   }
   // statistics: bytes merged and ids produced by this pass (algorithmic bytes for the roofline)
@@ -1393,14 +1426,15 @@ __global__ __launch_bounds__(256) void k_bpe_long(Work w, Tables t) {
   for (uint32_t li = uni(blockIdx.x * (blockDim.x >> 6) + wid); li < n_long; li += n_waves) {
     const uint64_t e = w.long_list[li];
     const uint32_t s = uni((uint32_t)e);
-    const uint32_t j = uni((uint32_t)(e >> 32));
+    const uint32_t j = uni((uint32_t)(e >> 32) & 0xFFFFu);
+    const uint32_t doc = (e & kLongDoc) ? kRecDoc : 0u;
     const uint32_t n = uni(piece_end(w, s) - s);
     // tiers: LDS up to kLdsPos positions, global memory beyond (only beyond the dense wave tiers
     // when those run, i.e. without added tokens)
     const uint32_t gmin = (t.n_at != 0 || t.dbg == 7) ? kLdsPos : kWaveMax;
     if (GMEM != (n > gmin)) continue;
     const uint8_t* bytes = w.text + s;
-    uint32_t* out = w.scratch + s;
+    uint32_t* out = w.lscratch + s;
     uint32_t cnt;
     if constexpr (GMEM) {
       LongState<true> L{w.lw + s, w.lw + (size_t)B + s, w.lw + 2 * (size_t)B + s, w.lw + 3 * (size_t)B + s};
@@ -1413,7 +1447,7 @@ __global__ __launch_bounds__(256) void k_bpe_long(Work w, Tables t) {
     if (lane == 0) {
       const uint32_t tile = s / kTile;
       w.long_cnt[li] = cnt;
-      w.tcnt[(size_t)tile * kTileSlots + j] = kRecLong | li;
+      w.tcnt[(size_t)tile * kTileSlots + j] = kRecLong | li | doc;
       atomicAdd(&w.tile_tok[tile], cnt);
     }
   }
@@ -1789,16 +1823,17 @@ __global__ __launch_bounds__(64 * NW) void k_bpe_wave(Work w, Tables t) {
   for (uint32_t li = uni(blockIdx.x * NW + wid); li < n_long; li += n_waves) {
     const uint64_t e = w.long_list[li];
     const uint32_t s = uni((uint32_t)e);
-    const uint32_t j = uni((uint32_t)(e >> 32));
+    const uint32_t j = uni((uint32_t)(e >> 32) & 0xFFFFu);
+    const uint32_t doc = (e & kLongDoc) ? kRecDoc : 0u;
     const uint32_t n = uni(piece_end(w, s) - s);
     if (n <= LO || n > 64u * K) continue;
     uint32_t cnt;
-    if constexpr (SEG) cnt = bpe_wave_seg<K, HOT>(t, P, s_b2id, w.text + s, n, SegSlice<K>{slice}, w.scratch + s, err);
-    else cnt = bpe_wave_dense<K, HOT>(t, P, s_b2id, w.text + s, n, WaveSlice<K>{slice}, w.scratch + s, err);
+    if constexpr (SEG) cnt = bpe_wave_seg<K, HOT>(t, P, s_b2id, w.text + s, n, SegSlice<K>{slice}, w.lscratch + s, err);
+    else cnt = bpe_wave_dense<K, HOT>(t, P, s_b2id, w.text + s, n, WaveSlice<K>{slice}, w.lscratch + s, err);
     if (lane == 0) {
       const uint32_t tile = s / kTile;
       w.long_cnt[li] = cnt;
-      w.tcnt[(size_t)tile * kTileSlots + j] = kRecLong | li;
+      w.tcnt[(size_t)tile * kTileSlots + j] = kRecLong | li | doc;
       atomicAdd(&w.tile_tok[tile], cnt);
     }
   }
@@ -1848,105 +1883,81 @@ hipError_t launch_bpe_long(const Work& w, const Tables& t, hipStream_t s) {
 }
 
 // ------------------------------------------------------------------------------------------
-// emission.  tile_tok is scanned to each tile's first id; one workgroup per tile scans its
-// pieces' counts (blocked: 16 consecutive pieces per thread), copies each piece's ids from
-// scratch to ids[] (interleaved: coalesced writes), and leaves the first id (within the tile) of
-// each piece that starts a document in tcnt for k_tokoff (the only records it reads).
+// emission.  tile_tok is scanned to each tile's first id; then one wavefront per tile walks the
+// tile's piece records in rounds of 256 pieces: lane l takes pieces 256 r + 4 l .. + 3 (one
+// 16-byte record load; the next round's loads are issued before this round's stores), a wave
+// scan gives each piece's first id within the tile, and the lane writes the ids itself: a
+// whole-piece hit carries its id in the record, a merged piece's ids are copied from scratch.
+// Consecutive lanes write consecutive id runs, so every cache line of the output is written
+// whole within a few store instructions.  A doc-start piece (kRecDoc) leaves its first id
+// within the tile in its record slot for k_tokoff.  No LDS, no barrier: occupancy is set by
+// VGPRs alone and the record -> scratch chains of 8 waves per SIMD overlap.
+
+constexpr int kEmitWaves = 4;  // tiles per k_emit workgroup
 
 __device__ __forceinline__ uint32_t rec_count(const Work& w, uint32_t v) {
-  return (v & kRecHit) ? 1u : (v & kRecLong) ? w.long_cnt[v & ~kRecLong] : (v & 0xFFFFu);
+  return (v & kRecHit) ? 1u : (v & kRecLong) ? w.long_cnt[v & kRecLongMask] : (v & 0xFFFFu);
 }
 
-__global__ __launch_bounds__(256) void k_emit(Work w, uint32_t* __restrict__ ids, uint64_t ids_cap) {
-  __shared__ uint32_t s_scan[17];
-  // s_off[j + j / 16]: the padding makes the blocked writes (16 consecutive pieces per thread)
-  // conflict-free; the interleaved reads stay consecutive
-  __shared__ uint32_t s_off[kTileSlots + kTileSlots / 16 + 2];
-  auto so = [](uint32_t j) { return j + (j >> 4); };
-  const uint32_t tile = blockIdx.x, tid = threadIdx.x;
-  const uint32_t np = w.tile_np[tile];
-  const uint64_t base = w.tile_tok[tile];
+__global__ __launch_bounds__(64 * kEmitWaves) void k_emit(Work w, uint32_t* __restrict__ ids, uint64_t ids_cap) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t tile = uni(blockIdx.x * kEmitWaves + (threadIdx.x >> 6));
+  if (tile >= w.n_tiles) return;
+  const uint32_t np = uni(w.tile_np[tile]);
+  const uint64_t base = uni(w.tile_tok[tile]);
   uint32_t* tcnt = w.tcnt + (size_t)tile * kTileSlots;
-  const uint32_t* src0 = w.scratch + (size_t)tile * kTile;
-  // 1. thread tid scans pieces [16 tid, 16 tid + 16): four 16-byte loads, one workgroup scan
-  constexpr int PER = kTileSlots / 256;
-  const uint32_t jb = tid * PER;
-  uint32_t c[PER];
-  if (jb < np) {
-#pragma unroll
-    for (int k = 0; k < PER / 4; k++) {
-      const uint4 v = reinterpret_cast<const uint4*>(tcnt + jb)[k];
-      c[4 * k] = v.x; c[4 * k + 1] = v.y; c[4 * k + 2] = v.z; c[4 * k + 3] = v.w;
-    }
-  }
-  uint32_t sum = 0;
-#pragma unroll
-  for (int k = 0; k < PER; k++) {
-    c[k] = jb + k < np ? rec_count(w, c[k]) : 0u;
-    sum += c[k];
-  }
-  uint32_t total;
-  uint32_t o = block_excl_scan<uint32_t>(sum, s_scan, &total);
-  uint32_t pre[PER];
-#pragma unroll
-  for (int k = 0; k < PER; k++) {
-    pre[k] = o;
-    s_off[so(jb + k)] = o;
-    o += c[k];
-  }
-  if (tid == 0) s_off[so(np)] = total;
-  __syncthreads();
-  // 2. copy, piece j = tid + 256 k: consecutive lanes write consecutive ids.  A whole-piece hit
-  // carries its id in the record; other pieces read theirs from scratch, all first reads of a
-  // thread's pieces in flight together, the rest (multi-id pieces) four at a time.
-  uint32_t rec[PER];
-#pragma unroll
-  for (int k = 0; k < PER; k++) {
-    const uint32_t j = tid + 256 * k;
-    rec[k] = j < np ? tcnt[j] : kRecHit;
-  }
-  auto src_of = [&](uint32_t r) -> const uint32_t* {
-    return (r & kRecLong) ? w.scratch + (uint32_t)w.long_list[r & ~kRecLong] : src0 + ((r >> 16) & 0xFFFu);
+  const uint32_t* src0 = w.scratch + (size_t)tile * kTileSlots;
+  auto load = [&](uint32_t j0) {
+    return j0 < np ? *reinterpret_cast<const uint4*>(tcnt + j0) : make_uint4(0, 0, 0, 0);
   };
-  uint32_t v0[PER];
+  uint32_t run = 0;  // ids of the earlier rounds (wave-uniform)
+  uint4 nx = load(4 * lane);
+  for (uint32_t r0 = 0; r0 < np; r0 += 256) {
+    const uint32_t j0 = r0 + 4 * lane;
+    const uint32_t rec[4] = {nx.x, nx.y, nx.z, nx.w};
+    if (r0 + 256 < np) nx = load(j0 + 256);
+    uint32_t c[4], sum = 0;
 #pragma unroll
-  for (int k = 0; k < PER; k++) {
-    const uint32_t r = rec[k];
-    v0[k] = (r & kRecHit) ? (r & ~kRecHit) : src_of(r)[0];
-  }
-#pragma unroll
-  for (int k = 0; k < PER; k++) {
-    const uint32_t j = tid + 256 * k;
-    if (j >= np) break;
-    const uint32_t oj = s_off[so(j)], cj = s_off[so(j + 1)] - oj;
-    const uint64_t dst = base + oj;
-    if (cj > 0 && dst < ids_cap) ids[dst] = v0[k];
-    for (uint32_t m = 1; m < cj; m += 4) {
-      const uint32_t* sp = src_of(rec[k]);
-      uint32_t x[4];
-#pragma unroll
-      for (int i = 0; i < 4; i++) x[i] = m + i < cj ? sp[m + i] : 0u;
-#pragma unroll
-      for (int i = 0; i < 4; i++)
-        if (m + i < cj && dst + m + i < ids_cap) ids[dst + m + i] = x[i];  // the host reports CTOK_E_CAPACITY when short
+    for (int k = 0; k < 4; k++) {
+      c[k] = j0 + k < np ? rec_count(w, rec[k]) : 0u;
+      sum += c[k];
     }
-  }
-  __syncthreads();  // every record has been read: doc-start pieces get their first id
-  if (tid < kTileWords) {  // lane = 64-byte word of the tile; its doc starts are piece starts
-    const uint32_t g = tile * kTileWords + tid;
-    if (2 * g < w.n_words) {
-      uint64_t m = (uint64_t)w.docbits[2 * g] | ((uint64_t)w.docbits[2 * g + 1] << 32);
-      const uint64_t P = (uint64_t)w.pbits[2 * g] | ((uint64_t)w.pbits[2 * g + 1] << 32);
-      const uint32_t j0 = w.wpref[(size_t)tile * 64 + tid];
-      while (m) {
-        const uint32_t b = (uint32_t)__builtin_ctzll(m);
-        m &= m - 1;
-        const uint32_t j = j0 + (uint32_t)__popcll(P & ((1ull << b) - 1));
-        tcnt[j] = s_off[so(j)];
+    const uint32_t inc = wave_incl_scan(sum);
+    uint32_t o = run + inc - sum;
+    run = uni(run + (uint32_t)__shfl((int)inc, 63, 64));
+    // first ids: all loads of this lane's pieces in flight together
+    // (records past np are stale: c[k] == 0 keeps them from being followed)
+    const uint32_t* sp[4];
+    uint32_t v0[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint32_t r = rec[k];
+      const bool follow = c[k] != 0 && !(r & kRecHit);
+      sp[k] = !follow ? src0
+              : (r & kRecLong) ? w.lscratch + (uint32_t)w.long_list[r & kRecLongMask]
+              : ((r & kRecAlt) ? w.lscratch + (size_t)tile * kTile : src0) + ((r >> 16) & 0xFFFu);
+      v0[k] = (r & kRecHit) ? (r & kRecIdMask) : (follow ? sp[k][0] : 0u);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint32_t r = rec[k], cj = c[k];
+      const uint64_t dst = base + o;
+      if (cj > 0 && dst < ids_cap) ids[dst] = v0[k];
+      if (cj > 1) {  // merged / long piece: the rest of its ids, four loads in flight at a time
+        const uint32_t* spk = sp[k];
+        for (uint32_t m = 1; m < cj; m += 4) {
+          uint32_t x[4];
+#pragma unroll
+          for (int i = 0; i < 4; i++) x[i] = m + i < cj ? spk[m + i] : 0u;
+#pragma unroll
+          for (int i = 0; i < 4; i++)
+            if (m + i < cj && dst + m + i < ids_cap) ids[dst + m + i] = x[i];  // the host reports CTOK_E_CAPACITY when short
+        }
       }
+      if ((r & kRecDoc) && j0 + k < np) tcnt[j0 + k] = o;  // read by k_tokoff
+      o += cj;
     }
   }
-  (void)pre;
 }
 
 // tok_off[d] = first id of the piece that starts at doc_off[d] (every non-empty doc starts a
@@ -1971,7 +1982,7 @@ __global__ void k_tokoff(Work w, uint64_t* __restrict__ tok_off) {
 
 hipError_t launch_emit(const Work& w, uint32_t* ids, uint64_t ids_cap, uint64_t* tok_off, hipStream_t s) {
   HIPCHK(scan_u32(w.tile_tok, w.tile_tok, (uint64_t)w.n_tiles, nullptr, w.scan_tmp, w.scan_tmp_cap, s));
-  if (w.n_tiles) k_emit<<<w.n_tiles, 256, 0, s>>>(w, ids, ids_cap);
+  if (w.n_tiles) k_emit<<<(w.n_tiles + kEmitWaves - 1) / kEmitWaves, 64 * kEmitWaves, 0, s>>>(w, ids, ids_cap);
   k_tokoff<<<(w.n_docs + 1 + 255) / 256, 256, 0, s>>>(w, tok_off);
   return hipGetLastError();
 }

@@ -28,11 +28,11 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/
 cat "$OUT/prof_bench.json"
 if [ "$PMC" = pmc ]; then
   timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- \
-    python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-parity > "$OUT/pmc_fetch.log" 2>&1 \
+    python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-parity --corpus-workers 1 > "$OUT/pmc_fetch.log" 2>&1 \
     || { tail -20 "$OUT/pmc_fetch.log"; exit 1; }
   timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
-    python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-parity > "$OUT/pmc_write.log" 2>&1 \
+    python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-parity --corpus-workers 1 > "$OUT/pmc_write.log" 2>&1 \
     || { tail -20 "$OUT/pmc_write.log"; exit 1; }
-  python3 "$ROOT/tools/pmc_traffic.py" "$OUT/pmc_fetch" "$OUT/pmc_write" "$OUT/pmc_traffic.json"
+  python3 "$ROOT/tools/pmc_traffic.py" "$OUT/pmc_fetch" "$OUT/pmc_write" "$OUT/pmc_traffic.json" c4/10000000
 fi
 echo "gpu_check $TAG done"

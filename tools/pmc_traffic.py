@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """HBM traffic per kernel launch from rocprofv3 PMC passes (profiling helper, not product code).
 
-Usage: python tools/pmc_traffic.py FETCH_DIR WRITE_DIR OUT.json
+Usage: python tools/pmc_traffic.py FETCH_DIR WRITE_DIR OUT.json [WORKLOAD]
+  WORKLOAD: bench.py's config/docs of the profiled command (e.g. c4/10000000); bench.py uses
+  the file's numbers only for that workload
   FETCH_DIR: output of `rocprofv3 --pmc FETCH_SIZE ...` (…_counter_collection.csv)
   WRITE_DIR: output of `rocprofv3 --pmc WRITE_SIZE ...`
 
@@ -37,9 +39,10 @@ def load(d, counter):
 
 def main():
     fetch_dir, write_dir, out = sys.argv[1:4]
+    workload = sys.argv[4] if len(sys.argv) > 4 else None
     f = load(fetch_dir, "FETCH_SIZE")
     w = load(write_dir, "WRITE_SIZE")
-    res = {"unit": "bytes per launch", "fetch_correction": 2.0,
+    res = {"unit": "bytes per launch", "fetch_correction": 2.0, "workload": workload,
            "note": "FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE, KiB -> bytes",
            "fetch_kib": f, "write_kib": w, "hbm_bytes_per_launch": {}}
     for k in sorted(set(f) | set(w)):
