@@ -201,7 +201,7 @@ struct DeviceState {
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   uint64_t* host = nullptr;       // pinned host words for small device->host readbacks
   // tables
-  DevBuf<uint64_t> merge_tab, lds_image;
+  DevBuf<uint64_t> merge_tab, lds_image, lds16_image, merge16;
   DevBuf<uint32_t> pair0;
   DevBuf<uint32_t> piece_tab;
   DevBuf<uint32_t> rank_newid;
@@ -278,6 +278,8 @@ struct ctok {
   std::vector<uint64_t> merge_tab;
   uint32_t merge_mask = 0;
   std::vector<uint64_t> lds_image;  // kLdsImageBytes: hot table + Bloom filter
+  std::vector<uint64_t> lds16_image, merge16;  // narrow vocabularies: the 32-bit-key tables (key16)
+  uint32_t merge16_mask = 0;
   std::vector<uint32_t> pair0;      // 256 x 256 byte-pair merge values
   size_t hot_entries = 0;
   std::vector<uint32_t> piece_tab;  // 4 u32 per slot (see ctok_internal.h piece_hash)
@@ -289,6 +291,7 @@ struct ctok {
   std::vector<uint8_t> at_flags;
   bool proper = true;
   bool compact = false;
+  bool narrow = false;  // every vocab id < 2^16
   // decode (src/huggingface/mod.rs:710-747): decoder kind, per-id decoded bytes
   int decoder = 1;                  // 1 ByteLevel, 0 raw concatenation (unknown decoder type), -1 unsupported
   std::string decoder_name;         // for the unsupported message
@@ -663,6 +666,11 @@ void load(ctok* t, const char* buf, size_t len) {
   lap("ranks");
   if (merges.size() >= (size_t)kNoRank - 2) throw_err(CTOK_E_UNSUPPORTED, "more than 4M merges");
   t->rank_newid = valid_new;
+  {
+    uint32_t max_id = 0;
+    for (const auto& kv : t->vocab) max_id = std::max(max_id, kv.second);
+    t->narrow = max_id < 0xFFFFu;
+  }
   // compact table: values are the new ids themselves when new id is strictly increasing in rank
   {
     std::vector<std::pair<uint32_t, uint32_t>> rv;  // (rank, new id) of the entries that can merge
@@ -757,6 +765,43 @@ void load(ctok* t, const char* buf, size_t len) {
       bloom[b2 >> 5] |= 1u << (b2 & 31);
     }
     t->hot_entries = placed;
+    // narrow vocabularies: the same tables keyed by key16 (ctok_internal.h), for the register
+    // merge passes.  Global table: every entry, in rank order; hot table / Bloom filter: as above.
+    if (t->narrow) {
+      size_t cap16 = 1024;
+      while (cap16 < ranks.size() * 8 + 16) cap16 <<= 1;
+      t->merge16.assign(cap16, kEmpty);
+      t->merge16_mask = (uint32_t)(cap16 - 1);
+      for (const auto& rk : by_rank_key) {
+        const uint32_t a = (uint32_t)(rk.second >> 32), b = (uint32_t)rk.second;
+        uint64_t val = rk.first;
+        if (t->compact) val = rk.first < valid_new.size() ? valid_new[rk.first] : kPanicVal;
+        uint32_t h = hash16_h(a, b) & t->merge16_mask;
+        while (t->merge16[h] != kEmpty) h = (h + 1) & t->merge16_mask;
+        t->merge16[h] = (val << 32) | key16(a, b);
+      }
+      t->lds16_image.assign(kLdsImageBytes / 8, 0);
+      uint64_t* hot16 = t->lds16_image.data();
+      std::fill(hot16, hot16 + kHotU64, kEmpty);
+      uint32_t* bloom16 = reinterpret_cast<uint32_t*>(hot16 + kHotU64);
+      for (const auto& re : by_rank) {
+        const uint64_t e = re.second;
+        const uint32_t a = (uint32_t)((e >> kIdBits) & ((1u << kIdBits) - 1)), b = (uint32_t)(e & ((1u << kIdBits) - 1));
+        const uint32_t h = hash16_h(a, b), g = hash16_g(a, b);
+        uint64_t* slot = nullptr;
+        if (use_hot && re.first < valid_new.size())
+          for (uint32_t c : {h >> 20, g >> 20})
+            for (int k = 0; k < 2 && !slot; k++)
+              if (hot16[2 * c + k] == kEmpty) slot = &hot16[2 * c + k];
+        if (slot) {
+          *slot = ((e >> 42) << 32) | key16(a, b);
+          continue;
+        }
+        const uint32_t b1 = h & (kBloomBits - 1), b2 = g >> 14;
+        bloom16[b1 >> 5] |= 1u << (b1 & 31);
+        bloom16[b2 >> 5] |= 1u << (b2 & 31);
+      }
+    }
   }
   lap("lds_image");
   // rank monotonicity ("proper"): every merge consuming z ranks after every merge producing z
@@ -978,6 +1023,10 @@ DeviceState* device_state(ctok* t, int device) {
   hipStream_t s = ds->stream;
   upload(ds->merge_tab, t->merge_tab.data(), t->merge_tab.size(), s);
   upload(ds->lds_image, t->lds_image.data(), t->lds_image.size(), s);
+  if (t->narrow) {
+    upload(ds->lds16_image, t->lds16_image.data(), t->lds16_image.size(), s);
+    upload(ds->merge16, t->merge16.data(), t->merge16.size(), s);
+  }
   upload(ds->pair0, t->pair0.data(), t->pair0.size(), s);
   upload(ds->rank_newid, t->rank_newid.data(), t->rank_newid.size(), s);
   upload(ds->piece_tab, t->piece_tab.data(), t->piece_tab.size(), s);
@@ -1002,6 +1051,9 @@ DeviceState* device_state(ctok* t, int device) {
   tb.merge_mask = t->merge_mask;
   tb.lds_image = (const uint4*)ds->lds_image.p;
   tb.pair0 = ds->pair0.p;
+  tb.lds16_image = (const uint4*)ds->lds16_image.p;
+  tb.merge16 = ds->merge16.p;
+  tb.merge16_mask = t->merge16_mask;
   tb.piece_tab = (const uint4*)ds->piece_tab.p;
   tb.piece_mask = t->piece_mask;
   tb.rank_newid = ds->rank_newid.p;
@@ -1026,6 +1078,7 @@ DeviceState* device_state(ctok* t, int device) {
   tb.n_at = (uint32_t)t->at_id.size();
   tb.proper = (t->proper && !getenv("CTOK_FORCE_IMPROPER")) ? 1 : 0;
   tb.compact = t->compact ? 1 : 0;
+  tb.narrow = (t->narrow && !getenv("CTOK_FORCE_WIDE_SLOTS")) ? 1 : 0;
   tb.dbg = getenv("CTOK_DBG_MODE") ? (uint32_t)atoi(getenv("CTOK_DBG_MODE")) : 0;
   DeviceState* r = ds.get();
   t->devs[device] = std::move(ds);

@@ -104,6 +104,22 @@ constexpr uint32_t kBloomWords = kBloomBits / 32;
 constexpr uint32_t kLdsImageBytes = kHotU64 * 8 + kBloomWords * 4;
 constexpr uint32_t kSortCap = 8192;  // merge-pass chunk entries sorted by length bucket (u16 in LDS)
 
+// Narrow vocabularies (every id < 2^16, Tables::narrow): the register merge passes use a second
+// set of pair tables keyed by the 32-bit pair key a << 16 | b, whose lookups cost about half the
+// VALU of the 42-bit ones above.  Entries are u64 value << 32 | key; ~0 = empty (no id is 0xFFFF).
+//   LDS image (kLdsImageBytes): hot table of kHotBuckets buckets of two entries, a pair in bucket
+//   hash16_h >> 20 or hash16_g >> 20; then a Bloom filter (kBloomBits) over the other entries,
+//   bits hash16_h & (kBloomBits - 1) and hash16_g >> 14.
+//   Global table (merge16, load <= 1/8): open addressing from hash16_h & mask.
+__host__ __device__ inline uint32_t key16(uint32_t a, uint32_t b) { return (a << 16) | b; }
+__host__ __device__ inline uint32_t hash16_h(uint32_t a, uint32_t b) {
+  const uint32_t h = mul24(a, 0x9E3779u) + mul24(b, 0x85EBCBu);
+  return h ^ (h >> 13);
+}
+__host__ __device__ inline uint32_t hash16_g(uint32_t a, uint32_t b) {
+  return mul24(b, 0xC2B2AFu) + mul24(a ^ 0x5A5Au, 0x27D4EBu);
+}
+
 // Whole-piece table: raw byte strings of <= 8 bytes whose BPE is exactly one token (checked at
 // load time by running the merge loop on every vocab entry).  Entry = {lo32, hi32, len, id} of
 // the zero-padded bytes; len == 0 marks an empty slot.
@@ -120,6 +136,9 @@ struct Tables {            // device pointers, owned by the host runtime
   const uint4* lds_image;  // hot table + Bloom filter (kLdsImageBytes), copied to LDS by the merge passes;
                            // then the Bloom filter of all pairs (kBloomWords u32)
   const uint32_t* pair0;   // [256 * 256] merge-table value of the byte pair (a, b), kNoRank if none
+  const uint4* lds16_image;  // narrow: hot table + Bloom filter of the 32-bit-key tables (see key16)
+  const uint64_t* merge16;   // narrow: global table, value << 32 | key16
+  uint32_t merge16_mask;
   const uint4* piece_tab;  // whole-piece table (see piece_hash), piece_mask + 2 slots (the last stays empty)
   uint32_t piece_mask;
   const uint32_t* rank_newid;
@@ -145,6 +164,7 @@ struct Tables {            // device pointers, owned by the host runtime
   uint32_t n_at;
   uint32_t proper;          // 1: merge table is rank-monotone (parallel same-rank rounds exact)
   uint32_t compact;         // 1: entry values are new ids (strictly increasing in rank), else ranks
+  uint32_t narrow;          // 1: every vocab id < 2^16 (the merge passes keep the last tier's tokens as u16 in LDS)
   uint32_t dbg;             // debug mode (CTOK_DBG_MODE), 0 in production
 };
 

@@ -860,6 +860,81 @@ __device__ __forceinline__ uint32_t rank_lds(const PairLds& P, uint32_t a, uint3
   return v;
 }
 
+// One pair lookup of a merge pass, split in two so that the global-table load (issued by
+// start, only when the LDS stage cannot decide) overlaps the caller's other work before finish.
+// NARROW = false: the 42-bit-key tables (mhash / mhash2); true: the 32-bit-key tables (key16,
+// ctok_internal.h), whose hashes and bucket compares take about half the VALU.
+template <bool NARROW, bool HOT> struct Probe;
+
+template <bool HOT>
+struct Probe<false, HOT> {
+  uint32_t a, b, h, r;
+  uint64_t e;
+  bool g;
+  __device__ __forceinline__ void start(const Tables& t, const PairLds& P, uint32_t a_, uint32_t b_, bool live) {
+    a = a_;
+    b = b_;
+    h = mhash(a, b);
+    r = rank_lds<HOT>(P, a, b, h, mhash2(h), g);
+    g = g && live;
+    e = 0;
+    if (g) e = t.merge_tab[h & t.merge_mask];
+  }
+  __device__ __forceinline__ uint32_t finish(const Tables& t, uint32_t* err) {
+    if (g) r = resolve_rank(t, pair_key(a, b), h & t.merge_mask, e, err);
+    return r;
+  }
+};
+
+template <bool HOT>
+struct Probe<true, HOT> {
+  uint32_t k, h, r;
+  uint64_t e;
+  bool g;
+  __device__ __forceinline__ void start(const Tables& t, const PairLds& P, uint32_t a, uint32_t b, bool live) {
+    a &= 0xFFFFu;  // (ids < 2^16; known to the compiler, the hashes use 24-bit multiplies)
+    b &= 0xFFFFu;
+    k = key16(a, b);
+    h = hash16_h(a, b);
+    const uint32_t h2 = hash16_g(a, b);
+    const uint32_t b1 = h & (kBloomBits - 1), b2 = h2 >> 14;
+    const uint32_t f = (P.bloom[b1 >> 5] >> (b1 & 31)) & (P.bloom[b2 >> 5] >> (b2 & 31)) & 1u;
+    const uint32_t c1 = 2 * (h >> 20), c2 = 2 * (h2 >> 20);
+    const uint64_t x0 = P.hot[c1], x1 = P.hot[c1 + 1], y0 = P.hot[c2], y1 = P.hot[c2 + 1];
+    uint32_t v = kNoRank;
+    bool hit = false;
+    auto chk = [&](uint64_t x) {
+      const bool m = (uint32_t)x == k;
+      v = m ? (uint32_t)(x >> 32) : v;
+      hit |= m;
+    };
+    chk(x0);
+    chk(x1);
+    chk(y0);
+    chk(y1);
+    r = v;
+    g = !hit && f && live;
+    e = 0;
+    if (g) e = t.merge16[h & t.merge16_mask];
+  }
+  __device__ __forceinline__ uint32_t finish(const Tables& t, uint32_t* err) {
+    if (g) {
+      uint32_t s = h & t.merge16_mask;
+      for (;;) {
+        if ((uint32_t)e == k) {
+          r = (uint32_t)(e >> 32);
+          if (value_panics(t, r)) { atomicOr(err, kErrPanic); r = kNoRank; }
+          break;
+        }
+        if (e == kEmpty) { r = kNoRank; break; }
+        s = (s + 1) & t.merge16_mask;
+        e = t.merge16[s];
+      }
+    }
+    return r;
+  }
+};
+
 template <int N> struct LdsClass;
 template <> struct LdsClass<8> { static constexpr int cls = 0; static constexpr uint32_t cap = kCap0; };
 template <> struct LdsClass<16> { static constexpr int cls = 1; static constexpr uint32_t cap = kCap1; };
@@ -876,7 +951,7 @@ __device__ __forceinline__ const uint32_t* class_list(const Work& w) {
 // merged, the slots right of it shift left by one, the two new pairs' ranks are looked up.
 // Returns true when it stopped because the piece shrank to <= stop tokens (the caller continues
 // on fewer slots), false when no pair can merge.  Slots >= m hold kDead / kNoRank.
-template <int N, bool COMPACT, bool HOT>
+template <int N, bool COMPACT, bool HOT, bool NARROW>
 __device__ __forceinline__ bool merge_slots(const Tables& t, const PairLds& P, uint32_t* tk, uint32_t* rk,
                                             uint32_t& m, uint32_t stop, uint32_t* err) {
   for (;;) {
@@ -894,15 +969,9 @@ __device__ __forceinline__ bool merge_slots(const Tables& t, const PairLds& P, u
       R = ((uint32_t)k == bi + 2) ? tk[k] : R;
     }
     const bool has_l = bi > 0, has_r = bi + 2 < m;
-    const uint32_t hl1 = mhash(L, nid), hr1 = mhash(nid, R);
-    bool gl, gr;
-    uint32_t rl = rank_lds<HOT>(P, L, nid, hl1, mhash2(hl1), gl);
-    uint32_t rr = rank_lds<HOT>(P, nid, R, hr1, mhash2(hr1), gr);
-    gl = gl && has_l;
-    gr = gr && has_r;
-    uint64_t el = 0, er = 0;
-    if (gl) el = t.merge_tab[hl1 & t.merge_mask];
-    if (gr) er = t.merge_tab[hr1 & t.merge_mask];
+    Probe<NARROW, HOT> pl, pr;
+    pl.start(t, P, L, nid, has_l);
+    pr.start(t, P, nid, R, has_r);
 #pragma unroll
     for (int k = 0; k < N; k++) {  // ascending: tk[k+1] is read before it is overwritten
       const uint32_t nxt_t = k + 1 < N ? tk[k + 1] : kDead;
@@ -912,14 +981,72 @@ __device__ __forceinline__ bool merge_slots(const Tables& t, const PairLds& P, u
       rk[k] = gt ? nxt_r : rk[k];
     }
     m--;
-    if (gl) rl = resolve_rank(t, pair_key(L, nid), hl1 & t.merge_mask, el, err);
-    if (gr) rr = resolve_rank(t, pair_key(nid, R), hr1 & t.merge_mask, er, err);
-    rl = has_l ? rl : kNoRank;
-    rr = has_r ? rr : kNoRank;
+    const uint32_t rl = has_l ? pl.finish(t, err) : kNoRank;
+    const uint32_t rr = has_r ? pr.finish(t, err) : kNoRank;
 #pragma unroll
     for (int k = 0; k < N - 1; k++)
       rk[k] = ((uint32_t)k + 1 == bi) ? rl : (((uint32_t)k == bi) ? rr : rk[k]);
   }
+}
+
+// The last tier (<= 8 tokens) with the working state in LDS instead of registers: positions stay
+// fixed, a live mask says which slots still hold a token, and slot s keeps the key
+// rank << 3 | s of the pair its token starts (~0 when the slot is dead or last).  A merge then
+// reads the keys (four ds_read2st64, a v_min tree), writes three keys and one token, and reads its
+// two neighbours by index; the register tiers' N-wide select / shift chains (~100 VALU per merge
+// at N = 8) are gone.  Tokens are u16 (narrow vocabularies: every id < 2^16), so 960 threads'
+// state (48 B each) fits beside the 96 KiB image.  Pair lookups use the 32-bit-key tables.
+//   keys:   s_key[s * NT + tid] (u32; read two at a time with ds_read2st64)
+//   tokens: s_tok[s * NT + tid] (u16)
+// Semantics are merge_slots': the lowest (rank, position) pair merges (src/bpe.rs:118-149).
+typedef __attribute__((address_space(3))) uint16_t lds_u16;
+
+// out_of(m) returns where the piece's m ids go (called once, after the last merge).
+template <bool COMPACT, bool HOT, uint32_t NT, typename OutOf>
+__device__ __forceinline__ uint32_t merge_lds8(const Tables& t, const PairLds& P, const uint32_t* tk, const uint32_t* rk,
+                                               uint32_t m, lds_u32* s_key, lds_u16* s_tok, uint32_t* err,
+                                               OutOf&& out_of) {
+  const uint32_t tid = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    s_key[k * NT + tid] = (uint32_t)k + 1 < m ? (rk[k] << 3) | (uint32_t)k : ~0u;
+    s_tok[k * NT + tid] = (uint16_t)tk[k];
+  }
+  // live slots, with a sentinel at bit 8 (so every "next live" search finds a bit)
+  uint32_t lv = ((1u << m) - 1u) | 0x100u;
+  for (;;) {
+    uint32_t kk[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) kk[k] = s_key[k * NT + tid];
+    const uint32_t best = min(min(min(kk[0], kk[1]), min(kk[2], kk[3])), min(min(kk[4], kk[5]), min(kk[6], kk[7])));
+    if (best >= (kNoRank << 3)) break;
+    const uint32_t bi = best & 7u, r = best >> 3;
+    // (ids < 2^16: the mask lets the hashes use 24-bit multiplies)
+    const uint32_t nid = (COMPACT ? r : t.rank_newid[r]) & 0xFFFFu;
+    const uint32_t p = bi + 1 + (uint32_t)__builtin_ctz(lv >> (bi + 1));  // the right token's slot
+    const uint32_t q = p + 1 + (uint32_t)__builtin_ctz(lv >> (p + 1));    // the token after it (8: none)
+    const bool has_r = q < 8;
+    const uint32_t lo = lv & ((1u << bi) - 1u);
+    const bool has_l = lo != 0;
+    const uint32_t pv = 31u - (uint32_t)__builtin_clz(lo | 1u);           // the token before
+    const uint32_t L = s_tok[pv * NT + tid], R = s_tok[min(q, 7u) * NT + tid];
+    s_tok[bi * NT + tid] = (uint16_t)nid;
+    s_key[p * NT + tid] = ~0u;
+    lv &= ~(1u << p);
+    m--;
+    Probe<true, HOT> pl, pr;
+    pl.start(t, P, L, nid, has_l);
+    pr.start(t, P, nid, R, has_r);
+    const uint32_t rl = pl.finish(t, err), rr = pr.finish(t, err);
+    if (has_l) s_key[pv * NT + tid] = (rl << 3) | pv;
+    s_key[bi * NT + tid] = has_r ? (rr << 3) | bi : ~0u;
+  }
+  // live tokens in slot order to out[0 .. m)
+  uint32_t* out = out_of(m);
+#pragma unroll
+  for (int k = 0; k < 8; k++)
+    if ((lv >> k) & 1u) out[__popc(lv & ((1u << k) - 1u))] = s_tok[k * NT + tid];
+  return m;
 }
 
 // Workgroup-shared scratch of a merge pass.
@@ -936,9 +1063,11 @@ struct PassLds {
 // `load` fills the workgroup's LDS tables (image, byte -> id); it runs at the first chunk with
 // work, so a workgroup that finds only empty lists never reads the 32..96 KiB image (`loaded`
 // is shared by the passes of one kernel).
-template <int N, bool COMPACT, bool HOT, uint32_t NT, uint32_t SORTCAP, typename Load>
+// L8: the <= 8-token tier runs in LDS (merge_lds8, narrow vocabularies; s_key / s_tok its state).
+template <int N, bool COMPACT, bool HOT, uint32_t NT, uint32_t SORTCAP, bool L8 = false, typename Load>
 __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const PairLds& P, const int32_t* s_b2id,
-                                           PassLds<SORTCAP>& S, bool& loaded, Load&& load) {
+                                           PassLds<SORTCAP>& S, bool& loaded, Load&& load,
+                                           lds_u32* s_key = nullptr, lds_u16* s_tok = nullptr) {
   using LC = LdsClass<N>;
   constexpr int K = 64;
   const uint32_t tid = threadIdx.x;
@@ -1073,21 +1202,29 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
       uint32_t m = n;
       // tiers: N slots while the piece has more than N/2 tokens, then N/2, ... down to 8 slots
       bool more = true;
-      if constexpr (N >= 64) more = merge_slots<64, COMPACT, HOT>(t, P, tk, rk, m, 32, err);
+      if constexpr (N >= 64) more = merge_slots<64, COMPACT, HOT, L8>(t, P, tk, rk, m, 32, err);
       if constexpr (N >= 32) {
-        if (more) more = merge_slots<32, COMPACT, HOT>(t, P, tk, rk, m, 16, err);
+        if (more) more = merge_slots<32, COMPACT, HOT, L8>(t, P, tk, rk, m, 16, err);
       }
       if constexpr (N >= 16) {
-        if (more) more = merge_slots<16, COMPACT, HOT>(t, P, tk, rk, m, 8, err);
+        if (more) more = merge_slots<16, COMPACT, HOT, L8>(t, P, tk, rk, m, 8, err);
       }
-      if (more) merge_slots<8, COMPACT, HOT>(t, P, tk, rk, m, 0, err);
       // ids go to the next free slots of the tile's region for this class (dense: a wave's
       // stores fill whole lines), the record points at them
-      const uint32_t pos = atomicAdd(&S.tsum[kt], m);
-      uint32_t* out = w.scratch + (size_t)tile * kTileSlots + pos;
+      uint32_t pos = 0;
+      auto out_of = [&](uint32_t mm) {
+        pos = atomicAdd(&S.tsum[kt], mm);
+        return w.scratch + (size_t)tile * kTileSlots + pos;
+      };
+      if (L8 && more) {
+        m = merge_lds8<COMPACT, HOT, NT>(t, P, tk, rk, m, s_key, s_tok, err, out_of);
+      } else {
+        if (!L8 && more) merge_slots<8, COMPACT, HOT, L8>(t, P, tk, rk, m, 0, err);
+        uint32_t* out = out_of(m);
 #pragma unroll
-      for (int k = 0; k < N; k++)
-        if ((uint32_t)k < m) out[k] = tk[k];
+        for (int k = 0; k < N; k++)
+          if ((uint32_t)k < m) out[k] = tk[k];
+      }
       w.tcnt[(size_t)tile * kTileSlots + j] = rec_short(m, pos) | ((e & kEntDoc) ? kRecDoc : 0u);
       st_bytes += n;
       st_ids += m;
@@ -1113,23 +1250,32 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
   __syncthreads();
 }
 
-// Pieces of <= 16 bytes (classes 0 and 1): one 1024-thread workgroup per CU holding the whole
-// LDS image (hot table + Bloom filter); a workgroup moves on to class 1 as soon as class 0 has
-// no chunk left, with no kernel boundary in between.
-template <bool COMPACT>
+// Pieces of <= 16 bytes (classes 0 and 1): one workgroup per CU holding the whole LDS image
+// (hot table + Bloom filter); a workgroup moves on to class 1 as soon as class 0 has no chunk
+// left, with no kernel boundary in between.  NARROW (every id < 2^16): 960 threads, the last
+// tier's state in LDS (merge_lds8); else 1024 threads, all tiers in registers.
+template <bool NARROW> struct ShortCfg { static constexpr uint32_t NT = NARROW ? 960 : 1024; };
+
+template <bool COMPACT, bool NARROW>
 __global__ __launch_bounds__(1024) void k_bpe_short(Work w, Tables t) {
+  constexpr uint32_t NT = ShortCfg<NARROW>::NT;
   extern __shared__ __attribute__((aligned(16))) uint4 s_img[];
   __shared__ int32_t s_b2id[256];
   __shared__ PassLds<kSortCap> S;
+  __shared__ uint32_t s_key[NARROW ? 8 * NT : 1];
+  __shared__ uint16_t s_tok[NARROW ? 8 * NT : 1];
   const uint32_t tid = threadIdx.x;
+  const uint4* img = NARROW ? t.lds16_image : t.lds_image;
   auto load = [&] {
-    for (uint32_t i = tid; i < kLdsImageBytes / 16; i += 1024) s_img[i] = t.lds_image[i];
-    for (uint32_t i = tid; i < 256; i += 1024) s_b2id[i] = t.byte2id[i];
+    for (uint32_t i = tid; i < kLdsImageBytes / 16; i += NT) s_img[i] = img[i];
+    for (uint32_t i = tid; i < 256; i += NT) s_b2id[i] = t.byte2id[i];
   };
   bool loaded = false;
   const PairLds P{(const lds_u64*)s_img, (const lds_u32*)(s_img + kHotBuckets)};
-  class_pass<8, COMPACT, true, 1024, kSortCap>(w, t, P, s_b2id, S, loaded, load);
-  class_pass<16, COMPACT, true, 1024, kSortCap>(w, t, P, s_b2id, S, loaded, load);
+  lds_u32* sk = (lds_u32*)s_key;
+  lds_u16* st = (lds_u16*)s_tok;
+  class_pass<8, COMPACT, true, NT, kSortCap, NARROW>(w, t, P, s_b2id, S, loaded, load, sk, st);
+  class_pass<16, COMPACT, true, NT, kSortCap, NARROW>(w, t, P, s_b2id, S, loaded, load, sk, st);
 }
 
 // Pieces of 17..32 bytes (CLS = 2, on the main stream after k_bpe_short) or 33..64 bytes (CLS = 3,
@@ -1140,47 +1286,59 @@ __global__ __launch_bounds__(1024) void k_bpe_short(Work w, Tables t) {
 // main stream after class 2; both instances take chunks from the same counter, so a handful of
 // class-3 pieces (long merge chains) is done by the side instance in the shadow of the main
 // stream's passes, and a large class 3 (multilingual text) is shared by both as CUs free up.
-template <bool COMPACT, int CLS>
+template <bool COMPACT, int CLS, bool NARROW>
 __global__ __launch_bounds__(512) void k_bpe_mid(Work w, Tables t) {
   extern __shared__ __attribute__((aligned(16))) uint4 s_img[];
   __shared__ int32_t s_b2id[256];
   __shared__ PassLds<kSortCap> S;
+  __shared__ uint32_t s_key[NARROW ? 8 * 512 : 1];
+  __shared__ uint16_t s_tok[NARROW ? 8 * 512 : 1];
   // (the image is loaded up front: a lazy load pushes the 64-slot pass into scratch; the kernel
   // returns at once when k_segment found no piece of its class)
   if (w.counters[CLS == 2 ? kCtrAnyMid : kCtrAnyC3] == 0) return;
   if (__atomic_load_n(&w.counters[ctr_chunk(CLS)], __ATOMIC_RELAXED) * 64ull >= w.n_tiles) return;
   const uint32_t tid = threadIdx.x;
-  for (uint32_t i = tid; i < kLdsImageBytes / 16; i += 512) s_img[i] = t.lds_image[i];
+  const uint4* img = NARROW ? t.lds16_image : t.lds_image;
+  for (uint32_t i = tid; i < kLdsImageBytes / 16; i += 512) s_img[i] = img[i];
   for (uint32_t i = tid; i < 256; i += 512) s_b2id[i] = t.byte2id[i];
   bool loaded = true;
   const PairLds P{(const lds_u64*)s_img, (const lds_u32*)(s_img + kHotBuckets)};
-  class_pass<CLS == 2 ? 32 : 64, COMPACT, true, 512, kSortCap>(w, t, P, s_b2id, S, loaded, [] {});
+  class_pass<CLS == 2 ? 32 : 64, COMPACT, true, 512, kSortCap, NARROW>(w, t, P, s_b2id, S, loaded, [] {},
+                                                                     (lds_u32*)s_key, (lds_u16*)s_tok);
 }
 
+template <bool C, int CLS, bool NW>
+static hipError_t launch_mid_t(const Work& w, const Tables& t, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    HIPCHK(hipFuncSetAttribute((const void*)k_bpe_mid<C, CLS, NW>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)kLdsImageBytes));
+    attr = true;
+  }
+  if (!w.n_tiles) return hipSuccess;
+  k_bpe_mid<C, CLS, NW><<<min((w.n_tiles + 63) / 64, w.n_cus), 512, kLdsImageBytes, s>>>(w, t);
+  return hipGetLastError();
+}
 template <bool C, int CLS>
 static hipError_t launch_mid(const Work& w, const Tables& t, hipStream_t s) {
-  static bool attr = false;
-  if (!attr) {
-    HIPCHK(hipFuncSetAttribute((const void*)k_bpe_mid<C, CLS>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)kLdsImageBytes));
-    attr = true;
-  }
-  if (!w.n_tiles) return hipSuccess;
-  k_bpe_mid<C, CLS><<<min((w.n_tiles + 63) / 64, w.n_cus), 512, kLdsImageBytes, s>>>(w, t);
-  return hipGetLastError();
+  return t.narrow ? launch_mid_t<C, CLS, true>(w, t, s) : launch_mid_t<C, CLS, false>(w, t, s);
 }
 
-template <bool C>
-static hipError_t launch_short(const Work& w, const Tables& t, hipStream_t s) {
+template <bool C, bool NW>
+static hipError_t launch_short_t(const Work& w, const Tables& t, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
-    HIPCHK(hipFuncSetAttribute((const void*)k_bpe_short<C>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    HIPCHK(hipFuncSetAttribute((const void*)k_bpe_short<C, NW>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)kLdsImageBytes));
     attr = true;
   }
   if (!w.n_tiles) return hipSuccess;
-  k_bpe_short<C><<<min((w.n_tiles + 63) / 64, w.n_cus), 1024, kLdsImageBytes, s>>>(w, t);
+  k_bpe_short<C, NW><<<min((w.n_tiles + 63) / 64, w.n_cus), ShortCfg<NW>::NT, kLdsImageBytes, s>>>(w, t);
   return hipGetLastError();
+}
+template <bool C>
+static hipError_t launch_short(const Work& w, const Tables& t, hipStream_t s) {
+  return t.narrow ? launch_short_t<C, true>(w, t, s) : launch_short_t<C, false>(w, t, s);
 }
 
 hipError_t launch_bpe_class(const Work& w, const Tables& t, int cls, hipStream_t s) {
