@@ -23,8 +23,8 @@ import numpy as np
 from . import _native as _n
 
 __version__ = "0.3.3"
-__all__ = ["Tokenizer", "Encoding", "BatchEncoding", "PanicException", "UnsupportedConfigError", "DeviceError",
-           "__version__"]
+__all__ = ["Tokenizer", "Trainer", "Encoding", "BatchEncoding", "PanicException", "UnsupportedConfigError",
+           "DeviceError", "__version__"]
 
 
 class PanicException(BaseException):
@@ -150,6 +150,7 @@ def _split_lists(flat: np.ndarray, off: np.ndarray) -> list:
 
 
 from .encoding import BatchEncoding, Encoding  # noqa: E402
+from .trainer import Trainer  # noqa: E402
 
 
 class Tokenizer:

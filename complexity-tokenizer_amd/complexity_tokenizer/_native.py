@@ -105,6 +105,15 @@ class PadOpts(ctypes.Structure):
     _fields_ = [("flags", ctypes.c_uint32), ("pad_id", ctypes.c_uint32), ("max_length", ctypes.c_uint64)]
 
 
+class TrainerConfig(ctypes.Structure):  # include/ctok_trainer.h
+    _fields_ = [("vocab_size", ctypes.c_uint64), ("min_frequency", ctypes.c_uint32),
+                ("min_word_length", ctypes.c_uint64), ("inl_alpha", ctypes.c_float), ("inl_beta", ctypes.c_float),
+                ("inl_gate", ctypes.c_float), ("inl_mu_target", ctypes.c_float),
+                ("inl_velocity_max", ctypes.c_float), ("inl_beta_max", ctypes.c_float),
+                ("special", ctypes.c_char_p), ("special_off", ctypes.POINTER(ctypes.c_uint64)),
+                ("n_special", ctypes.c_uint64), ("device", ctypes.c_int)]
+
+
 _p = ctypes.c_void_p
 _u64 = ctypes.c_uint64
 _u64p = ctypes.POINTER(ctypes.c_uint64)
@@ -142,6 +151,19 @@ SIGS = {
                                          ctypes.POINTER(DecodeStats)]),
     "ctok_decode_batch_device": (ctypes.c_int, [_p, _p, _p, _u64, _u64, ctypes.c_uint32, _p, _u64, _p, _u64p,
                                                 ctypes.POINTER(Exec), ctypes.POINTER(DecodeStats)]),
+    # include/ctok_trainer.h
+    "ctok_trainer_create": (ctypes.c_int, [ctypes.POINTER(TrainerConfig), ctypes.POINTER(_p)]),
+    "ctok_trainer_destroy": (None, [_p]),
+    "ctok_trainer_count": (ctypes.c_int, [_p, _p, _p, _u64, ctypes.c_int]),
+    "ctok_trainer_train": (ctypes.c_int, [_p, ctypes.c_int]),
+    "ctok_trainer_train_words": (ctypes.c_int, [_p, _p, _p, _p, _u64]),
+    "ctok_trainer_vocab_size": (_u64, [_p]),
+    "ctok_trainer_num_merges": (_u64, [_p]),
+    "ctok_trainer_json": (ctypes.c_int, [_p, ctypes.c_char_p, _sz, ctypes.POINTER(_sz)]),
+    "ctok_trainer_save": (ctypes.c_int, [_p, ctypes.c_char_p]),
+    "ctok_trainer_initial_pairs": (ctypes.c_int, [_p, _p, _p, _p, _u64, _u64p]),
+    "ctok_trainer_timing": (ctypes.c_int, [_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                           ctypes.POINTER(ctypes.c_double)]),
 }
 
 for _name, (_res, _args) in SIGS.items():

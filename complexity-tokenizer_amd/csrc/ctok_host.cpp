@@ -1119,7 +1119,7 @@ double now_ms() {
 // The pipeline on device-resident buffers.  Returns the token count.
 uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const uint64_t* d_off, uint64_t n_docs,
                        uint64_t n_bytes, uint32_t* d_ids, uint64_t ids_cap, uint64_t* d_tok_off, hipStream_t s,
-                       bool timing, ctok_stats* st, bool split_added = true) {
+                       bool timing, ctok_stats* st, bool split_added = true, bool segment_only = false) {
   if (n_bytes >= 0xF0000000ull) throw_err(CTOK_E_ARG, "a single call is limited to < 3.75 GiB of text; split the batch");
   if (n_docs >= 0xF0000000ull) throw_err(CTOK_E_ARG, "too many documents in one call");
   // split_added = false: encode_to_encoding's words go straight to BpeTokenizer::encode, with
@@ -1238,6 +1238,15 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   if (timing) HIPTRY(hipEventRecord(ds->ev[7], s));
   STEP("segment", launch_segment(w, tb, s));
   if (timing) HIPTRY(hipEventRecord(ds->ev[1], s));
+  if (segment_only) {  // pre-tokenization only (the trainer's word counting): pbits of the text
+    HIPTRY(hipMemcpyAsync(ds->host + 1, ds->counters.p, kNumCounters * 4, hipMemcpyDeviceToHost, s));
+    spin_sync(ds, s);
+    if (speculate && ((volatile uint32_t*)(ds->host + 1))[12]) {
+      speculate = false;
+      continue;
+    }
+    return 0;
+  }
   HIPTRY(hipEventRecord(ds->ev_fork, s));
   HIPTRY(hipStreamWaitEvent(ds->side, ds->ev_fork, 0));
   STEP("bpe_long", launch_bpe_long(w, tb, ds->side));
@@ -1600,6 +1609,55 @@ RangeOut encode_host_range(ctok* t, DeviceState* ds, const uint8_t* text, const 
 }
 
 }  // namespace
+
+// ----------------------------------------------------------------------------- internal API
+// for trainer_host.cpp (host_common.h): errors, and the GPU pre-tokenizer of a host batch
+
+namespace {
+int run(const std::function<void()>& f);
+}
+
+namespace ctok_host {
+[[noreturn]] void throw_error(int code, const std::string& msg) { throw_err(code, msg); }
+int run_guarded(const std::function<void()>& f) { return run(f); }
+
+// NFC (when the tokenizer normalises) + ByteLevel pre-tokenization of n_docs host texts on device
+// dev: the text the pieces index (normalised when normalisation ran), its doc offsets, and the
+// piece-start bitmap (bit g = a piece starts at byte g).
+void pretokenize(ctok* t, int dev, const uint8_t* utf8, const uint64_t* doc_off, uint64_t n_docs,
+                 std::vector<uint8_t>& text, std::vector<uint64_t>& off, std::vector<uint32_t>& pbits) {
+  if (doc_off[0] != 0) throw_err(CTOK_E_ARG, "offsets[0] must be 0");
+  for (uint64_t d = 0; d < n_docs; d++)
+    if (doc_off[d + 1] < doc_off[d]) throw_err(CTOK_E_ARG, "offsets must be non-decreasing");
+  const uint64_t n_in = doc_off[n_docs];
+  if (n_in && !utf8) throw_err(CTOK_E_ARG, "null text");
+  DeviceState* ds = device_state(t, dev);
+  std::lock_guard<std::mutex> lk(ds->mu);
+  HIPTRY(hipSetDevice(dev));
+  hipStream_t s = ds->stream;
+  ds->pad_in_text.ensure(n_in + 16);
+  ds->pad_in_off.ensure(n_docs + 1);
+  if (n_in) HIPTRY(hipMemcpyAsync(ds->pad_in_text.p, utf8, n_in, hipMemcpyHostToDevice, s));
+  HIPTRY(hipMemsetAsync(ds->pad_in_text.p + n_in, 0, 16, s));
+  HIPTRY(hipMemcpyAsync(ds->pad_in_off.p, doc_off, (n_docs + 1) * 8, hipMemcpyHostToDevice, s));
+  encode_device(t, ds, ds->pad_in_text.p, ds->pad_in_off.p, n_docs, n_in, nullptr, 0, nullptr, s, false, nullptr, true,
+                true);
+  const uint64_t B = ds->last_B;
+  pbits.assign((B + 31) / 32, 0);
+  off.resize(n_docs + 1);
+  text.resize(B);
+  if (!pbits.empty()) HIPTRY(hipMemcpyAsync(pbits.data(), ds->pbits.p, pbits.size() * 4, hipMemcpyDeviceToHost, s));
+  if (ds->last_norm) {
+    if (B) HIPTRY(hipMemcpyAsync(text.data(), ds->norm_text.p, B, hipMemcpyDeviceToHost, s));
+    HIPTRY(hipMemcpyAsync(off.data(), ds->norm_off.p, (n_docs + 1) * 8, hipMemcpyDeviceToHost, s));
+  }
+  HIPTRY(hipStreamSynchronize(s));
+  if (!ds->last_norm) {
+    if (B) std::memcpy(text.data(), utf8, B);
+    std::memcpy(off.data(), doc_off, (n_docs + 1) * 8);
+  }
+}
+}  // namespace ctok_host
 
 // ----------------------------------------------------------------------------- C ABI
 

@@ -19,10 +19,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def test_exports_every_declared_symbol():
-    with open(os.path.join(ROOT, "include", "ctok.h")) as f:
-        hdr = f.read()
+    hdr = ""
+    for h in sorted(os.listdir(os.path.join(ROOT, "include"))):
+        if h.endswith(".h"):
+            with open(os.path.join(ROOT, "include", h)) as f:
+                hdr += f.read()
     names = sorted(set(re.findall(r"\b(ctok_[a-z_0-9]+)\s*\(", hdr)))
-    assert len(names) >= 14
+    assert len(names) >= 25 and "ctok_trainer_train" in names
     lib = ctypes.CDLL(_native.LIB_PATH)
     missing = [n for n in names if not hasattr(lib, n)]
     assert not missing, missing
