@@ -21,6 +21,7 @@ import os
 import numpy as np
 
 from . import _native as _n
+from . import _fast  # the Python-object edges of encode_batch (csrc/pyfast.c); built with libctok.so
 
 __version__ = "0.3.3"
 __all__ = ["Tokenizer", "Trainer", "Encoding", "BatchEncoding", "PanicException", "UnsupportedConfigError",
@@ -63,20 +64,11 @@ def _hub_cache_dir() -> str:
 
 def pack_texts(texts) -> tuple[np.ndarray, np.ndarray]:
     """list[str] -> (utf-8 bytes as uint8 array, uint64 offsets[D+1]).  Mirrors the PyO3
-    `Vec<String>` extraction: a bare str is refused and every element must be a str."""
-    if isinstance(texts, (str, bytes)):
-        raise TypeError("Can't extract `str` to `Vec`")
-    enc = []
-    for t in texts:
-        if not isinstance(t, str):
-            raise TypeError("'%s' object cannot be converted to 'PyString'" % type(t).__name__)
-        enc.append(t.encode("utf-8"))
-    lens = np.fromiter((len(e) for e in enc), dtype=np.uint64, count=len(enc))
-    off = np.zeros(len(enc) + 1, dtype=np.uint64)
-    np.cumsum(lens, out=off[1:])
-    # 16 bytes of padding keep the device-side 16-byte loads inside the allocation
-    buf = np.frombuffer(b"".join(enc) + b"\0" * 16, dtype=np.uint8)
-    return buf, off
+    `Vec<String>` extraction: a bare str is refused and every element must be a str.  One C pass
+    (complexity_tokenizer._fast.pack, csrc/pyfast.c); 16 bytes of padding keep the device-side
+    16-byte loads inside the allocation."""
+    buf, offs = _fast.pack(texts)
+    return np.frombuffer(buf, dtype=np.uint8), np.frombuffer(offs, dtype=np.uint64)
 
 
 def _as_str(t):
@@ -134,16 +126,23 @@ def pack_ids(batch) -> tuple[np.ndarray, np.ndarray]:
     return np.asarray(flat, dtype=np.uint64).astype(np.uint32), off
 
 
+_ID_CACHE: list = []
+
+
 def _split_lists(flat: np.ndarray, off: np.ndarray) -> list:
-    """(flat uint array, offsets[D+1]) -> D Python lists.  The cyclic garbage collector is paused
-    while the lists are built: creating ~1e5 container objects otherwise triggers collections
-    that rescan every list built so far (3x the cost of the conversion itself)."""
+    """(flat uint32 ids, uint64 offsets[D+1]) -> D Python lists, built in C (csrc/pyfast.c) from a
+    shared cache of the int objects 0 .. 2^17 - 1 (ids past it are created per use).  The cyclic
+    garbage collector is paused while the lists are built: creating ~1e5 container objects
+    otherwise triggers collections that rescan every list built so far."""
+    global _ID_CACHE
+    if not _ID_CACHE:
+        _ID_CACHE = list(range(1 << 17))
+    flat = np.ascontiguousarray(flat, dtype=np.uint32)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
     was = gc.isenabled()
     gc.disable()
     try:
-        f = flat.tolist()
-        o = off.tolist()
-        return [f[o[i]:o[i + 1]] for i in range(len(o) - 1)]
+        return _fast.split(flat.ctypes.data, off.ctypes.data, len(off) - 1, _ID_CACHE)
     finally:
         if was:
             gc.enable()

@@ -193,7 +193,8 @@ struct HostPipe {
 struct DeviceState {
   int device = -1;
   uint32_t n_cus = 1;
-  std::mutex mu;
+  std::recursive_mutex mu;  // serialises calls on this device; recursive: ctok_encode_padded holds it
+                            // across its nested ctok_encode_padded_device call
   hipStream_t stream = nullptr;
   hipEvent_t ev[12] = {};
   hipEvent_t ev_sync = nullptr;   // spin-waited completion marker (no blocking-wait wakeup latency)
@@ -1119,7 +1120,8 @@ double now_ms() {
 // The pipeline on device-resident buffers.  Returns the token count.
 uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const uint64_t* d_off, uint64_t n_docs,
                        uint64_t n_bytes, uint32_t* d_ids, uint64_t ids_cap, uint64_t* d_tok_off, hipStream_t s,
-                       bool timing, ctok_stats* st, bool split_added = true, bool segment_only = false) {
+                       bool timing, ctok_stats* st, bool split_added = true, bool segment_only = false,
+                       bool keep_first = false) {
   if (n_bytes >= 0xF0000000ull) throw_err(CTOK_E_ARG, "a single call is limited to < 3.75 GiB of text; split the batch");
   if (n_docs >= 0xF0000000ull) throw_err(CTOK_E_ARG, "too many documents in one call");
   // split_added = false: encode_to_encoding's words go straight to BpeTokenizer::encode, with
@@ -1186,6 +1188,7 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   w.n_tiles = (uint32_t)((B + kTile - 1) / kTile);
   w.n_cus = ds->n_cus;
   w.nfc_watch = speculate ? 1u : 0u;
+  w.keep_first = keep_first ? 1u : 0u;
   const size_t nt = w.n_tiles;
   ds->docbits.ensure(w.n_words + 8);
   ds->pbits.ensure(w.n_words + 8);
@@ -1632,7 +1635,7 @@ void pretokenize(ctok* t, int dev, const uint8_t* utf8, const uint64_t* doc_off,
   const uint64_t n_in = doc_off[n_docs];
   if (n_in && !utf8) throw_err(CTOK_E_ARG, "null text");
   DeviceState* ds = device_state(t, dev);
-  std::lock_guard<std::mutex> lk(ds->mu);
+  std::lock_guard<std::recursive_mutex> lk(ds->mu);
   HIPTRY(hipSetDevice(dev));
   hipStream_t s = ds->stream;
   ds->pad_in_text.ensure(n_in + 16);
@@ -1761,7 +1764,7 @@ int ctok_encode_batch_device(const ctok* tc, const uint8_t* d_utf8, const uint64
     double t0 = now_ms();
     int dev = exec ? exec->device : 0;
     DeviceState* ds = device_state(t, dev);
-    std::lock_guard<std::mutex> lk(ds->mu);
+    std::lock_guard<std::recursive_mutex> lk(ds->mu);
     HIPTRY(hipSetDevice(dev));
     hipStream_t s = exec && exec->stream ? (hipStream_t)exec->stream : ds->stream;
     bool timing = exec && (exec->flags & CTOK_F_TIMING);
@@ -1780,7 +1783,7 @@ int ctok_decode_batch_device(const ctok* tc, const uint32_t* d_ids, const uint64
     double t0 = now_ms();
     int dev = exec ? exec->device : 0;
     DeviceState* ds = device_state(t, dev);
-    std::lock_guard<std::mutex> lk(ds->mu);
+    std::lock_guard<std::recursive_mutex> lk(ds->mu);
     HIPTRY(hipSetDevice(dev));
     hipStream_t s = exec && exec->stream ? (hipStream_t)exec->stream : ds->stream;
     bool timing = exec && (exec->flags & CTOK_F_TIMING);
@@ -1810,7 +1813,7 @@ int ctok_decode_batch(const ctok* tc, const uint32_t* ids, const uint64_t* tok_o
     if (T && !ids) throw_err(CTOK_E_ARG, "null ids");
     int dev = exec ? exec->device : 0;
     DeviceState* ds = device_state(t, dev);
-    std::lock_guard<std::mutex> lk(ds->mu);
+    std::lock_guard<std::recursive_mutex> lk(ds->mu);
     HIPTRY(hipSetDevice(dev));
     hipStream_t s = exec && exec->stream ? (hipStream_t)exec->stream : ds->stream;
     bool timing = exec && (exec->flags & CTOK_F_TIMING);
@@ -1887,7 +1890,7 @@ int ctok_encode_batch(const ctok* tc, const uint8_t* utf8_in, const uint64_t* do
       auto shard = [&](size_t g) {
         try {
           DeviceState* ds = device_state(t, devs[g]);
-          std::lock_guard<std::mutex> lk(ds->mu);
+          std::lock_guard<std::recursive_mutex> lk(ds->mu);
           HIPTRY(hipSetDevice(devs[g]));
           uint32_t* out = ids;
           uint64_t cap = ids_cap;
@@ -2046,7 +2049,7 @@ int ctok_encode_padded_device(const ctok* tc, const uint8_t* d_utf8, const uint6
       throw_err(CTOK_E_UNSUPPORTED, "post-processor template with more than 16 items");
     int dev = exec ? exec->device : 0;
     DeviceState* ds = device_state(t, dev);
-    std::lock_guard<std::mutex> lk(ds->mu);
+    std::lock_guard<std::recursive_mutex> lk(ds->mu);
     HIPTRY(hipSetDevice(dev));
     hipStream_t s = exec && exec->stream ? (hipStream_t)exec->stream : ds->stream;
     const bool timing = exec && (exec->flags & CTOK_F_TIMING);
@@ -2131,19 +2134,18 @@ int ctok_encode_padded(const ctok* tc, const uint8_t* utf8, const uint64_t* doc_
     const uint64_t rows = (o->flags & CTOK_P_PAIRS) ? n_docs / 2 : n_docs;
     int dev = exec ? exec->device : 0;
     DeviceState* ds = device_state(t, dev);
-    hipStream_t s;
-    {
-      std::lock_guard<std::mutex> lk(ds->mu);
-      HIPTRY(hipSetDevice(dev));
-      s = exec && exec->stream ? (hipStream_t)exec->stream : ds->stream;
-      ds->pad_in_text.ensure(B + 16);
-      ds->pad_in_off.ensure(n_docs + 1);
-      ds->pad_rowlen.ensure(rows + 1);
-      for (auto& b : ds->pad_out) b.ensure(cap ? cap : 1);
-      if (B) HIPTRY(hipMemcpyAsync(ds->pad_in_text.p, utf8, B, hipMemcpyHostToDevice, s));
-      HIPTRY(hipMemsetAsync(ds->pad_in_text.p + B, 0, 16, s));
-      HIPTRY(hipMemcpyAsync(ds->pad_in_off.p, doc_off, (n_docs + 1) * 8, hipMemcpyHostToDevice, s));
-    }
+    // held from staging to readback: another thread's call on this device cannot overwrite the
+    // staged inputs or the outputs in between (the nested device call locks again, recursively)
+    std::lock_guard<std::recursive_mutex> lk(ds->mu);
+    HIPTRY(hipSetDevice(dev));
+    hipStream_t s = exec && exec->stream ? (hipStream_t)exec->stream : ds->stream;
+    ds->pad_in_text.ensure(B + 16);
+    ds->pad_in_off.ensure(n_docs + 1);
+    ds->pad_rowlen.ensure(rows + 1);
+    for (auto& b : ds->pad_out) b.ensure(cap ? cap : 1);
+    if (B) HIPTRY(hipMemcpyAsync(ds->pad_in_text.p, utf8, B, hipMemcpyHostToDevice, s));
+    HIPTRY(hipMemsetAsync(ds->pad_in_text.p + B, 0, 16, s));
+    HIPTRY(hipMemcpyAsync(ds->pad_in_off.p, doc_off, (n_docs + 1) * 8, hipMemcpyHostToDevice, s));
     ctok_exec ex = exec ? *exec : ctok_exec{};
     ex.stream = s;
     uint64_t width = 0;
@@ -2153,7 +2155,6 @@ int ctok_encode_padded(const ctok* tc, const uint8_t* utf8, const uint64_t* doc_
                                              stats);
     *width_out = width;
     if (rc != CTOK_OK && rc != CTOK_E_CAPACITY) throw_err(rc, g_err);
-    std::lock_guard<std::mutex> lk(ds->mu);
     HIPTRY(hipMemcpyAsync(row_len, ds->pad_rowlen.p, rows * 8, hipMemcpyDeviceToHost, s));
     if (rc == CTOK_OK && rows * width) {
       const size_t nb = rows * width * 4;
@@ -2170,8 +2171,9 @@ int ctok_encode_padded(const ctok* tc, const uint8_t* utf8, const uint64_t* doc_
 // Offsets and word ids of encode_to_encoding (src/huggingface/mod.rs:395-480).  The ids and the
 // piece starts (the pre-tokenizer's words) come from the GPU encode; the walk that places each
 // word in the original text by str::find and each token inside its word is a sequential host
-// pass per document, as in the reference.  A word's ids are the ids whose token strings (one
-// char per non-dropped byte) add up to the word's non-dropped bytes.
+// pass per document, as in the reference.  A word's ids are its piece's ids on the device (k_emit
+// leaves every piece's first id for this call), not a sum of token string lengths: with the
+// rank-shift quirk (src/bpe.rs:60-69) an id's token string need not be its piece's bytes.
 int ctok_encode_offsets(const ctok* tc, const uint8_t* utf8, const uint64_t* doc_off, uint64_t n_docs,
                         uint32_t* ids, uint64_t* offsets, uint32_t* word_ids, uint64_t cap, uint64_t* tok_off,
                         const ctok_exec* exec) {
@@ -2185,7 +2187,7 @@ int ctok_encode_offsets(const ctok* tc, const uint8_t* utf8, const uint64_t* doc
     if (n_in && !utf8) throw_err(CTOK_E_ARG, "null text");
     const int dev = exec ? exec->device : 0;
     DeviceState* ds = device_state(t, dev);
-    std::lock_guard<std::mutex> lk(ds->mu);
+    std::lock_guard<std::recursive_mutex> lk(ds->mu);
     HIPTRY(hipSetDevice(dev));
     hipStream_t s = exec && exec->stream ? (hipStream_t)exec->stream : ds->stream;
     ds->pad_in_text.ensure(n_in + 16);
@@ -2196,15 +2198,21 @@ int ctok_encode_offsets(const ctok* tc, const uint8_t* utf8, const uint64_t* doc
     ds->pad_ids.ensure(ctok_ids_bound(t, n_in, n_docs));
     ds->pad_tokoff.ensure(n_docs + 1);
     const uint64_t ntok = encode_device(t, ds, ds->pad_in_text.p, ds->pad_in_off.p, n_docs, n_in, ds->pad_ids.p,
-                                        ds->pad_ids.cap, ds->pad_tokoff.p, s, false, nullptr, false);
+                                        ds->pad_ids.cap, ds->pad_tokoff.p, s, false, nullptr, false, false, true);
     const uint64_t B = ds->last_B;
     const bool norm = ds->last_norm;
-    std::vector<uint32_t> hid(ntok), pb((B + 31) / 32);
+    // each piece's first id: tile_tok[tile] (scanned) + tcnt[tile][j] (k_emit with keep_first)
+    const uint64_t n_tiles = (B + kTile - 1) / kTile;
+    std::vector<uint32_t> hid(ntok), pb((B + 31) / 32), pfirst(n_tiles * kTileSlots), tfirst(n_tiles + 1);
     std::vector<uint64_t> toff(n_docs + 1), noff;
     std::vector<uint8_t> ntext;
     HIPTRY(hipMemcpyAsync(toff.data(), ds->pad_tokoff.p, (n_docs + 1) * 8, hipMemcpyDeviceToHost, s));
     if (ntok) HIPTRY(hipMemcpyAsync(hid.data(), ds->pad_ids.p, ntok * 4, hipMemcpyDeviceToHost, s));
     if (!pb.empty()) HIPTRY(hipMemcpyAsync(pb.data(), ds->pbits.p, pb.size() * 4, hipMemcpyDeviceToHost, s));
+    if (n_tiles) {
+      HIPTRY(hipMemcpyAsync(pfirst.data(), ds->tcnt.p, pfirst.size() * 4, hipMemcpyDeviceToHost, s));
+      HIPTRY(hipMemcpyAsync(tfirst.data(), ds->tile_tok.p, tfirst.size() * 4, hipMemcpyDeviceToHost, s));
+    }
     if (norm) {
       ntext.resize(B + 1);
       noff.resize(n_docs + 1);
@@ -2227,6 +2235,8 @@ int ctok_encode_offsets(const ctok* tc, const uint8_t* utf8, const uint64_t* doc
       }
     }
     auto is_start = [&](uint64_t g) { return (pb[g >> 5] >> (g & 31)) & 1u; };
+    // first id of the piece starting at byte g, the j-th piece of its tile
+    auto first_id = [&](uint64_t g, uint32_t j) { return (uint64_t)tfirst[g / kTile] + pfirst[(g / kTile) * kTileSlots + j]; };
     // documents are independent: contiguous ranges over host threads, each with its own cache
     auto walk = [&](uint64_t d_begin, uint64_t d_end) {
     std::unordered_map<uint32_t, std::pair<uint32_t, uint32_t>> tlen;  // id -> (bytes, chars) of its token string
@@ -2242,6 +2252,8 @@ int ctok_encode_offsets(const ctok* tc, const uint8_t* utf8, const uint64_t* doc
       return tlen.emplace(id, std::make_pair(nb, nc)).first->second;
     };
     std::string word;
+    uint64_t jpos = ~0ull;  // the next piece's start and its index in its tile
+    uint32_t jcur = 0;
     for (uint64_t d = d_begin; d < d_end; d++) {
       const uint8_t* o = utf8 + doc_off[d];
       const uint64_t olen = doc_off[d + 1] - doc_off[d];
@@ -2249,9 +2261,23 @@ int ctok_encode_offsets(const ctok* tc, const uint8_t* utf8, const uint64_t* doc
       const uint8_t* nt = norm ? ntext.data() + g0 : o;
       const std::string_view orig((const char*)o, olen);
       uint64_t search = 0, k = toff[d], widx = 0;
+      // j: the piece's index within its tile (pieces start in text order; a tile's first piece is
+      // 0), carried over from the previous document's last piece
+      uint32_t j = 0;
+      if (g0 < g1) {
+        if (jpos == g0) j = jcur;
+        else
+          for (uint64_t x = (g0 / kTile) * kTile; x < g0; x++) j += is_start(x);
+      }
       for (uint64_t p = g0; p < g1;) {
         uint64_t q = p + 1;
         while (q < g1 && !is_start(q)) q++;
+        // the piece's ids: up to the next piece's first id (the next doc's first piece, or the end)
+        uint64_t nq = q;
+        while (nq < B && !is_start(nq)) nq++;
+        const uint32_t jn = nq < B && nq / kTile == p / kTile ? j + 1 : 0;
+        const uint64_t k_end = nq < B ? first_id(nq, jn) : ntok;
+        if (first_id(p, j) != k) throw_err(CTOK_E_DEVICE, "offsets: piece ids out of order");
         word.clear();
         uint64_t kept = 0;  // bytes whose char is in the vocab (the others are dropped, src/bpe.rs:94-97)
         for (uint64_t i = p; i < q; i++) {
@@ -2280,19 +2306,21 @@ int ctok_encode_offsets(const ctok* tc, const uint8_t* utf8, const uint64_t* doc
         }
         search = we;
         uint64_t at = ws;
-        for (uint64_t got = 0; got < kept; k++) {
-          if (k >= toff[d + 1]) throw_err(CTOK_E_DEVICE, "offsets: ids and words disagree");
+        (void)kept;
+        if (k_end > toff[d + 1]) throw_err(CTOK_E_DEVICE, "offsets: ids and words disagree");
+        for (; k < k_end; k++) {
           const auto L = token_len(hid[k]);
-          if (L.second == 0) throw_err(CTOK_E_UNSUPPORTED, "offsets: an id without a token string");
           const uint64_t e = std::min<uint64_t>(at + L.first, we);
           offsets[2 * k] = at;
           offsets[2 * k + 1] = e;
           word_ids[k] = (uint32_t)widx;
           at = e;
-          got += L.second;
         }
         widx++;
         p = q;
+        j = jn;
+        jpos = nq;
+        jcur = jn;
       }
       if (k != toff[d + 1]) throw_err(CTOK_E_DEVICE, "offsets: ids and words disagree");
     }

@@ -180,6 +180,8 @@ struct Work {              // device pointers, sized by the host for one call
   uint32_t n_cus;          // compute units of the device (persistent merge-pass grid)
   uint32_t nfc_watch;      // 1: the text was not NFC-checked; k_segment sets counters[12] on a
                            // code point NFC might change
+  uint32_t keep_first;     // 1: k_emit leaves every piece's first id within its tile in tcnt (not
+                           // only doc-start pieces'), for ctok_encode_offsets
   uint16_t* wpref;         // [n_tiles * 64] pieces of the tile before each 64-byte word
   uint32_t* tile_np;       // [n_tiles] pieces starting in the tile
   uint32_t* tile_tok;      // [n_tiles + 1] tokens per tile, scanned in place to the tile's first id

@@ -2112,7 +2112,7 @@ __global__ __launch_bounds__(64 * kEmitWaves) void k_emit(Work w, uint32_t* __re
             if (m + i < cj && dst + m + i < ids_cap) ids[dst + m + i] = x[i];  // the host reports CTOK_E_CAPACITY when short
         }
       }
-      if ((r & kRecDoc) && j0 + k < np) tcnt[j0 + k] = o;  // read by k_tokoff
+      if ((w.keep_first || (r & kRecDoc)) && j0 + k < np) tcnt[j0 + k] = o;  // read by k_tokoff
       o += cj;
     }
   }

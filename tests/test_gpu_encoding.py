@@ -9,7 +9,7 @@ import pytest
 
 from complexity_tokenizer import PanicException, Tokenizer
 from oracle import ref_py
-from tests import encoding_cases
+from tests import encoding_cases, toys
 
 pytestmark = pytest.mark.gpu
 
@@ -170,11 +170,15 @@ def _offset_texts():
     return out
 
 
-@pytest.mark.parametrize("variant", ["plain", "prefix_space", "nfc"])
+@pytest.mark.parametrize("variant", ["plain", "prefix_space", "nfc", "invalid_merges"])
 def test_offsets_and_word_ids(base, variant):
     """ctok_encode_offsets vs the oracle's encode_single_to_encoding: ids, per-token byte ranges
-    and word indices equal, texts whose walk panics in the reference raise PanicException."""
+    and word indices equal, texts whose walk panics in the reference raise PanicException.
+    invalid_merges: the rank-shift quirk (src/bpe.rs:60-69) makes some ids' token strings differ
+    from their word's bytes, so ids are attributed to words by the device's per-piece counts."""
     obj = json.loads(json.dumps(base))
+    if variant == "invalid_merges":
+        obj = toys.with_invalid_merges(obj, seed=2, n_bad=30)
     if variant == "prefix_space":
         obj["pre_tokenizer"]["add_prefix_space"] = True
     if variant == "nfc":
@@ -211,3 +215,30 @@ def test_offsets_lookups(base):
     p = tok.encode_pair_to_encoding("ab cd", "ef")
     q = ref.encode_to_encoding("ab cd", "ef")
     assert p.offsets == q.offsets and p.word_ids == q.word_ids
+
+
+def test_encode_padded_concurrent_threads(base):
+    """Two threads calling encode_padded on one device (ctypes releases the GIL): each call holds
+    the device's lock from staging its inputs to reading back its outputs."""
+    import threading
+    tok, _ = pair_of(encoding_cases.with_post_processor(base, "bert"))
+    a = ["hello world %d" % i for i in range(300)]
+    b = ["a much longer text number %d with more words in it" % i for i in range(500)]
+    want = {0: tok.encode_padded(a, padding="longest"), 1: tok.encode_padded(b, padding="longest")}
+    errs = []
+
+    def work(k, texts):
+        try:
+            for _ in range(20):
+                got = tok.encode_padded(texts, padding="longest")
+                for key in want[k]:
+                    assert np.array_equal(np.asarray(got[key]), np.asarray(want[k][key])), key
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+
+    th = [threading.Thread(target=work, args=(0, a)), threading.Thread(target=work, args=(1, b))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs[0]
