@@ -199,7 +199,7 @@ struct DeviceState {
   hipEvent_t ev[12] = {};
   hipEvent_t ev_sync = nullptr;   // spin-waited completion marker (no blocking-wait wakeup latency)
   hipStream_t side = nullptr;     // long-piece pass, overlapped with the short merge passes
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_cnt = nullptr;
   uint64_t* host = nullptr;       // pinned host words for small device->host readbacks
   // tables
   DevBuf<uint64_t> merge_tab, lds_image, lds16_image, merge16;
@@ -213,7 +213,7 @@ struct DeviceState {
   DevBuf<uint64_t> comp_key;
   Tables t{};
   // workspace
-  DevBuf<uint32_t> docbits, pbits, tile_np, tile_tok, tcls, list0, list1, list2, list3, tcnt, scratch, lscratch, counters, lw;
+  DevBuf<uint32_t> docbits, pbits, tile_np, tile_tok, tile_doc, tcls, list0, list1, list2, list3, tcnt, scratch, lscratch, counters, lw;
   DevBuf<uint64_t> tregion;
   DevBuf<uint16_t> wpref;
   DevBuf<uint32_t> long_cnt;
@@ -257,6 +257,7 @@ struct DeviceState {
       if (ev_sync) (void)hipEventDestroy(ev_sync);
       if (ev_fork) (void)hipEventDestroy(ev_fork);
       if (ev_join) (void)hipEventDestroy(ev_join);
+      if (ev_cnt) (void)hipEventDestroy(ev_cnt);
       if (side) (void)hipStreamDestroy(side);
       if (host) (void)hipHostFree(host);
       if (stream) (void)hipStreamDestroy(stream);
@@ -1019,6 +1020,7 @@ DeviceState* device_state(ctok* t, int device) {
   HIPTRY(hipEventCreateWithFlags(&ds->ev_sync, hipEventDisableTiming));
   HIPTRY(hipEventCreateWithFlags(&ds->ev_fork, hipEventDisableTiming));
   HIPTRY(hipEventCreateWithFlags(&ds->ev_join, hipEventDisableTiming));
+  HIPTRY(hipEventCreateWithFlags(&ds->ev_cnt, hipEventDisableTiming));
   HIPTRY(hipStreamCreateWithFlags(&ds->side, hipStreamNonBlocking));
   HIPTRY(hipHostMalloc((void**)&ds->host, 4096, hipHostMallocDefault));
   hipStream_t s = ds->stream;
@@ -1195,6 +1197,7 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   ds->wpref.ensure(nt * 64 + 8);
   ds->tile_np.ensure(nt + 8);
   ds->tile_tok.ensure(nt + 8);
+  ds->tile_doc.ensure(nt + 8);
   ds->tcls.ensure(kNumClasses * nt + 8);
   ds->list0.ensure(nt * kCap0 + 8);
   if (tb.n_at == 0) {
@@ -1216,6 +1219,7 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   w.wpref = ds->wpref.p;
   w.tile_np = ds->tile_np.p;
   w.tile_tok = ds->tile_tok.p;
+  w.tile_doc = ds->tile_doc.p;
   w.tcls = ds->tcls.p;
   w.list0 = ds->list0.p;
   w.list1 = ds->list1.p;
@@ -1252,8 +1256,12 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   }
   HIPTRY(hipEventRecord(ds->ev_fork, s));
   HIPTRY(hipStreamWaitEvent(ds->side, ds->ev_fork, 0));
-  STEP("bpe_long", launch_bpe_long(w, tb, ds->side));
-  HIPTRY(hipEventRecord(ds->ev_join, ds->side));
+  // k_segment's counters (long pieces, class 3 present) come back on the side stream while the
+  // main stream's merge passes run; the long-piece tiers are then launched with grids sized for
+  // the pieces there are, or not at all (no idle workgroups queued behind the merge passes)
+  volatile uint32_t* seg_cnt = (volatile uint32_t*)(ds->host + 64);
+  HIPTRY(hipMemcpyAsync((void*)seg_cnt, ds->counters.p, kNumCounters * 4, hipMemcpyDeviceToHost, ds->side));
+  HIPTRY(hipEventRecord(ds->ev_cnt, ds->side));
   STEP("bpe_short", launch_bpe_class(w, tb, 0, s));
   if (timing) HIPTRY(hipEventRecord(ds->ev[2], s));
   if (timing) HIPTRY(hipEventRecord(ds->ev[8], s));
@@ -1261,6 +1269,13 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   if (timing) HIPTRY(hipEventRecord(ds->ev[10], s));
   STEP("bpe_c3", launch_bpe_class(w, tb, 4, s));
   if (timing) HIPTRY(hipEventRecord(ds->ev[9], s));
+  for (;;) {
+    const hipError_t e = hipEventQuery(ds->ev_cnt);
+    if (e == hipSuccess) break;
+    if (e != hipErrorNotReady) throw_err(CTOK_E_DEVICE, std::string("hipEventQuery: ") + hipGetErrorString(e));
+  }
+  STEP("bpe_long", launch_bpe_long(w, tb, ds->side, seg_cnt[0], seg_cnt[kCtrAnyC3] != 0));
+  HIPTRY(hipEventRecord(ds->ev_join, ds->side));
   HIPTRY(hipStreamWaitEvent(s, ds->ev_join, 0));
   if (timing) HIPTRY(hipEventRecord(ds->ev[5], s));
   STEP("bpe_dropped", launch_bpe_class(w, tb, 3, s));

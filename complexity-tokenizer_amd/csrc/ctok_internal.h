@@ -38,6 +38,7 @@ __host__ __device__ constexpr int ctr_stat(int c) { return c < 3 ? 6 + 2 * c : 1
 __host__ __device__ constexpr int ctr_chunk(int c) { return c < 3 ? 13 + c : 18; }
 constexpr int kCtrAnyMid = 19;  // counters[19] != 0: some tile has a class-2 piece
 constexpr int kCtrAnyC3 = 20;   // counters[20] != 0: some tile has a class-3 piece
+constexpr int kCtrEmptyDocs = 21;  // counters[21]: empty documents (k_docstart); 0: k_emit writes tok_off
 // List entry (u32): start within the tile [0,12), piece index within the tile [12,24), length [24,31)
 // (<= kMedMax = 64), kEntDoc: the piece starts a document.
 constexpr uint32_t kEntDoc = 1u << 31;
@@ -185,6 +186,7 @@ struct Work {              // device pointers, sized by the host for one call
   uint16_t* wpref;         // [n_tiles * 64] pieces of the tile before each 64-byte word
   uint32_t* tile_np;       // [n_tiles] pieces starting in the tile
   uint32_t* tile_tok;      // [n_tiles + 1] tokens per tile, scanned in place to the tile's first id
+  uint32_t* tile_doc;      // [n_tiles + 1] documents starting in the tile, scanned to the tile's first doc
   uint32_t* tcls;          // [kNumClasses][n_tiles] entries of each class list
   uint32_t* list0;         // [n_tiles * kCap0] (also every <= 32 B piece when added tokens can match)
   uint32_t* list1;         // [n_tiles * kCap1]
@@ -292,7 +294,9 @@ hipError_t launch_segment(const Work& w, const Tables& t, hipStream_t s);
 hipError_t launch_count_pieces(const Work& w, hipStream_t s);
 // cls 0: classes 0 and 1; 2: classes 2 and 3; 3: dropped-byte pieces (mid_list)
 hipError_t launch_bpe_class(const Work& w, const Tables& t, int cls, hipStream_t s);
-hipError_t launch_bpe_long(const Work& w, const Tables& t, hipStream_t s);
+// long-piece tiers (side stream): n_long = k_segment's long-list length, any_c3 = a class-3
+// piece exists (the side instance of the 33..64 B pass); grids sized for them, nothing when empty
+hipError_t launch_bpe_long(const Work& w, const Tables& t, hipStream_t s, uint32_t n_long, bool any_c3);
 hipError_t launch_emit(const Work& w, uint32_t* ids, uint64_t ids_cap, uint64_t* tok_off, hipStream_t s);
 // exclusive scan of n u32 (n read from *n_dev when non-null, else n_max); out[n] = total
 hipError_t scan_u32(const uint32_t* in, uint32_t* out, uint64_t n_max, const uint32_t* n_dev,

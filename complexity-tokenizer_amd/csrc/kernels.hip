@@ -23,6 +23,7 @@
 // classes {White_Space, L, N, other} (derivation in DESIGN.md), bit-parallel on 64-bit masks.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <type_traits>
 
 #include "ctok_internal.h"
@@ -152,16 +153,24 @@ __device__ __forceinline__ uint32_t rank_of(const Tables& t, uint32_t a, uint32_
 // ------------------------------------------------------------------------------------------
 // doc-start bitmap
 
-__global__ void k_docstart(const uint64_t* __restrict__ off, uint32_t n_docs, uint32_t* __restrict__ bits) {
+// (empty documents set no bit and are counted into counters[kCtrEmptyDocs], one atomic per wave)
+__global__ void k_docstart(const uint64_t* __restrict__ off, uint32_t n_docs, uint32_t* __restrict__ bits,
+                           uint32_t* __restrict__ counters) {
   const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
-  if (d >= n_docs) return;
-  const uint64_t a = off[d], b = off[d + 1];
-  if (a < b) atomicOr(&bits[a >> 5], 1u << (a & 31));
+  bool empty = false;
+  if (d < n_docs) {
+    const uint64_t a = off[d], b = off[d + 1];
+    if (a < b) atomicOr(&bits[a >> 5], 1u << (a & 31));
+    empty = a == b;
+  }
+  const uint64_t m = __ballot(empty);
+  if (m && (threadIdx.x & 63) == (uint32_t)__ffsll((unsigned long long)m) - 1)
+    atomicAdd(&counters[kCtrEmptyDocs], (uint32_t)__popcll(m));
 }
 
 hipError_t launch_docstart(const Work& w, hipStream_t s) {
   HIPCHK(hipMemsetAsync(w.docbits, 0, (size_t)(w.n_words + 2) * 4, s));
-  if (w.n_docs) k_docstart<<<(w.n_docs + 255) / 256, 256, 0, s>>>(w.doc_off, w.n_docs, w.docbits);
+  if (w.n_docs) k_docstart<<<(w.n_docs + 255) / 256, 256, 0, s>>>(w.doc_off, w.n_docs, w.docbits, w.counters);
   return hipGetLastError();
 }
 
@@ -430,6 +439,8 @@ __global__ __launch_bounds__(64 * kSegWaves) void k_segment(Work w, Tables t) {
       if (gw + 1 < w.n_words) w.pbits[gw + 1] = (uint32_t)(st >> 32);
     }
   }
+  // documents starting in the tile: its words' doc-start bits within the text (summed at the end)
+  uint32_t nd = (!first && !last) ? (uint32_t)__popcll(D & valid) : 0u;
   const uint32_t c = (!first && !last) ? (uint32_t)__popcll(st) : 0u;
   const uint32_t inc = wave_incl_scan(c);
   if (!first && !last) w.wpref[(size_t)tile * 64 + lane - 1] = (uint16_t)(inc - c);
@@ -570,8 +581,11 @@ __global__ __launch_bounds__(64 * kSegWaves) void k_segment(Work w, Tables t) {
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) nd += (uint32_t)__shfl_xor((int)nd, o, 64);
   if (lane == 0) {
     w.tile_tok[tile] = hits;  // initial token count (the merge passes add theirs atomically)
+    w.tile_doc[tile] = nd;
     w.tile_np[tile] = np;
     // id regions of the register passes (ids <= bytes per piece; all four fit in kTileSlots:
     // the lists hold pieces that start in the tile and end within its 62-byte look-ahead)
@@ -2011,37 +2025,45 @@ static hipError_t launch_wave(const Work& w, const Tables& t, uint32_t grid, hip
   return hipGetLastError();
 }
 
-hipError_t launch_bpe_long(const Work& w, const Tables& t, hipStream_t s) {
+hipError_t launch_bpe_long(const Work& w, const Tables& t, hipStream_t s, uint32_t n_long, bool any_c3) {
+  auto cap = [](uint32_t want, uint32_t most) { return std::max(1u, std::min(want, most)); };
   if (t.n_at != 0 || t.dbg == 7) {
     // added tokens can match inside pieces: the linked-list kernel with the added-token split.
     // One wavefront per workgroup (32 KiB of LDS each): a long-piece workgroup fits on a CU next
     // to a merge-pass workgroup (96 KiB), so this pass overlaps them instead of taking CUs away
+    if (n_long == 0) return hipSuccess;
     const size_t lds = 4 * kLdsPos * sizeof(uint32_t);
-    k_bpe_long<false><<<512, 64, lds, s>>>(w, t);
-    k_bpe_long<true><<<128, 256, 0, s>>>(w, t);
+    k_bpe_long<false><<<cap(n_long, 512), 64, lds, s>>>(w, t);
+    k_bpe_long<true><<<cap((n_long + 3) / 4, 128), 256, 0, s>>>(w, t);
     return hipGetLastError();
   }
-  // dense wave tiers: <= 256 B (4 waves per workgroup, Bloom filter only, 43 KiB of LDS: fits
-  // next to a merge-pass workgroup), 257..2048 B and 2049..4096 B (one wave per workgroup with the
-  // whole image, 117 / 137 KiB); longer pieces: GMEM linked list.
-  // The long list holds pieces > kMedMax B and pieces whose end lies past the tile's look-ahead
-  // (>= 63 B: they can be shorter than kMedMax), so the first tier starts at 1 B.
-  HIPCHK((launch_wave<4, 0, 4, false, false>(w, t, 2 * w.n_cus, s)));
-  if (t.dbg == 8) {  // A/B: the compacting kernel for the long tiers too
-    HIPCHK((launch_wave<32, 256, 1, true, false>(w, t, w.n_cus, s)));
-    HIPCHK((launch_wave<64, 2048, 1, true, false>(w, t, w.n_cus, s)));
-  } else {
-    HIPCHK((launch_wave<16, 256, 2, true, true>(w, t, w.n_cus, s)));
-    HIPCHK((launch_wave<64, 1024, 1, true, true>(w, t, w.n_cus, s)));
+  if (n_long) {
+    // dense wave tiers: <= 256 B (4 waves per workgroup, Bloom filter only, 43 KiB of LDS: fits
+    // next to a merge-pass workgroup), 257..1024 B and 1025..4096 B (segmented, 2 / 1 waves per
+    // workgroup with the whole image); longer pieces: GMEM linked list.  Grids: at most one wave
+    // per long piece.
+    // The long list holds pieces > kMedMax B and pieces whose end lies past the tile's look-ahead
+    // (>= 63 B: they can be shorter than kMedMax), so the first tier starts at 1 B.
+    HIPCHK((launch_wave<4, 0, 4, false, false>(w, t, cap((n_long + 3) / 4, 2 * w.n_cus), s)));
+    if (t.dbg == 8) {  // A/B: the compacting kernel for the long tiers too
+      HIPCHK((launch_wave<32, 256, 1, true, false>(w, t, cap(n_long, w.n_cus), s)));
+      HIPCHK((launch_wave<64, 2048, 1, true, false>(w, t, cap(n_long, w.n_cus), s)));
+    } else {
+      HIPCHK((launch_wave<16, 256, 2, true, true>(w, t, cap((n_long + 1) / 2, w.n_cus), s)));
+      HIPCHK((launch_wave<64, 1024, 1, true, true>(w, t, cap(n_long, w.n_cus), s)));
+    }
+    k_bpe_long<true><<<cap((n_long + 3) / 4, 128), 256, 0, s>>>(w, t);
+    HIPCHK(hipGetLastError());
   }
-  k_bpe_long<true><<<128, 256, 0, s>>>(w, t);
-  HIPCHK(hipGetLastError());
-  // 33..64 B register pass, side-stream instance (see k_bpe_mid)
+  // 33..64 B register pass, side-stream instance (see k_bpe_mid): it shares class 3 with the main
+  // instance as the long tiers free CUs; with no long pieces the main instance alone runs it
+  if (!any_c3 || n_long == 0) return hipSuccess;
   return t.compact ? launch_mid<true, 3>(w, t, s) : launch_mid<false, 3>(w, t, s);
 }
 
 // ------------------------------------------------------------------------------------------
-// emission.  tile_tok is scanned to each tile's first id; then one wavefront per tile walks the
+// emission.  tile_tok is scanned to each tile's first id (tile_doc to its first document); then
+// one wavefront per tile walks the
 // tile's piece records in rounds of 256 pieces: lane l takes pieces 256 r + 4 l .. + 3 (one
 // 16-byte record load; the next round's loads are issued before this round's stores), a wave
 // scan gives each piece's first id within the tile, and the lane writes the ids itself: a
@@ -2057,12 +2079,17 @@ __device__ __forceinline__ uint32_t rec_count(const Work& w, uint32_t v) {
   return (v & kRecHit) ? 1u : (v & kRecLong) ? w.long_cnt[v & kRecLongMask] : (v & 0xFFFFu);
 }
 
-__global__ __launch_bounds__(64 * kEmitWaves) void k_emit(Work w, uint32_t* __restrict__ ids, uint64_t ids_cap) {
+__global__ __launch_bounds__(64 * kEmitWaves) void k_emit(Work w, uint32_t* __restrict__ ids, uint64_t ids_cap,
+                                                         uint64_t* __restrict__ tok_off) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t tile = uni(blockIdx.x * kEmitWaves + (threadIdx.x >> 6));
   if (tile >= w.n_tiles) return;
   const uint32_t np = uni(w.tile_np[tile]);
   const uint64_t base = uni(w.tile_tok[tile]);
+  // no empty documents: the n-th doc-start piece of the tile starts document tile_doc[tile] + n,
+  // so tok_off is written here (k_tokoff then only writes tok_off[n_docs])
+  const bool direct = uni(w.counters[kCtrEmptyDocs]) == 0;
+  uint32_t drun = uni(w.tile_doc[tile]);
   uint32_t* tcnt = w.tcnt + (size_t)tile * kTileSlots;
   const uint32_t* src0 = w.scratch + (size_t)tile * kTileSlots;
   auto load = [&](uint32_t j0) {
@@ -2083,6 +2110,15 @@ __global__ __launch_bounds__(64 * kEmitWaves) void k_emit(Work w, uint32_t* __re
     const uint32_t inc = wave_incl_scan(sum);
     uint32_t o = run + inc - sum;
     run = uni(run + (uint32_t)__shfl((int)inc, 63, 64));
+    uint32_t dord = 0;  // this lane's first doc-start piece's document (direct mode)
+    if (direct) {
+      uint32_t nd = 0;
+#pragma unroll
+      for (int k = 0; k < 4; k++) nd += (j0 + k < np && (rec[k] & kRecDoc)) ? 1u : 0u;
+      const uint32_t dinc = wave_incl_scan(nd);
+      dord = drun + dinc - nd;
+      drun = uni(drun + (uint32_t)__shfl((int)dinc, 63, 64));
+    }
     // first ids: all loads of this lane's pieces in flight together
     // (records past np are stale: c[k] == 0 keeps them from being followed)
     const uint32_t* sp[4];
@@ -2112,7 +2148,11 @@ __global__ __launch_bounds__(64 * kEmitWaves) void k_emit(Work w, uint32_t* __re
             if (m + i < cj && dst + m + i < ids_cap) ids[dst + m + i] = x[i];  // the host reports CTOK_E_CAPACITY when short
         }
       }
-      if ((w.keep_first || (r & kRecDoc)) && j0 + k < np) tcnt[j0 + k] = o;  // read by k_tokoff
+      if ((r & kRecDoc) && j0 + k < np) {
+        if (direct) tok_off[dord++] = base + o;
+        else tcnt[j0 + k] = o;  // read by k_tokoff
+      }
+      if (w.keep_first && j0 + k < np) tcnt[j0 + k] = o;  // ctok_encode_offsets
       o += cj;
     }
   }
@@ -2120,9 +2160,7 @@ __global__ __launch_bounds__(64 * kEmitWaves) void k_emit(Work w, uint32_t* __re
 
 // tok_off[d] = first id of the piece that starts at doc_off[d] (every non-empty doc starts a
 // piece; an empty doc shares the next doc's start, or the end of the text)
-__global__ void k_tokoff(Work w, uint64_t* __restrict__ tok_off) {
-  const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
-  if (d > w.n_docs) return;
+__device__ __forceinline__ void tokoff_one(const Work& w, uint64_t* __restrict__ tok_off, uint32_t d) {
   const uint64_t x = w.doc_off[d];
   uint64_t r;
   if (x >= w.n_bytes) {
@@ -2138,10 +2176,22 @@ __global__ void k_tokoff(Work w, uint64_t* __restrict__ tok_off) {
   tok_off[d] = r;
 }
 
+__global__ void k_tokoff(Work w, uint64_t* __restrict__ tok_off) {
+  if (w.counters[kCtrEmptyDocs] == 0) {  // k_emit wrote tok_off[0 .. n_docs)
+    if (blockIdx.x == 0 && threadIdx.x == 0) tok_off[w.n_docs] = w.tile_tok[w.n_tiles];
+    return;
+  }
+  for (uint32_t d = blockIdx.x * blockDim.x + threadIdx.x; d <= w.n_docs; d += gridDim.x * blockDim.x)
+    tokoff_one(w, tok_off, d);
+}
+
 hipError_t launch_emit(const Work& w, uint32_t* ids, uint64_t ids_cap, uint64_t* tok_off, hipStream_t s) {
   HIPCHK(scan_u32(w.tile_tok, w.tile_tok, (uint64_t)w.n_tiles, nullptr, w.scan_tmp, w.scan_tmp_cap, s));
-  if (w.n_tiles) k_emit<<<(w.n_tiles + kEmitWaves - 1) / kEmitWaves, 64 * kEmitWaves, 0, s>>>(w, ids, ids_cap);
-  k_tokoff<<<(w.n_docs + 1 + 255) / 256, 256, 0, s>>>(w, tok_off);
+  HIPCHK(scan_u32(w.tile_doc, w.tile_doc, (uint64_t)w.n_tiles, nullptr, w.scan_tmp, w.scan_tmp_cap, s));
+  if (w.n_tiles)
+    k_emit<<<(w.n_tiles + kEmitWaves - 1) / kEmitWaves, 64 * kEmitWaves, 0, s>>>(w, ids, ids_cap, tok_off);
+  // (grid-stride: with no empty document only tok_off[n_docs] is left to write)
+  k_tokoff<<<std::min<uint32_t>((w.n_docs + 1 + 255) / 256, 4096), 256, 0, s>>>(w, tok_off);
   return hipGetLastError();
 }
 

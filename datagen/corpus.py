@@ -352,6 +352,32 @@ def corpus_c5(n_docs: int = 1_000_000, seed: int = 5):
     return pack(docs)
 
 
+# C5-NFC: C5 with NFC-active text in a fraction of the docs (the GPU NFC path's workload, verdict
+# round 1 item 8): decomposed Latin (e + U+0301 -> U+00E9, A + U+030A + U+0301), Hangul conjoining
+# jamo (composed to syllables), Devanagari with nukta / virama and Arabic harakat (non-zero
+# combining classes, reordered by canonical order), and combining marks stacked out of order.
+_NFC_SNIPPETS = [s.encode() for s in [
+    "caf\u0065\u0301 ", "A\u030a\u0301ngstr\u00f6m ", "\u1100\u1161\u11a8\u1100\u1161 ", "\u0915\u093c\u094d\u0937 ",
+    "\u0928\u092e\u0938\u094d\u0924\u0947 ", "\u0628\u0650\u0633\u0652\u0645\u0650 ", "a\u0323\u0302b\u0302\u0323 ",
+    "o\u0308\u0304 ", "\u212b \u2126 ", "n\u0303o\u0303 ", "\u05e9\u05c1\u05b8 ", "\u0e01\u0e48\u0e32 "]]
+
+
+def corpus_c5nfc(n_docs: int = 1_000_000, seed: int = 5, frac: float = 0.03):
+    """C5's docs with one NFC-active snippet spliced (at a char boundary) into `frac` of them."""
+    text, off = corpus_c5(n_docs, seed)
+    docs = unpack(text, off)
+    rng = np.random.default_rng([seed, 0x4E4643])
+    pick = rng.choice(n_docs, size=max(1, int(n_docs * frac)), replace=False)
+    for j, d in enumerate(pick):
+        sn = _NFC_SNIPPETS[j % len(_NFC_SNIPPETS)]
+        doc = docs[d]
+        cut = int(rng.integers(0, len(doc) + 1))
+        while 0 < cut < len(doc) and (doc[cut] & 0xC0) == 0x80:
+            cut -= 1
+        docs[d] = doc[:cut] + sn + doc[cut:]
+    return pack(docs)
+
+
 # ----------------------------------------------------------------------------- helpers
 
 def pack(docs: list[bytes]):
@@ -367,4 +393,5 @@ def unpack(text: np.ndarray, off: np.ndarray) -> list[bytes]:
     return [t[o[i]:o[i + 1]] for i in range(len(o) - 1)]
 
 
-CONFIGS = {"C1": corpus_c1, "C2": corpus_c2, "C3": corpus_c3, "C4": corpus_c4, "C5": corpus_c5}
+CONFIGS = {"C1": corpus_c1, "C2": corpus_c2, "C3": corpus_c3, "C4": corpus_c4, "C5": corpus_c5,
+           "C5NFC": corpus_c5nfc}

@@ -72,6 +72,7 @@ CONFIGS = {  # name -> (tokenizer fixture, corpus fn)
     "C2": ("gpt2_50k", corpus.corpus_c2),
     "C3": ("llama3_128k", corpus.corpus_c3),
     "C5": ("multi_32k", corpus.corpus_c5),
+    "C5NFC": ("multi_32k", corpus.corpus_c5nfc),
 }
 
 

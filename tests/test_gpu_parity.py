@@ -119,6 +119,20 @@ def test_multi_sample(multi_path):
     assert_same(ids, toff, *rc.encode_packed(text, off))
 
 
+def test_multi_nfc_sample(multi_path):
+    """C5-NFC: 5% of 20k multilingual docs carry NFC-active text (decomposed Latin, conjoining
+    jamo, Devanagari / Arabic / Hebrew / Thai marks): the k_segment speculation fails and the GPU
+    NFC path (k_nfc_check -> k_norm -> the pipeline again) runs."""
+    with open(multi_path) as f:
+        obj = json.load(f)
+    tok = Tokenizer.from_file(multi_path)
+    rc = ref_c.RefC(obj)
+    text, off = corpus.corpus_c5nfc(20_000, seed=56, frac=0.05)
+    ids, toff = tok.encode_packed(text, off, timing=True)
+    assert tok.last_stats["nfc_docs"] > 0
+    assert_same(ids, toff, *rc.encode_packed(text, off))
+
+
 def test_improper_table(gpt2):
     obj, _, _ = gpt2
     sh = toys.shuffled_merges(obj, seed=3)
