@@ -1066,7 +1066,7 @@ __device__ __forceinline__ uint32_t merge_lds8(const Tables& t, const PairLds& P
 // Workgroup-shared scratch of a merge pass.
 template <uint32_t SORTCAP>
 struct PassLds {
-  uint32_t pre[65], tsum[64], tbase[64], stat[2], bcnt[4], bfill[4], chunk;
+  uint32_t pre[65], tsum[64], tbase[64], stat[2], bcnt[4], bfill[4], chunk, next;
   uint16_t perm[SORTCAP];  // the chunk's entries ordered by length bucket
 };
 
@@ -1098,7 +1098,10 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
   // through LDS): workgroups that start late, or whose CU is shared, take fewer chunks
   __syncthreads();
   for (;;) {
-    if (tid == 0) S.chunk = atomicAdd(&w.counters[ctr_chunk(LC::cls)], 1u);
+    if (tid == 0) {
+      S.chunk = atomicAdd(&w.counters[ctr_chunk(LC::cls)], 1u);
+      S.next = 0;
+    }
     __syncthreads();
     const uint32_t c0 = S.chunk * K;
     if (c0 >= w.n_tiles) break;
@@ -1143,105 +1146,126 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
       }
       __syncthreads();
     }
-    // software pipeline over a thread's pieces i, i + NT, ...: the list entry is loaded two pieces
-    // ahead and the piece's text words one piece ahead, so the merges of one piece hide the two
-    // dependent global loads of the next
     auto entry = [&](uint32_t i, uint32_t& kt) {
       const uint32_t q = sorted ? (uint32_t)S.perm[i] : i;
       kt = tile_of<K>(S.pre, q);
       return list[(size_t)(c0 + kt) * LC::cap + (q - S.pre[kt])];
     };
     auto start_of = [&](uint32_t e, uint32_t kt) { return (c0 + kt) * kTile + (e & 0xFFFu); };
-    // (64 slots: no registers to spare, no pipeline)
-    constexpr bool kPf = N <= 32;
-    constexpr int kPw = kPf ? N / 4 : 1;
-    uint32_t e0 = 0, kt0 = 0, e1 = 0, kt1 = 0;
-    uint32_t wv0[kPw];
-    if (kPf && tid < E) {
-      e0 = entry(tid, kt0);
-      load_words<kPw>(w.text, start_of(e0, kt0), w.n_bytes, wv0);
-    }
-    if (kPf && tid + NT < E) e1 = entry(tid + NT, kt1);
-    for (uint32_t i = tid; i < E; i += NT) {
-      uint32_t e, kt;
-      uint32_t wv[N / 4];
-      if constexpr (kPf) {
-        e = e0;
-        kt = kt0;
+    // one piece: list entry e of chunk tile kt, its first N bytes in wv
+    auto body = [&](uint32_t e, uint32_t kt, const uint32_t* wv) {
+        const uint32_t tile = c0 + kt;
+        const uint32_t s = tile * kTile + (e & 0xFFFu);
+        const uint32_t j = ent_j(e);
+        const uint32_t n = ent_len(e);
+        uint32_t tk[N], rk[N];
+        bool missing = false;
+        {
+#pragma unroll
+          for (int k = 0; k < N; k++) {
+            const int32_t id = s_b2id[byte_of(wv[k >> 2], k)];
+            missing |= ((uint32_t)k < n) & (id < 0);
+            tk[k] = (uint32_t)id;
+          }
+        }
+        if (missing) {  // a byte char absent from the vocab is dropped: generic path
+          w.mid_list[atomicAdd(&w.counters[4], 1u)] =
+              (uint64_t)s | ((uint64_t)j << 32) | ((uint64_t)n << 48) | ((e & kEntDoc) ? kMidDoc : 0ull);
+          return;
+        }
+        // initial pair ranks: every initial pair is a byte pair, one load each from the 256 x 256
+        // byte-pair table (L2-resident), all in flight together
+        {
+          uint32_t bytes[N];
+#pragma unroll
+          for (int k = 0; k < N; k++) bytes[k] = byte_of(wv[k >> 2], k);
+#pragma unroll
+          for (int k = 0; k < N - 1; k++) rk[k] = t.pair0[(bytes[k] << 8) | bytes[k + 1]];
+#pragma unroll
+          for (int k = 0; k < N - 1; k++) {
+            const bool live = (uint32_t)k + 1 < n;
+            if (live && rk[k] != kNoRank && value_panics(t, rk[k])) atomicOr(err, kErrPanic);
+            rk[k] = (live && !(rk[k] != kNoRank && value_panics(t, rk[k]))) ? rk[k] : kNoRank;
+          }
+        }
+        rk[N - 1] = kNoRank;
+        uint32_t m = n;
+        // tiers: N slots while the piece has more than N/2 tokens, then N/2, ... down to 8 slots
+        bool more = true;
+        if constexpr (N >= 64) more = merge_slots<64, COMPACT, HOT, L8>(t, P, tk, rk, m, 32, err);
+        if constexpr (N >= 32) {
+          if (more) more = merge_slots<32, COMPACT, HOT, L8>(t, P, tk, rk, m, 16, err);
+        }
+        if constexpr (N >= 16) {
+          if (more) more = merge_slots<16, COMPACT, HOT, L8>(t, P, tk, rk, m, 8, err);
+        }
+        // ids go to the next free slots of the tile's region for this class (dense: a wave's
+        // stores fill whole lines), the record points at them
+        uint32_t pos = 0;
+        auto out_of = [&](uint32_t mm) {
+          pos = atomicAdd(&S.tsum[kt], mm);
+          return w.scratch + (size_t)tile * kTileSlots + pos;
+        };
+        if (L8 && more) {
+          m = merge_lds8<COMPACT, HOT, NT>(t, P, tk, rk, m, s_key, s_tok, err, out_of);
+        } else {
+          if (!L8 && more) merge_slots<8, COMPACT, HOT, L8>(t, P, tk, rk, m, 0, err);
+          uint32_t* out = out_of(m);
+#pragma unroll
+          for (int k = 0; k < N; k++)
+            if ((uint32_t)k < m) out[k] = tk[k];
+        }
+        w.tcnt[(size_t)tile * kTileSlots + j] = rec_short(m, pos) | ((e & kEntDoc) ? kRecDoc : 0u);
+        st_bytes += n;
+        st_ids += m;
+    };
+    if constexpr (N > 32) {
+      // 64 slots: no registers to spare for a pipeline; a static stride over the chunk
+      for (uint32_t i = tid; i < E; i += NT) {
+        uint32_t kt;
+        const uint32_t e = entry(i, kt);
+        uint32_t wv[N / 4];
+        load_words<N / 4>(w.text, start_of(e, kt), w.n_bytes, wv);
+        body(e, kt, wv);
+      }
+    } else {
+      // Each wavefront takes blocks of 64 entries from S.next (one LDS atomic per block): a wave
+      // whose pieces merge quickly takes more blocks, so the chunk's waves finish together
+      // instead of each owning a fixed stride of the chunk (which cost 8% (<= 8 B) .. 15%
+      // (9..16 B) of the pass at the chunk barrier).  Software pipeline over a wave's blocks b0,
+      // b1, b2: the list entry is loaded two blocks ahead and the piece's text words one block
+      // ahead, so the merges of one piece hide the two dependent global loads of the next.
+      const uint32_t lane = tid & 63;
+      auto take = [&]() -> uint32_t {
+        uint32_t b = 0;
+        if (lane == 0) b = atomicAdd(&S.next, 64u);
+        return uni((uint32_t)__shfl((int)b, 0, 64));
+      };
+      constexpr int kPw = N / 4;
+      uint32_t e0 = 0, kt0 = 0, e1 = 0, kt1 = 0;
+      uint32_t wv0[kPw];
+      uint32_t b0 = take();
+      uint32_t b1 = b0 < E ? take() : E;
+      if (b0 + lane < E) {
+        e0 = entry(b0 + lane, kt0);
+        load_words<kPw>(w.text, start_of(e0, kt0), w.n_bytes, wv0);
+      }
+      if (b1 + lane < E) e1 = entry(b1 + lane, kt1);
+      while (b0 < E) {  // wave-uniform
+        const uint32_t i = b0 + lane;
+        const uint32_t b2 = b1 < E ? take() : E;
+        const uint32_t e = e0, kt = kt0;
+        uint32_t wv[N / 4];
 #pragma unroll
         for (int k = 0; k < N / 4; k++) wv[k] = wv0[k];
         e0 = e1;
         kt0 = kt1;
-        if (i + NT < E) load_words<kPw>(w.text, start_of(e0, kt0), w.n_bytes, wv0);
-        if (i + 2 * NT < E) e1 = entry(i + 2 * NT, kt1);
-      } else {
-        e = entry(i, kt);
-        load_words<N / 4>(w.text, start_of(e, kt), w.n_bytes, wv);
+        if (b1 + lane < E) load_words<kPw>(w.text, start_of(e0, kt0), w.n_bytes, wv0);
+        if (b2 + lane < E) e1 = entry(b2 + lane, kt1);
+        b0 = b1;
+        b1 = b2;
+        if (i < E) body(e, kt, wv);
       }
-      const uint32_t tile = c0 + kt;
-      const uint32_t s = tile * kTile + (e & 0xFFFu);
-      const uint32_t j = ent_j(e);
-      const uint32_t n = ent_len(e);
-      uint32_t tk[N], rk[N];
-      bool missing = false;
-      {
-#pragma unroll
-        for (int k = 0; k < N; k++) {
-          const int32_t id = s_b2id[byte_of(wv[k >> 2], k)];
-          missing |= ((uint32_t)k < n) & (id < 0);
-          tk[k] = (uint32_t)id;
-        }
-      }
-      if (missing) {  // a byte char absent from the vocab is dropped: generic path
-        w.mid_list[atomicAdd(&w.counters[4], 1u)] =
-            (uint64_t)s | ((uint64_t)j << 32) | ((uint64_t)n << 48) | ((e & kEntDoc) ? kMidDoc : 0ull);
-        continue;
-      }
-      // initial pair ranks: every initial pair is a byte pair, one load each from the 256 x 256
-      // byte-pair table (L2-resident), all in flight together
-      {
-        uint32_t bytes[N];
-#pragma unroll
-        for (int k = 0; k < N; k++) bytes[k] = byte_of(wv[k >> 2], k);
-#pragma unroll
-        for (int k = 0; k < N - 1; k++) rk[k] = t.pair0[(bytes[k] << 8) | bytes[k + 1]];
-#pragma unroll
-        for (int k = 0; k < N - 1; k++) {
-          const bool live = (uint32_t)k + 1 < n;
-          if (live && rk[k] != kNoRank && value_panics(t, rk[k])) atomicOr(err, kErrPanic);
-          rk[k] = (live && !(rk[k] != kNoRank && value_panics(t, rk[k]))) ? rk[k] : kNoRank;
-        }
-      }
-      rk[N - 1] = kNoRank;
-      uint32_t m = n;
-      // tiers: N slots while the piece has more than N/2 tokens, then N/2, ... down to 8 slots
-      bool more = true;
-      if constexpr (N >= 64) more = merge_slots<64, COMPACT, HOT, L8>(t, P, tk, rk, m, 32, err);
-      if constexpr (N >= 32) {
-        if (more) more = merge_slots<32, COMPACT, HOT, L8>(t, P, tk, rk, m, 16, err);
-      }
-      if constexpr (N >= 16) {
-        if (more) more = merge_slots<16, COMPACT, HOT, L8>(t, P, tk, rk, m, 8, err);
-      }
-      // ids go to the next free slots of the tile's region for this class (dense: a wave's
-      // stores fill whole lines), the record points at them
-      uint32_t pos = 0;
-      auto out_of = [&](uint32_t mm) {
-        pos = atomicAdd(&S.tsum[kt], mm);
-        return w.scratch + (size_t)tile * kTileSlots + pos;
-      };
-      if (L8 && more) {
-        m = merge_lds8<COMPACT, HOT, NT>(t, P, tk, rk, m, s_key, s_tok, err, out_of);
-      } else {
-        if (!L8 && more) merge_slots<8, COMPACT, HOT, L8>(t, P, tk, rk, m, 0, err);
-        uint32_t* out = out_of(m);
-#pragma unroll
-        for (int k = 0; k < N; k++)
-          if ((uint32_t)k < m) out[k] = tk[k];
-      }
-      w.tcnt[(size_t)tile * kTileSlots + j] = rec_short(m, pos) | ((e & kEntDoc) ? kRecDoc : 0u);
-      st_bytes += n;
-      st_ids += m;
     }
     tile_share_flush<K>(w, c0, S.tsum, S.tbase);
     __syncthreads();
