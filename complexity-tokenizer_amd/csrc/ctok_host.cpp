@@ -688,7 +688,8 @@ void load(ctok* t, const char* buf, size_t len) {
   size_t cap = 1024;
   // load factor <= 1/8: a lookup the Bloom filter lets through is often a pair with no merge,
   // whose linear probe runs to an empty slot (C2 k_bpe_short 0.54 -> 0.48 ms against 1/2)
-  while (cap < ranks.size() * 8 + 16) cap <<= 1;
+  const size_t f42 = getenv("CTOK_MERGE_SLACK") ? (size_t)atoi(getenv("CTOK_MERGE_SLACK")) : 8;  // A/B knob
+  while (cap < ranks.size() * f42 + 16) cap <<= 1;
   t->merge_tab.assign(cap, kEmpty);
   t->merge_mask = (uint32_t)(cap - 1);
   // inserted in rank order: the low-rank (frequent) pairs sit in their home slots, so their
@@ -771,7 +772,12 @@ void load(ctok* t, const char* buf, size_t len) {
     // merge passes.  Global table: every entry, in rank order; hot table / Bloom filter: as above.
     if (t->narrow) {
       size_t cap16 = 1024;
-      while (cap16 < ranks.size() * 8 + 16) cap16 <<= 1;
+      // load <= 1/64: a lookup that reaches this table (a hot-table miss passing the Bloom filter)
+      // stops at its first slot almost always, and a wavefront waits for its slowest lane's
+      // probe chain -- C2 k_bpe_short 0.414 ms at 1/8, 0.391 at 1/32, 0.385 at 1/128 (A/B on one
+      // box, profiles/r02/v9_ab_merge16_load.txt); 32 MB for 50k merges
+      const size_t f16 = getenv("CTOK_MERGE16_SLACK") ? (size_t)atoi(getenv("CTOK_MERGE16_SLACK")) : 64;
+      while (cap16 < ranks.size() * f16 + 16) cap16 <<= 1;
       t->merge16.assign(cap16, kEmpty);
       t->merge16_mask = (uint32_t)(cap16 - 1);
       for (const auto& rk : by_rank_key) {
@@ -908,7 +914,8 @@ void load(ctok* t, const char* buf, size_t len) {
     // slot (C2 k_segment 0.42 -> 0.32 ms against the hash-map order used before)
     std::sort(ents.begin(), ents.end(), [](const auto& x, const auto& y) { return x.second < y.second; });
     size_t pcap = 1024;
-    while (pcap < ents.size() * 8 + 16) pcap <<= 1;  // load <= 1/8: misses end early (C2 k_segment -10%)
+    const size_t fp = getenv("CTOK_PIECE_SLACK") ? (size_t)atoi(getenv("CTOK_PIECE_SLACK")) : 8;  // A/B knob
+    while (pcap < ents.size() * fp + 16) pcap <<= 1;  // load <= 1/8: misses end early (C2 k_segment -10%)
     t->piece_tab.assign((pcap + 1) * 4, 0);  // + one slot that stays empty (k_segment's no-probe lanes)
     t->piece_mask = (uint32_t)(pcap - 1);
     for (const auto& e : ents) {
