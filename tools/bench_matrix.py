@@ -160,13 +160,29 @@ def run_config(name, args, torch, dev):
     del d_text, d_off, d_ids, d_tok
     torch.cuda.empty_cache()
 
-    # e2e: host buffers through the pinned pipeline
+    # e2e: host buffers through the pinned pipeline, the C ABI with caller-owned output buffers
+    # reused across calls (ctok_encode_batch), as a C / Rust caller holds them; "e2e_numpy" is
+    # Tokenizer.encode_packed, which allocates fresh output arrays per call (their page faults,
+    # and the munmap of the previous call's arrays, are part of it)
+    import ctypes
+    from complexity_tokenizer import _native as _n
     res = {}
-    for label, devs_, chunk in (("e2e", None, 0), ("e2e_2shards", [0, 0], 0), ("e2e_chunk8", None, 8)):
+    cap_ids = n_bytes + n_docs + 16
+    o_ids = np.zeros(cap_ids, dtype=np.uint32)
+    o_off = np.zeros(n_docs + 1, dtype=np.uint64)
+    for label, devs_, chunk in (("e2e", None, 0), ("e2e_2shards", [0, 0], 0), ("e2e_chunk8", None, 8),
+                                ("e2e_numpy", None, 0)):
         tok.devices, tok.chunk_mb = devs_, chunk
 
         def estep():
-            res["r"] = tok.encode_packed(text, off)
+            if label == "e2e_numpy":
+                res["r"] = tok.encode_packed(text, off)
+                return
+            ex = tok._host_exec(False)
+            rc = _n.lib.ctok_encode_batch(tok._h, text.ctypes.data, off.ctypes.data, n_docs, o_ids.ctypes.data,
+                                          cap_ids, o_off.ctypes.data, ctypes.byref(ex), None)
+            assert rc == 0, _n.last_error()
+            res["r"] = (o_ids[: int(o_off[-1])], o_off)
 
         # (timed without per-call event timing: its synchronous event reads serialise the
         # chunk pipeline; one more call collects the H2D / D2H stats)
