@@ -1281,7 +1281,8 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
     if (e == hipSuccess) break;
     if (e != hipErrorNotReady) throw_err(CTOK_E_DEVICE, std::string("hipEventQuery: ") + hipGetErrorString(e));
   }
-  STEP("bpe_long", launch_bpe_long(w, tb, ds->side, seg_cnt[0], seg_cnt[kCtrAnyC3] != 0));
+  if (!(speculate && seg_cnt[12]))  // (a failed NFC speculation discards this pass: nothing to launch)
+    STEP("bpe_long", launch_bpe_long(w, tb, ds->side, seg_cnt[0], seg_cnt[kCtrAnyC3] != 0));
   HIPTRY(hipEventRecord(ds->ev_join, ds->side));
   HIPTRY(hipStreamWaitEvent(s, ds->ev_join, 0));
   if (timing) HIPTRY(hipEventRecord(ds->ev[5], s));

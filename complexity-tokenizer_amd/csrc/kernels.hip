@@ -87,6 +87,11 @@ __device__ T block_excl_scan(T v, T* smem /*[17]*/, T* total) {
 // wave reduces over inactive lanes and never terminates).
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// NFC speculation failed in k_segment (a code point NFC might change): the rest of this pass is
+// discarded (the host checks, normalises and runs the pipeline again), so the kernels after
+// k_segment return at once instead of merging text that will be re-encoded.
+__device__ __forceinline__ bool spec_failed(const Work& w) { return w.nfc_watch && uni(w.counters[12]) != 0; }
+
 // wave-aggregated append to an LDS counter: returns this lane's slot (lanes with take == false
 // get garbage).  One ds_add per wave instead of one per lane.
 __device__ __forceinline__ uint32_t wave_append(uint32_t* counter, bool take) {
@@ -604,6 +609,7 @@ hipError_t launch_segment(const Work& w, const Tables& t, hipStream_t s) {
 
 // pieces in the batch (statistics only): one workgroup sums tile_np into counters[5]
 __global__ __launch_bounds__(1024) void k_count_pieces(Work w) {
+  if (spec_failed(w)) return;
   __shared__ uint32_t s_red[16];
   uint32_t c = 0;
   for (uint32_t i = threadIdx.x; i < w.n_tiles; i += 1024) c += w.tile_np[i];
@@ -745,6 +751,7 @@ constexpr int kTilesGeneric = 2;  // tiles per workgroup, generic pass over list
 // MID pieces can be up to kMedMax bytes (class 3 finds them too): 64 slots, 128 threads.
 template <bool MID>
 __global__ __launch_bounds__(MID ? 128 : 256) void k_bpe_generic(Work w, Tables t) {
+  if (spec_failed(w)) return;
   constexpr uint32_t NT = MID ? 128 : 256;
   constexpr uint32_t SLOTS = MID ? kMedMax : kShortMax;
   __shared__ uint32_t s_tok[SLOTS * NT];
@@ -1296,6 +1303,7 @@ template <bool NARROW> struct ShortCfg { static constexpr uint32_t NT = NARROW ?
 
 template <bool COMPACT, bool NARROW>
 __global__ __launch_bounds__(1024) void k_bpe_short(Work w, Tables t) {
+  if (spec_failed(w)) return;
   constexpr uint32_t NT = ShortCfg<NARROW>::NT;
   extern __shared__ __attribute__((aligned(16))) uint4 s_img[];
   __shared__ int32_t s_b2id[256];
@@ -1326,6 +1334,7 @@ __global__ __launch_bounds__(1024) void k_bpe_short(Work w, Tables t) {
 // stream's passes, and a large class 3 (multilingual text) is shared by both as CUs free up.
 template <bool COMPACT, int CLS, bool NARROW>
 __global__ __launch_bounds__(512) void k_bpe_mid(Work w, Tables t) {
+  if (spec_failed(w)) return;
   extern __shared__ __attribute__((aligned(16))) uint4 s_img[];
   __shared__ int32_t s_b2id[256];
   __shared__ PassLds<kSortCap> S;
@@ -2105,6 +2114,7 @@ __device__ __forceinline__ uint32_t rec_count(const Work& w, uint32_t v) {
 
 __global__ __launch_bounds__(64 * kEmitWaves) void k_emit(Work w, uint32_t* __restrict__ ids, uint64_t ids_cap,
                                                          uint64_t* __restrict__ tok_off) {
+  if (spec_failed(w)) return;
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t tile = uni(blockIdx.x * kEmitWaves + (threadIdx.x >> 6));
   if (tile >= w.n_tiles) return;
@@ -2201,6 +2211,7 @@ __device__ __forceinline__ void tokoff_one(const Work& w, uint64_t* __restrict__
 }
 
 __global__ void k_tokoff(Work w, uint64_t* __restrict__ tok_off) {
+  if (spec_failed(w)) return;
   if (w.counters[kCtrEmptyDocs] == 0) {  // k_emit wrote tok_off[0 .. n_docs)
     if (blockIdx.x == 0 && threadIdx.x == 0) tok_off[w.n_docs] = w.tile_tok[w.n_tiles];
     return;
@@ -2425,15 +2436,10 @@ __device__ uint32_t nfc_compose(const Tables& t, uint32_t a, uint32_t b) {
   return kNone;
 }
 
-// full NFC of s[0, n) into buf (capacity 4n code points); returns the code point count
-__device__ uint32_t nfc_doc(const Tables& t, const uint8_t* s, uint32_t n, uint32_t* buf) {
-  uint32_t k = 0;
-  for (uint32_t i = 0; i < n;) {
-    uint32_t cp;
-    i += dev_decode(s, n, i, &cp);
-    k += nfc_decompose(t, cp, buf + k);
-  }
-  for (uint32_t i = 1; i < k; i++) {  // canonical ordering (stable by combining class)
+// canonical ordering (stable by combining class) then canonical composition of buf[0, k) in place
+// (UAX #15); returns the new count
+__device__ uint32_t nfc_reorder_compose(const Tables& t, uint32_t* buf, uint32_t k) {
+  for (uint32_t i = 1; i < k; i++) {
     const uint32_t c = buf[i];
     const int cc = nfc16(t, c) & 0xFF;
     if (!cc) continue;
@@ -2462,20 +2468,67 @@ __device__ uint32_t nfc_doc(const Tables& t, const uint8_t* s, uint32_t n, uint3
   return comp;
 }
 
+// NFC of s[0, n) into buf (capacity 4n code points); returns the code point count.  A code point
+// with nfc16 == 0 (ccc 0 and NFC_QC Yes) is a normalisation boundary: nothing after it combines
+// with anything before it, and it is unchanged unless a following code point combines with it.
+// So only the segments around unstable code points are normalised -- from the boundary before
+// the first (popped back from the output) to the next boundary -- and everything else is copied:
+// the decomposition / composition table searches run for a few code points of a document, not for
+// all of them.  Output in buf[0 ..) (<= 1.5 n code points), segment workspace in buf[2n ..).
+__device__ uint32_t nfc_doc(const Tables& t, const uint8_t* s, uint32_t n, uint32_t* buf) {
+  uint32_t* tmp = buf + 2 * (size_t)n;
+  uint32_t k = 0;
+  bool last_boundary = false;  // buf[k - 1] is a boundary code point copied through
+  for (uint32_t i = 0; i < n;) {
+    uint32_t cp;
+    const int len = dev_decode(s, n, i, &cp);
+    if (nfc16(t, cp) == 0) {
+      buf[k++] = cp;
+      last_boundary = true;
+      i += len;
+      continue;
+    }
+    uint32_t m = 0;
+    if (last_boundary) m = nfc_decompose(t, buf[--k], tmp);  // the segment starts at the boundary before
+    while (i < n) {
+      uint32_t c;
+      const int l = dev_decode(s, n, i, &c);
+      if (nfc16(t, c) == 0) break;  // the next boundary ends the segment
+      m += nfc_decompose(t, c, tmp + m);
+      i += l;
+    }
+    m = nfc_reorder_compose(t, tmp, m);
+    for (uint32_t j = 0; j < m; j++) buf[k++] = tmp[j];
+    last_boundary = false;
+  }
+  return k;
+}
+
 __device__ __forceinline__ uint32_t u8size(uint32_t cp) { return cp < 0x80 ? 1 : cp < 0x800 ? 2 : cp < 0x10000 ? 3 : 4; }
 
 // phase 0: new_len[d] = normalised length (flagged docs: NFC code points left in cp_scratch)
 // phase 1: write the normalised text at new_off[d] (new_len scanned into offsets)
-__global__ void k_norm(const uint8_t* __restrict__ text, const uint64_t* __restrict__ off, uint32_t n_docs,
-                       const uint32_t* __restrict__ doc_flag, int add_prefix, int nfc, Tables t,
-                       uint32_t* cp_scratch, uint32_t* ncp, uint64_t* newv, uint8_t* out, int phase) {
-  const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+// Normalisation (NFC of the flagged documents, optional prefix space), a wavefront per
+// document: phase 0 sizes each output document, phase 1 (after a scan) writes it.  An unflagged
+// document is copied by the whole wave (consecutive lanes, consecutive bytes); a flagged one is
+// decomposed / reordered / composed by lane 0 (nfc_doc), rare by construction (the host runs
+// this only when some code point NFC might change occurs).
+constexpr int kNormWaves = 4;
+
+__global__ __launch_bounds__(64 * kNormWaves) void k_norm(const uint8_t* __restrict__ text,
+                                                          const uint64_t* __restrict__ off, uint32_t n_docs,
+                                                          const uint32_t* __restrict__ doc_flag, int add_prefix,
+                                                          int nfc, Tables t, uint32_t* cp_scratch, uint32_t* ncp,
+                                                          uint64_t* newv, uint8_t* out, int phase) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t d = uni(blockIdx.x * kNormWaves + (threadIdx.x >> 6));
   if (d >= n_docs) return;
   const uint64_t a = off[d];
   const uint32_t n = (uint32_t)(off[d + 1] - a);
-  const bool flagged = nfc && doc_flag[d];
+  const bool flagged = nfc && uni(doc_flag[d]) != 0;
   uint32_t* buf = cp_scratch + 4 * a;
   if (phase == 0) {
+    if (lane != 0) return;
     uint64_t len;
     uint32_t first;
     if (flagged) {
@@ -2490,35 +2543,33 @@ __global__ void k_norm(const uint8_t* __restrict__ text, const uint64_t* __restr
     }
     if (add_prefix && len > 0 && first != ' ') len += 1;  // src/pretokenizers.rs:163-167
     newv[d] = len;
-  } else {
-    uint8_t* o = out + newv[d];
-    const uint64_t o_end = newv[d + 1];
-    uint64_t len = 0;
-    if (flagged) {
-      const uint32_t k = ncp[d];
-      for (uint32_t i = 0; i < k; i++) len += u8size(buf[i]);
-      if (add_prefix && k > 0 && buf[0] != ' ') *o++ = ' ';
-      for (uint32_t i = 0; i < k; i++) {
-        const uint32_t c = buf[i];
-        if (c < 0x80) { *o++ = (uint8_t)c; }
-        else if (c < 0x800) { *o++ = (uint8_t)(0xC0 | (c >> 6)); *o++ = (uint8_t)(0x80 | (c & 0x3F)); }
-        else if (c < 0x10000) { *o++ = (uint8_t)(0xE0 | (c >> 12)); *o++ = (uint8_t)(0x80 | ((c >> 6) & 0x3F)); *o++ = (uint8_t)(0x80 | (c & 0x3F)); }
-        else { *o++ = (uint8_t)(0xF0 | (c >> 18)); *o++ = (uint8_t)(0x80 | ((c >> 12) & 0x3F)); *o++ = (uint8_t)(0x80 | ((c >> 6) & 0x3F)); *o++ = (uint8_t)(0x80 | (c & 0x3F)); }
-      }
-    } else {
-      if (add_prefix && n > 0 && text[a] != ' ') *o++ = ' ';
-      for (uint32_t i = 0; i < n; i++) *o++ = text[a + i];
-    }
-    (void)o_end;
-    (void)len;
+    return;
   }
+  uint8_t* o = out + newv[d];
+  if (flagged) {
+    if (lane != 0) return;
+    const uint32_t k = ncp[d];
+    if (add_prefix && k > 0 && buf[0] != ' ') *o++ = ' ';
+    for (uint32_t i = 0; i < k; i++) {
+      const uint32_t c = buf[i];
+      if (c < 0x80) { *o++ = (uint8_t)c; }
+      else if (c < 0x800) { *o++ = (uint8_t)(0xC0 | (c >> 6)); *o++ = (uint8_t)(0x80 | (c & 0x3F)); }
+      else if (c < 0x10000) { *o++ = (uint8_t)(0xE0 | (c >> 12)); *o++ = (uint8_t)(0x80 | ((c >> 6) & 0x3F)); *o++ = (uint8_t)(0x80 | (c & 0x3F)); }
+      else { *o++ = (uint8_t)(0xF0 | (c >> 18)); *o++ = (uint8_t)(0x80 | ((c >> 12) & 0x3F)); *o++ = (uint8_t)(0x80 | ((c >> 6) & 0x3F)); *o++ = (uint8_t)(0x80 | (c & 0x3F)); }
+    }
+    return;
+  }
+  const uint32_t pre = (add_prefix && n > 0 && text[a] != ' ') ? 1u : 0u;
+  if (pre && lane == 0) o[0] = ' ';
+  for (uint32_t i = lane; i < n; i += 64) o[pre + i] = text[a + i];
 }
 
 hipError_t launch_norm(const uint8_t* text, const uint64_t* doc_off, uint32_t n_docs, const uint32_t* doc_flag,
                        int add_prefix, int nfc, const Tables& t, uint32_t* cp_scratch, uint32_t* ncp,
                        uint64_t* newv, uint8_t* out, int phase, hipStream_t s) {
-  if (n_docs) k_norm<<<(n_docs + 255) / 256, 256, 0, s>>>(text, doc_off, n_docs, doc_flag, add_prefix, nfc, t,
-                                                        cp_scratch, ncp, newv, out, phase);
+  if (n_docs)
+    k_norm<<<(n_docs + kNormWaves - 1) / kNormWaves, 64 * kNormWaves, 0, s>>>(text, doc_off, n_docs, doc_flag, add_prefix,
+                                                                          nfc, t, cp_scratch, ncp, newv, out, phase);
   return hipGetLastError();
 }
 
