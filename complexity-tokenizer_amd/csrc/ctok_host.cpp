@@ -477,10 +477,34 @@ void parse_post_processor(ctok* t, const ctj::Value* v) {
 }
 
 bool rust_regex_compiles(const std::string& p) {
-  for (const char* bad : {"(?=", "(?!", "(?<=", "(?<!", "(?>"})
-    if (p.find(bad) != std::string::npos) return false;
-  for (size_t i = 0; i + 1 < p.size(); i++)
-    if (p[i] == '\\' && p[i + 1] >= '1' && p[i + 1] <= '9') return false;
+  // Rust's regex crate has no look-around, atomic groups or backreferences.  Scanned token by
+  // token: an escaped character or anything inside a character class ([...], nested classes
+  // allowed) is a literal, so "[(?=]" or "\\(?=" do not count as look-ahead.
+  int cls = 0;  // character-class nesting depth
+  for (size_t i = 0; i < p.size(); i++) {
+    const char c = p[i];
+    if (c == '\\') {
+      if (i + 1 < p.size() && p[i + 1] >= '1' && p[i + 1] <= '9') return false;  // backreference
+      i++;
+      continue;
+    }
+    if (cls) {
+      if (c == '[') cls++;
+      else if (c == ']') cls--;
+      continue;
+    }
+    if (c == '[') {
+      cls = 1;
+      if (i + 1 < p.size() && p[i + 1] == '^') i++;
+      if (i + 1 < p.size() && p[i + 1] == ']') i++;  // a leading ']' is a literal
+      continue;
+    }
+    if (c == '(' && i + 2 < p.size() && p[i + 1] == '?') {
+      const char d = p[i + 2];
+      if (d == '=' || d == '!' || d == '>') return false;                                      // (?= (?! (?>
+      if (d == '<' && i + 3 < p.size() && (p[i + 3] == '=' || p[i + 3] == '!')) return false;  // (?<= (?<!
+    }
+  }
   return true;
 }
 

@@ -65,12 +65,33 @@ def deserialize_merges(items):
 
 
 def rust_regex_compiles(pattern: str) -> bool:
-    """Whether Rust `regex::Regex::new` accepts `pattern` (no look-around / backrefs / atomic)."""
-    for bad in ("(?=", "(?!", "(?<=", "(?<!", "(?>"):
-        if bad in pattern:
-            return False
-    if regex.search(r"\\[1-9]", pattern):
-        return False
+    """Whether Rust `regex::Regex::new` accepts `pattern` (no look-around / backrefs / atomic
+    groups).  Token scan: escaped characters and character-class contents are literals."""
+    p, i, cls = pattern, 0, 0
+    while i < len(p):
+        c = p[i]
+        if c == "\\":
+            if i + 1 < len(p) and p[i + 1] in "123456789":
+                return False
+            i += 2
+            continue
+        if cls:
+            cls += 1 if c == "[" else -1 if c == "]" else 0
+            i += 1
+            continue
+        if c == "[":
+            cls = 1
+            if p[i + 1:i + 2] == "^":
+                i += 1
+            if p[i + 1:i + 2] == "]":
+                i += 1
+            i += 1
+            continue
+        if c == "(" and p[i + 1:i + 2] == "?":
+            d = p[i + 2:i + 3]
+            if d in ("=", "!", ">") or (d == "<" and p[i + 3:i + 4] in ("=", "!")):
+                return False
+        i += 1
     return True
 
 

@@ -167,3 +167,26 @@ def test_shard_bounds_cover_and_balance():
              (np.array([3], np.uint32), np.array([0, 0, 1], np.uint64))]
     ids, toff = concat_results(parts)
     assert ids.tolist() == [1, 2, 3] and toff.tolist() == [0, 2, 2, 3]
+
+
+@pytest.mark.parametrize("pattern,compiles", [
+    ("\\s+(?!\\S)|\\s+", False),      # look-ahead: Rust's regex rejects it, the Split is a no-op
+    ("(?<=a)b", False), ("(?>ab)", False), ("(\\w)\\1", False),
+    ("[(?=]x", True),                 # '(?=' inside a character class is literal
+    ("\\(?=x", True),                 # escaped '(' : a literal paren, then an optional '='
+    ("[^]](?=x)", False), ("(?<name>a)b", True), ("\\s+", True),
+])
+def test_split_pattern_compilability(pattern, compiles):
+    """A Split whose pattern Rust's regex compiles would split (unsupported here: loud error); one it
+    cannot compile is skipped by the reference (src/pretokenizers.rs:298-330): the tokenizer loads.
+    The product and the oracle agree with each other on which is which."""
+    vocab = {c: i for i, c in enumerate(toys.byte_chars())}
+    split = {"type": "Split", "pattern": {"Regex": pattern}, "behavior": "Isolated"}
+    obj = toys.tok_json(vocab, [], pre_tokenizer={"type": "Sequence", "pretokenizers": [
+        split, {"type": "ByteLevel", "use_regex": False}]})
+    assert ref_py.rust_regex_compiles(pattern) == compiles
+    if compiles:
+        with pytest.raises(UnsupportedConfigError):
+            Tokenizer.from_str(json.dumps(obj))
+    else:
+        Tokenizer.from_str(json.dumps(obj))
