@@ -183,6 +183,35 @@ class Tokenizer:
         return Tokenizer(h.value)
 
     @staticmethod
+    def from_tables(vocab: dict, merges, added_tokens=(), nfc: bool = True, add_prefix_space: bool = False) -> "Tokenizer":
+        """Extension (ctok_create_from_tables): a ByteLevel BPE tokenizer from in-memory tables --
+        vocab {byte-level token string: id}, merges as (left id, right id) in rank order,
+        added_tokens as dicts with the tokenizer.json fields (id, content, special, single_word,
+        lstrip, rstrip, normalized) -- through the same loader as from_file."""
+        toks = [k.encode("utf-8") for k in vocab]
+        voff = np.zeros(len(toks) + 1, dtype=np.uint64)
+        np.cumsum([len(k) for k in toks], out=voff[1:])
+        vid = np.asarray([int(vocab[k]) for k in vocab], dtype=np.uint32)
+        ml = np.asarray([int(a) for a, _ in merges], dtype=np.uint32)
+        mr = np.asarray([int(b) for _, b in merges], dtype=np.uint32)
+        added_tokens = list(added_tokens)
+        ab = [a["content"].encode("utf-8") for a in added_tokens]
+        aoff = np.zeros(len(ab) + 1, dtype=np.uint64)
+        np.cumsum([len(x) for x in ab], out=aoff[1:])
+        aid = np.asarray([int(a["id"]) for a in added_tokens], dtype=np.uint32)
+        bits = {"special": 1, "single_word": 2, "lstrip": 4, "rstrip": 8, "normalized": 16}
+        afl = np.asarray([sum(v for k, v in bits.items() if a.get(k, False)) for a in added_tokens], dtype=np.uint8)
+        vb, abl = b"".join(toks), b"".join(ab)
+        ptr = lambda a: a.ctypes.data if len(a) else None  # noqa: E731
+        tb = _n.Tables(vb, ptr(voff), ptr(vid), len(toks), ptr(ml), ptr(mr), len(ml), abl, ptr(aoff), ptr(aid), ptr(afl),
+                       len(ab), 1 if nfc else 0, 1 if add_prefix_space else 0)
+        h = ctypes.c_void_p()
+        rc = _n.lib.ctok_create_from_tables(ctypes.byref(tb), ctypes.byref(h))
+        if rc != _n.CTOK_OK:
+            _raise(rc)
+        return Tokenizer(h.value)
+
+    @staticmethod
     def from_str(json_text: str) -> "Tokenizer":
         """HuggingFaceTokenizer::from_str (src/huggingface/mod.rs:168-173)."""
         b = json_text.encode("utf-8")

@@ -105,6 +105,14 @@ class PadOpts(ctypes.Structure):
     _fields_ = [("flags", ctypes.c_uint32), ("pad_id", ctypes.c_uint32), ("max_length", ctypes.c_uint64)]
 
 
+class Tables(ctypes.Structure):  # include/ctok.h ctok_tables
+    _fields_ = [("vocab", ctypes.c_char_p), ("vocab_off", ctypes.c_void_p), ("vocab_id", ctypes.c_void_p),
+                ("n_vocab", ctypes.c_uint64), ("merge_left", ctypes.c_void_p), ("merge_right", ctypes.c_void_p),
+                ("n_merges", ctypes.c_uint64), ("added", ctypes.c_char_p), ("added_off", ctypes.c_void_p),
+                ("added_id", ctypes.c_void_p), ("added_flags", ctypes.c_void_p), ("n_added", ctypes.c_uint64),
+                ("nfc", ctypes.c_int), ("add_prefix_space", ctypes.c_int)]
+
+
 class TrainerConfig(ctypes.Structure):  # include/ctok_trainer.h
     _fields_ = [("vocab_size", ctypes.c_uint64), ("min_frequency", ctypes.c_uint32),
                 ("min_word_length", ctypes.c_uint64), ("inl_alpha", ctypes.c_float), ("inl_beta", ctypes.c_float),
@@ -125,6 +133,7 @@ SIGS = {
     "ctok_version": (ctypes.c_char_p, []),
     "ctok_create_from_file": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(_p)]),
     "ctok_create_from_buffer": (ctypes.c_int, [ctypes.c_char_p, _sz, ctypes.POINTER(_p)]),
+    "ctok_create_from_tables": (ctypes.c_int, [ctypes.POINTER(Tables), ctypes.POINTER(_p)]),
     "ctok_destroy": (None, [_p]),
     "ctok_vocab_size": (_u64, [_p]),
     "ctok_token_to_id": (ctypes.c_int, [_p, ctypes.c_char_p, _sz, _u32p]),

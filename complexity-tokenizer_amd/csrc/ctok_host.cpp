@@ -620,6 +620,8 @@ void build_decode_table(ctok* t) {
   for (int k = 0; k < 8; k++) t->dec_bytes.push_back(0);
 }
 
+void load_root(ctok* t, const ctj::Value& root);
+
 void load(ctok* t, const char* buf, size_t len) {
   // CTOK_LOAD_TIMING=1: per-phase load times on stderr
   const bool lt = getenv("CTOK_LOAD_TIMING") != nullptr;
@@ -637,6 +639,20 @@ void load(ctok* t, const char* buf, size_t len) {
     throw_err(CTOK_E_PARSE, e.what());
   }
   lap("json");
+  load_root(t, root);
+}
+
+// The tokenizer from its parsed tokenizer.json value (from a file, a buffer, or built from tables
+// by ctok_create_from_tables).
+void load_root(ctok* t, const ctj::Value& root) {
+  const bool lt = getenv("CTOK_LOAD_TIMING") != nullptr;
+  auto lt0 = std::chrono::steady_clock::now();
+  auto lap = [&](const char* what) {
+    if (!lt) return;
+    const auto now = std::chrono::steady_clock::now();
+    fprintf(stderr, "[ctok load] %-12s %8.1f ms\n", what, std::chrono::duration<double, std::milli>(now - lt0).count());
+    lt0 = now;
+  };
   if (root.kind != ctj::Value::Object) throw_err(CTOK_E_PARSE, "invalid type: expected struct TokenizerJson");
   const ctj::Value* model = root.get("model");
   if (!model) throw_err(CTOK_E_PARSE, "missing field `model`");
@@ -1738,6 +1754,74 @@ int ctok_create_from_buffer(const char* json, size_t len, ctok** out) {
   return run([&] {
     std::unique_ptr<ctok> t(new ctok());
     load(t.get(), json, len);
+    *out = t.release();
+  });
+}
+
+int ctok_create_from_tables(const ctok_tables* tb, ctok** out) {
+  if (!tb || !out) return fail(CTOK_E_ARG, "null argument");
+  *out = nullptr;
+  return run([&] {
+    if ((tb->n_vocab && (!tb->vocab || !tb->vocab_off || !tb->vocab_id)) ||
+        (tb->n_merges && (!tb->merge_left || !tb->merge_right)) ||
+        (tb->n_added && (!tb->added || !tb->added_off || !tb->added_id || !tb->added_flags)))
+      throw_err(CTOK_E_ARG, "null table");
+    // the value tree tokenizer.json would parse to (no JSON text): model.vocab, model.merges as
+    // "a b" strings of the vocab's tokens, added_tokens, normalizer, ByteLevel pre-tokenizer/decoder
+    auto str = [](std::string v) { ctj::Value x; x.kind = ctj::Value::String; x.s = std::move(v); return x; };
+    auto num = [](uint64_t v) { ctj::Value x; x.kind = ctj::Value::Int; x.u = v; return x; };
+    auto boo = [](bool v) { ctj::Value x; x.kind = ctj::Value::Bool; x.b = v; return x; };
+    auto obj = [] { ctj::Value x; x.kind = ctj::Value::Object; return x; };
+    ctj::Value vocab = obj(), merges, added;
+    merges.kind = added.kind = ctj::Value::Array;
+    std::unordered_map<uint32_t, std::string> by_id;
+    vocab.obj.reserve(tb->n_vocab);
+    for (uint64_t i = 0; i < tb->n_vocab; i++) {
+      std::string k(tb->vocab + tb->vocab_off[i], tb->vocab_off[i + 1] - tb->vocab_off[i]);
+      by_id[tb->vocab_id[i]] = k;
+      vocab.obj.emplace_back(std::move(k), num(tb->vocab_id[i]));
+    }
+    merges.arr.reserve(tb->n_merges);
+    for (uint64_t r = 0; r < tb->n_merges; r++) {
+      auto a = by_id.find(tb->merge_left[r]), b = by_id.find(tb->merge_right[r]);
+      if (a == by_id.end() || b == by_id.end())
+        throw_err(CTOK_E_ARG, "merge " + std::to_string(r) + " names an id that is not in the vocab");
+      merges.arr.push_back(str(a->second + " " + b->second));
+    }
+    for (uint64_t i = 0; i < tb->n_added; i++) {
+      ctj::Value e = obj();
+      const uint8_t f = tb->added_flags[i];
+      e.obj.emplace_back("id", num(tb->added_id[i]));
+      e.obj.emplace_back("content", str(std::string(tb->added + tb->added_off[i], tb->added_off[i + 1] - tb->added_off[i])));
+      e.obj.emplace_back("special", boo(f & CTOK_ADDED_SPECIAL));
+      e.obj.emplace_back("single_word", boo(f & CTOK_ADDED_SINGLE_WORD));
+      e.obj.emplace_back("lstrip", boo(f & CTOK_ADDED_LSTRIP));
+      e.obj.emplace_back("rstrip", boo(f & CTOK_ADDED_RSTRIP));
+      e.obj.emplace_back("normalized", boo(f & CTOK_ADDED_NORMALIZED));
+      added.arr.push_back(std::move(e));
+    }
+    ctj::Value model = obj(), root = obj(), norm = obj(), pre = obj(), dec = obj();
+    model.obj.emplace_back("type", str("BPE"));
+    model.obj.emplace_back("vocab", std::move(vocab));
+    model.obj.emplace_back("merges", std::move(merges));
+    if (tb->nfc) {
+      norm.obj.emplace_back("type", str("NFC"));
+    } else {  // no normalisation (a null normalizer would mean NFC, src/huggingface/parsing.rs:89)
+      ctj::Value none;
+      none.kind = ctj::Value::Array;
+      norm.obj.emplace_back("type", str("Sequence"));
+      norm.obj.emplace_back("normalizers", std::move(none));
+    }
+    pre.obj.emplace_back("type", str("ByteLevel"));
+    pre.obj.emplace_back("add_prefix_space", boo(tb->add_prefix_space != 0));
+    dec.obj.emplace_back("type", str("ByteLevel"));
+    root.obj.emplace_back("model", std::move(model));
+    root.obj.emplace_back("added_tokens", std::move(added));
+    root.obj.emplace_back("normalizer", std::move(norm));
+    root.obj.emplace_back("pre_tokenizer", std::move(pre));
+    root.obj.emplace_back("decoder", std::move(dec));
+    auto t = std::make_unique<ctok>();
+    load_root(t.get(), root);
     *out = t.release();
   });
 }

@@ -45,6 +45,39 @@ const char* ctok_version(void);
 int ctok_create_from_file(const char* path, ctok** out);
 /* HuggingFaceTokenizer::from_str / from_buffer   src/huggingface/mod.rs:168-180 */
 int ctok_create_from_buffer(const char* json, size_t len, ctok** out);
+
+/* A tokenizer from in-memory tables instead of tokenizer.json text: the same
+ * loader (BpeTokenizer::new src/bpe.rs:52-79 with its rank quirks, added-token rules
+ * src/huggingface/mod.rs:247-334) on the model a ByteLevel BPE tokenizer.json describes.
+ *   vocab:  token i = vocab[vocab_off[i] .. vocab_off[i+1]) (its byte-level string), id vocab_id[i]
+ *   merges: merge r joins the tokens with ids merge_left[r], merge_right[r] (rank order; the new
+ *           token is the vocab entry of their concatenated strings, as for "a b" merge strings)
+ *   added:  content i = added[added_off[i] .. added_off[i+1]), id added_id[i], CTOK_ADDED_* flags
+ *   nfc:    1 = normalizer NFC, 0 = none; add_prefix_space: ByteLevel's flag */
+enum {
+  CTOK_ADDED_SPECIAL = 1,
+  CTOK_ADDED_SINGLE_WORD = 2,
+  CTOK_ADDED_LSTRIP = 4,
+  CTOK_ADDED_RSTRIP = 8,
+  CTOK_ADDED_NORMALIZED = 16
+};
+typedef struct ctok_tables {
+  const char* vocab;
+  const uint64_t* vocab_off;
+  const uint32_t* vocab_id;
+  uint64_t n_vocab;
+  const uint32_t* merge_left;
+  const uint32_t* merge_right;
+  uint64_t n_merges;
+  const char* added;
+  const uint64_t* added_off;
+  const uint32_t* added_id;
+  const uint8_t* added_flags;
+  uint64_t n_added;
+  int nfc;
+  int add_prefix_space;
+} ctok_tables;
+int ctok_create_from_tables(const ctok_tables* tables, ctok** out);
 void ctok_destroy(ctok* tok);
 
 /* Tokenizer.vocab_size                      src/bindings/tokenizer.rs:271-274 -> mod.rs:856-858 */

@@ -219,3 +219,15 @@ def test_nfc_speculation_redo(gpt2):
         want = rc.encode_batch(docs)
         assert got == want, "batch with tail %r differs" % tail
         assert tok.last_stats is None or tok.last_stats.get("nfc_docs", 0) == (1 if tail else 0)
+
+
+def test_from_tables_encodes_like_from_file(gpt2_path):
+    """ctok_create_from_tables on the fixture's tables (normalizer null = NFC, parsing.rs:89)."""
+    from tests.test_native_cpu import _tables_of
+    with open(gpt2_path) as f:
+        obj = json.load(f)
+    a = Tokenizer.from_file(gpt2_path)
+    b = Tokenizer.from_tables(*_tables_of(obj), nfc=True)
+    text, off = corpus.corpus_c1()
+    docs = [d.decode() for d in corpus.unpack(text, off)] + edge_cases.EDGE
+    assert a.encode_batch(docs) == b.encode_batch(docs)

@@ -190,3 +190,28 @@ def test_split_pattern_compilability(pattern, compiles):
             Tokenizer.from_str(json.dumps(obj))
     else:
         Tokenizer.from_str(json.dumps(obj))
+
+
+def _tables_of(obj):
+    vocab = obj["model"]["vocab"]
+    merges = []
+    for m in obj["model"]["merges"]:
+        a, b = m.split(" ") if isinstance(m, str) else m
+        merges.append((vocab[a], vocab[b]))
+    return vocab, merges, obj.get("added_tokens", [])
+
+
+def test_create_from_tables_matches_json(gpt2_path):
+    """ctok_create_from_tables: the same loader on tables instead of JSON text."""
+    with open(gpt2_path) as f:
+        obj = json.load(f)
+    vocab, merges, added = _tables_of(obj)
+    a = Tokenizer.from_file(gpt2_path)
+    b = Tokenizer.from_tables(vocab, merges, added, nfc=True)
+    assert a.vocab_size == b.vocab_size and a.special_tokens == b.special_tokens
+    for tok in list(vocab)[:: max(1, len(vocab) // 500)]:
+        assert a.token_to_id(tok) == b.token_to_id(tok)
+    for i in range(0, a.vocab_size, 97):
+        assert a.id_to_token(i) == b.id_to_token(i)
+    with pytest.raises(ValueError):
+        Tokenizer.from_tables(vocab, [(0, 10 ** 9)])
