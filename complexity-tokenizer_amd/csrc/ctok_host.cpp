@@ -216,7 +216,7 @@ struct DeviceState {
   DevBuf<uint32_t> docbits, pbits, tile_np, tile_tok, tile_doc, tcls, list0, list1, list2, list3, tcnt, scratch, lscratch, counters, lw;
   DevBuf<uint64_t> tregion;
   DevBuf<uint16_t> wpref;
-  DevBuf<uint32_t> long_cnt;
+  DevBuf<uint32_t> long_cnt, long_ord, long_hist;
   DevBuf<uint64_t> long_list, mid_list, scan_tmp;
   DevBuf<uint32_t> doc_flag, ncp;
   DevBuf<uint64_t> norm_off;
@@ -1258,6 +1258,8 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   ds->tregion.ensure(nt + 8);
   ds->long_list.ensure(B / kShortMax + nt + 8);
   ds->long_cnt.ensure(B / kShortMax + nt + 8);
+  ds->long_ord.ensure(B / kShortMax + nt + 8);
+  ds->long_hist.ensure(kLhWords);
   ds->mid_list.ensure(B / 2 + 8);
   ds->lw.ensure(4 * B + 64);
   ds->scan_tmp.ensure(scan_tmp_elems(std::max<uint64_t>(nt + 1, n_docs + 1)) + 64);
@@ -1273,6 +1275,8 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   w.list2 = ds->list2.p;
   w.list3 = ds->list3.p;
   w.long_cnt = ds->long_cnt.p;
+  w.long_ord = ds->long_ord.p;
+  w.long_hist = ds->long_hist.p;
   w.tcnt = ds->tcnt.p;
   w.scratch = ds->scratch.p;
   w.lscratch = ds->lscratch.p;

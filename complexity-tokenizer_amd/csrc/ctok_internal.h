@@ -39,6 +39,12 @@ __host__ __device__ constexpr int ctr_chunk(int c) { return c < 3 ? 13 + c : 18;
 constexpr int kCtrAnyMid = 19;  // counters[19] != 0: some tile has a class-2 piece
 constexpr int kCtrAnyC3 = 20;   // counters[20] != 0: some tile has a class-3 piece
 constexpr int kCtrEmptyDocs = 21;  // counters[21]: empty documents (k_docstart); 0: k_emit writes tok_off
+// Long-piece order (long_hist, u32[kLhWords], zeroed per call): pieces in descending length
+// buckets of 64 B (bucket d = 64 - (n - 1) / 64, d = 0 for n > 4096), so every wave tier's pieces
+// are a contiguous range of long_ord, longest first.
+constexpr int kLhBuckets = 65;
+constexpr int kLhHist = 0, kLhScan = 80, kLhFill = 160, kLhTake = 240, kLhWords = 320;
+__host__ __device__ inline uint32_t long_bucket(uint32_t n) { return n > 4096 ? 0u : 64u - (n - 1) / 64; }
 // List entry (u32): start within the tile [0,12), piece index within the tile [12,24), length [24,31)
 // (<= kMedMax = 64), kEntDoc: the piece starts a document.
 constexpr uint32_t kEntDoc = 1u << 31;
@@ -194,7 +200,9 @@ struct Work {              // device pointers, sized by the host for one call
   uint32_t* list3;         // [n_tiles * kCap3]
   uint32_t* tcnt;          // [n_tiles * kTileSlots] record of piece j (see kRecHit), then (k_emit) its
                            // first id within the tile
-  uint32_t* long_cnt;      // ids of long piece li
+  uint32_t* long_cnt;      // ids of long piece li (its length in bytes until a tier has run it)
+  uint32_t* long_ord;      // long-list indices in descending length buckets (k_long_order)
+  uint32_t* long_hist;     // [kLhWords] bucket counts | their exclusive scan | fill cursors | per-tier take counters
   uint32_t* scratch;       // [n_tiles * kTileSlots] ids of the register passes' pieces, per tile and class region
   uint32_t* lscratch;      // [n_bytes + 64] ids of a long / generic-pass piece starting at byte s at lscratch[s ..]
   uint2* tregion;          // [n_tiles] class region bases of the tile in scratch (region_base)

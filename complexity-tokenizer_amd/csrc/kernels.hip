@@ -1917,9 +1917,12 @@ __device__ uint32_t bpe_wave_seg(const Tables& t, const PairLds& P, const int32_
       for (int k = 0; k < K; k++) sites |= (uint64_t)(v[k] == r) << k;
     }
     const uint32_t first = sites ? a0 + (uint32_t)__builtin_ctzll(sites) : kNone;
-    const uint32_t lm = uni(wave_min_u32(first));
-    const bool chain = uni(tok[lm] == tok[nxt[lm]] ? 1u : 0u) != 0;
+    // every site holds the same pair (rank r's), so a lane tells (x, x) from its own first site
+    // (no second wave reduction on the round's critical path)
+    bool chain = false;
+    if (sites) chain = tok[first] == tok[nxt[first]];
     if (!t.proper) {
+      const uint32_t lm = uni(wave_min_u32(first));
       sites = first == lm ? 1ull << (lm - a0) : 0ull;  // the leftmost site only
     } else if (chain && sites) {
       // (x, x) runs: the 1st, 3rd, ... site of a run (d = sites before p in its run)
@@ -1941,36 +1944,72 @@ __device__ uint32_t bpe_wave_seg(const Tables& t, const PairLds& P, const int32_
       sites = keep;
     }
     const bool any = sites != 0;
-    for (uint64_t rest = sites; rest; rest &= rest - 1) sel[a0 + (uint32_t)__builtin_ctzll(rest)] = 1;
-    wave_sync_lds();
+    // A lane's sites go four at a time, the LDS reads (and in phase B the pair lookups, global
+    // loads included) of the four in flight together: no read of a phase depends on a write of
+    // the same phase (a site's right neighbour q is never a site; the left neighbour pp of a site
+    // may be a site, whose phase-A writes the barrier orders first).
+    constexpr int kB = 4;
+    auto take = [&](uint64_t& rest, uint32_t (&p)[kB]) {
+#pragma unroll
+      for (int i = 0; i < kB; i++) {
+        p[i] = rest ? a0 + (uint32_t)__builtin_ctzll(rest) : kNone;
+        rest &= rest - 1;
+      }
+    };
     // phase A: every selected site merges with its right neighbour
-    for (uint64_t rest = sites; rest; rest &= rest - 1) {
-      const uint32_t p = a0 + (uint32_t)__builtin_ctzll(rest);
-      const uint32_t q = nxt[p];
-      const uint32_t nq = nxt[q];
-      tok[p] = nid;
-      tok[q] = kDead;
-      rk[q] = kNoRank;
-      nxt[p] = (uint16_t)nq;
-      if (nq != kNoPos) prv[nq] = (uint16_t)p;
-      dirty[q / SW] = 1;
+    for (uint64_t rest = sites; rest;) {
+      uint32_t p[kB], q[kB], nq[kB];
+      take(rest, p);
+#pragma unroll
+      for (int i = 0; i < kB; i++) q[i] = p[i] != kNone ? (uint32_t)nxt[p[i]] : kNoPos;
+#pragma unroll
+      for (int i = 0; i < kB; i++) nq[i] = p[i] != kNone ? (uint32_t)nxt[q[i]] : kNoPos;
+#pragma unroll
+      for (int i = 0; i < kB; i++) {
+        if (p[i] == kNone) continue;
+        tok[p[i]] = nid;
+        tok[q[i]] = kDead;
+        rk[q[i]] = kNoRank;
+        nxt[p[i]] = (uint16_t)nq[i];
+        if (nq[i] != kNoPos) prv[nq[i]] = (uint16_t)p[i];
+        dirty[q[i] / SW] = 1;
+      }
     }
     wave_sync_lds();
-    // phase B: the new pairs' ranks (a left neighbour that is itself a site leaves the pair to
-    // that site's right-pair lookup)
-    for (uint64_t rest = sites; rest; rest &= rest - 1) {
-      const uint32_t p = a0 + (uint32_t)__builtin_ctzll(rest);
-      const uint32_t q = nxt[p];
-      rk[p] = q != kNoPos ? rank_pair<HOT>(t, P, nid, tok[q], err) : kNoRank;
-      const uint32_t pp = prv[p];
-      if (pp != kNoPos && !sel[pp]) {
-        rk[pp] = rank_pair<HOT>(t, P, tok[pp], nid, err);
-        dirty[pp / SW] = 1;
+    // phase B: the new pairs' ranks.  When the left neighbour pp is itself a site, its right-pair
+    // lookup and this site's left-pair lookup are the same pair (nid, nid) and write the same rank.
+    for (uint64_t rest = sites; rest;) {
+      uint32_t p[kB], q[kB], pp[kB], tq[kB], tp[kB];
+      take(rest, p);
+#pragma unroll
+      for (int i = 0; i < kB; i++) {
+        q[i] = p[i] != kNone ? (uint32_t)nxt[p[i]] : kNoPos;
+        pp[i] = p[i] != kNone ? (uint32_t)prv[p[i]] : kNoPos;
+      }
+#pragma unroll
+      for (int i = 0; i < kB; i++) {
+        tq[i] = q[i] != kNoPos ? (uint32_t)tok[q[i]] : 0u;
+        tp[i] = pp[i] != kNoPos ? (uint32_t)tok[pp[i]] : 0u;
+      }
+      Probe<false, HOT> R[kB], L[kB];
+#pragma unroll
+      for (int i = 0; i < kB; i++) {
+        R[i].start(t, P, nid, tq[i], q[i] != kNoPos);
+        L[i].start(t, P, tp[i], nid, pp[i] != kNoPos);
+      }
+#pragma unroll
+      for (int i = 0; i < kB; i++) {
+        if (p[i] == kNone) continue;
+        const uint32_t rr = R[i].finish(t, err), rl = L[i].finish(t, err);
+        rk[p[i]] = q[i] != kNoPos ? rr : kNoRank;
+        if (pp[i] != kNoPos) {
+          rk[pp[i]] = rl;
+          dirty[pp[i] / SW] = 1;
+        }
       }
     }
     if (any) dirty[lane] = 1;
     wave_sync_lds();
-    for (uint64_t rest = sites; rest; rest &= rest - 1) sel[a0 + (uint32_t)__builtin_ctzll(rest)] = 0;
     // (no per-round read of the panic flag: a panicking pair ranks as kNoRank, so the loop still
     // ends, and the host discards the batch -- a global load per round would double its latency)
   }
@@ -1986,35 +2025,103 @@ __device__ uint32_t bpe_wave_seg(const Tables& t, const PairLds& P, const int32_
   return c;
 }
 
-// One wavefront per piece of (LO, 64K] bytes; NW waves per workgroup, pieces dealt to waves by a
-// static stride over the long list.  LDS: the merge-table image (HOT: hot table + Bloom filter,
-// 96 KiB; else the Bloom filter, 32 KiB), loaded when the workgroup meets its first piece, and
-// one slice per wave.
-template <int K, uint32_t LO, int NW, bool HOT, bool SEG>
-__global__ __launch_bounds__(64 * NW) void k_bpe_wave(Work w, Tables t) {
-  constexpr uint32_t kSlice = SEG ? SegSlice<K>::kBytes : WaveSlice<K>::kBytes;
-  extern __shared__ __attribute__((aligned(16))) uint4 s_dyn[];
-  __shared__ int32_t s_b2id[256];
-  __shared__ uint32_t s_any;
-  constexpr uint32_t kImg = HOT ? kLdsImageBytes / 16 : kBloomWords / 4;  // uint4 units
-  const uint32_t tid = threadIdx.x, lane = tid & 63;
-  const uint32_t wid = uni(tid >> 6);
+// Long-piece order.  k_long_len: a wavefront per long piece finds its length (parked in
+// long_cnt until a tier overwrites it with the piece's id count) and counts the bucket of each
+// piece > kDenseMax B (workgroup histogram in LDS, one global add per non-empty bucket);
+// k_long_order: the buckets' exclusive scan (every workgroup computes it, workgroup 0 stores it)
+// and the scatter of those pieces' list indices, longest bucket first (LDS ranks within a
+// 256-piece step, one global reservation per bucket and step).  The segmented tiers take their
+// pieces from their own range of long_ord through a counter: the longest pieces start first and
+// a wave that finishes early takes the next one, so a tier's makespan is about its total rounds
+// over its waves (with a static stride one wave could draw several of the longest pieces).
+// Pieces <= kDenseMax B (many, short: a counter per piece would be a contended atomic each) are
+// dealt to the dense tier by a static stride over the long list.
+constexpr uint32_t kDenseMax = 256;
+
+__global__ __launch_bounds__(256) void k_long_len(Work w) {
+  __shared__ uint32_t s_hist[kLhBuckets];
+  const uint32_t lane = threadIdx.x & 63;
   const uint32_t n_long = uni(w.counters[0]);
-  if (n_long == 0) return;
-  const uint32_t n_waves = gridDim.x * NW;
-  // does any wave of this workgroup have a piece of this tier?  (the image is loaded only then)
-  if (tid == 0) s_any = 0;
+  const uint32_t n_waves = gridDim.x * 4;
+  if (threadIdx.x < (uint32_t)kLhBuckets) s_hist[threadIdx.x] = 0;
   __syncthreads();
-  for (uint32_t li = blockIdx.x * NW + wid; li < n_long; li += n_waves) {
+  for (uint32_t li = uni(blockIdx.x * 4 + (threadIdx.x >> 6)); li < n_long; li += n_waves) {
     const uint32_t s = uni((uint32_t)w.long_list[li]);
     const uint32_t n = uni(piece_end(w, s) - s);
-    if (n > LO && n <= 64u * K) {
-      if (lane == 0) s_any = 1;
-      break;
+    if (lane == 0) {
+      w.long_cnt[li] = n;
+      if (n > kDenseMax) atomicAdd(&s_hist[long_bucket(n)], 1u);
     }
   }
   __syncthreads();
-  if (s_any == 0) return;
+  if (threadIdx.x < (uint32_t)kLhBuckets && s_hist[threadIdx.x])
+    atomicAdd(&w.long_hist[kLhHist + threadIdx.x], s_hist[threadIdx.x]);
+}
+
+__global__ __launch_bounds__(256) void k_long_order(Work w) {
+  __shared__ uint32_t s_scan[kLhBuckets + 1], s_cnt[kLhBuckets], s_base[kLhBuckets];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t n_long = w.counters[0];
+  if (tid == 0) {
+    uint32_t a = 0;
+    for (int d = 0; d < kLhBuckets; d++) {
+      s_scan[d] = a;
+      a += w.long_hist[kLhHist + d];
+    }
+    s_scan[kLhBuckets] = a;
+  }
+  __syncthreads();
+  if (blockIdx.x == 0 && tid <= (uint32_t)kLhBuckets) w.long_hist[kLhScan + tid] = s_scan[tid];
+  if (s_scan[kLhBuckets] == 0) return;  // no piece > kDenseMax B
+  for (uint32_t b0 = blockIdx.x * 256; b0 < n_long; b0 += gridDim.x * 256) {
+    if (tid < (uint32_t)kLhBuckets) s_cnt[tid] = 0;
+    __syncthreads();
+    const uint32_t li = b0 + tid;
+    const uint32_t n = li < n_long ? w.long_cnt[li] : 0u;
+    const uint32_t d = long_bucket(n);
+    uint32_t r = 0;
+    if (n > kDenseMax) r = atomicAdd(&s_cnt[d], 1u);
+    __syncthreads();
+    if (tid < (uint32_t)kLhBuckets && s_cnt[tid]) s_base[tid] = atomicAdd(&w.long_hist[kLhFill + tid], s_cnt[tid]);
+    __syncthreads();
+    if (n > kDenseMax) w.long_ord[s_scan[d] + s_base[d] + r] = li;
+    __syncthreads();
+  }
+}
+
+// One wavefront per piece of (LO, 64K] bytes; NW waves per workgroup, each taking the tier's
+// pieces (a range of long_ord, longest first) from a counter.  LDS: the merge-table image (HOT:
+// hot table + Bloom filter, 96 KiB; else the Bloom filter, 32 KiB) and one slice per wave.
+template <int K, uint32_t LO, int NW, bool HOT, bool SEG>
+__global__ __launch_bounds__(64 * NW) void k_bpe_wave(Work w, Tables t) {
+  constexpr uint32_t kSlice = SEG ? SegSlice<K>::kBytes : WaveSlice<K>::kBytes;
+  constexpr uint32_t HI = 64u * K;
+  static_assert(HI <= 4096 && LO % 64 == 0 && LO < HI, "tier bounds: multiples of the 64 B buckets");
+  extern __shared__ __attribute__((aligned(16))) uint4 s_dyn[];
+  __shared__ int32_t s_b2id[256];
+  constexpr uint32_t kImg = HOT ? kLdsImageBytes / 16 : kBloomWords / 4;  // uint4 units
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  const uint32_t wid = uni(tid >> 6);
+  static_assert(SEG ? LO >= kDenseMax : HI <= kDenseMax, "ordered tiers: > kDenseMax B; dense tier: <= kDenseMax B");
+  const uint32_t n_long = uni(w.counters[0]);
+  const uint32_t lo = SEG ? uni(w.long_hist[kLhScan + kLhBuckets - HI / 64]) : 0u;
+  const uint32_t hi = SEG ? uni(w.long_hist[kLhScan + kLhBuckets - LO / 64]) : n_long;
+  // (a workgroup past the tier's piece count has nothing to take: return before the image load;
+  // the dense tier's workgroups check that they meet a piece of the tier)
+  if (lo >= hi || blockIdx.x * NW >= hi - lo) return;
+  if constexpr (!SEG) {
+    __shared__ uint32_t s_any;
+    if (tid == 0) s_any = 0;
+    __syncthreads();
+    for (uint32_t li = blockIdx.x * NW + wid; li < n_long; li += gridDim.x * NW) {
+      if (w.long_cnt[li] <= HI) {
+        if (lane == 0) s_any = 1;
+        break;
+      }
+    }
+    __syncthreads();
+    if (s_any == 0) return;
+  }
   // (HOT: hot table + the filter of the other pairs; else the filter of all pairs, stored after
   // the image)
   const uint4* img = HOT ? t.lds_image : t.lds_image + kLdsImageBytes / 16;
@@ -2025,13 +2132,24 @@ __global__ __launch_bounds__(64 * NW) void k_bpe_wave(Work w, Tables t) {
                         : PairLds{nullptr, (const lds_u32*)s_dyn};
   lds_u32* slice = (lds_u32*)((__attribute__((address_space(3))) uint8_t*)(s_dyn + kImg) + (size_t)wid * kSlice);
   uint32_t* err = &w.counters[2];
-  for (uint32_t li = uni(blockIdx.x * NW + wid); li < n_long; li += n_waves) {
+  for (uint32_t step = uni(blockIdx.x * NW + wid);; step += gridDim.x * NW) {
+    uint32_t li;
+    if constexpr (SEG) {
+      // every lane takes part (lane 0 adds 1, the others 0): no divergent branch around the
+      // atomic, whose structurised form (a divergent loop exit) once re-ran a piece forever
+      const uint32_t k = uni(atomicAdd(&w.long_hist[kLhTake + HI / 64], lane == 0 ? 1u : 0u));
+      if (k >= hi - lo) break;
+      li = uni(w.long_ord[lo + k]);
+    } else {
+      if (step >= n_long) break;
+      li = step;
+    }
+    const uint32_t n = uni(w.long_cnt[li]);
+    if (!SEG && n > HI) continue;
     const uint64_t e = w.long_list[li];
     const uint32_t s = uni((uint32_t)e);
     const uint32_t j = uni((uint32_t)(e >> 32) & 0xFFFFu);
     const uint32_t doc = (e & kLongDoc) ? kRecDoc : 0u;
-    const uint32_t n = uni(piece_end(w, s) - s);
-    if (n <= LO || n > 64u * K) continue;
     uint32_t cnt;
     if constexpr (SEG) cnt = bpe_wave_seg<K, HOT>(t, P, s_b2id, w.text + s, n, SegSlice<K>{slice}, w.lscratch + s, err);
     else cnt = bpe_wave_dense<K, HOT>(t, P, s_b2id, w.text + s, n, WaveSlice<K>{slice}, w.lscratch + s, err);
@@ -2072,18 +2190,28 @@ hipError_t launch_bpe_long(const Work& w, const Tables& t, hipStream_t s, uint32
   }
   if (n_long) {
     // dense wave tiers: <= 256 B (4 waves per workgroup, Bloom filter only, 43 KiB of LDS: fits
-    // next to a merge-pass workgroup), 257..1024 B and 1025..4096 B (segmented, 2 / 1 waves per
-    // workgroup with the whole image); longer pieces: GMEM linked list.  Grids: at most one wave
-    // per long piece.
+    // next to a merge-pass workgroup), 257..1024 B (segmented, 2 waves per workgroup with the
+    // whole image) and 1025..4096 B (segmented, 2 waves with the Bloom filter); longer pieces:
+    // GMEM linked list.  Grids: at most one wave per long piece.  k_long_len / k_long_order first
+    // (lengths, the longest-first order of the segmented tiers' pieces).
     // The long list holds pieces > kMedMax B and pieces whose end lies past the tile's look-ahead
     // (>= 63 B: they can be shorter than kMedMax), so the first tier starts at 1 B.
+    HIPCHK(hipMemsetAsync(w.long_hist, 0, kLhWords * sizeof(uint32_t), s));
+    k_long_len<<<cap((n_long + 3) / 4, 4 * w.n_cus), 256, 0, s>>>(w);
+    k_long_order<<<cap((n_long + 255) / 256, w.n_cus), 256, 0, s>>>(w);
+    HIPCHK(hipGetLastError());
     HIPCHK((launch_wave<4, 0, 4, false, false>(w, t, cap((n_long + 3) / 4, 2 * w.n_cus), s)));
-    if (t.dbg == 8) {  // A/B: the compacting kernel for the long tiers too
-      HIPCHK((launch_wave<32, 256, 1, true, false>(w, t, cap(n_long, w.n_cus), s)));
-      HIPCHK((launch_wave<64, 2048, 1, true, false>(w, t, cap(n_long, w.n_cus), s)));
+    if (t.dbg == 10) {  // A/B: 257..1024 B four waves per CU
+      HIPCHK((launch_wave<16, 256, 4, true, true>(w, t, cap((n_long + 3) / 4, w.n_cus), s)));
     } else {
       HIPCHK((launch_wave<16, 256, 2, true, true>(w, t, cap((n_long + 1) / 2, w.n_cus), s)));
+    }
+    // 1025..4096 B: two waves per CU with the Bloom filter only (32 + 2 x 53 KiB) beat one wave
+    // with the hot table (96 + 53 KiB): C3 10.3 -> 5.25 ms (profiles/r02/v14_ab_long_tiers.txt)
+    if (t.dbg == 9) {  // A/B: the hot-table variant
       HIPCHK((launch_wave<64, 1024, 1, true, true>(w, t, cap(n_long, w.n_cus), s)));
+    } else {
+      HIPCHK((launch_wave<64, 1024, 2, false, true>(w, t, cap((n_long + 1) / 2, w.n_cus), s)));
     }
     k_bpe_long<true><<<cap((n_long + 3) / 4, 128), 256, 0, s>>>(w, t);
     HIPCHK(hipGetLastError());

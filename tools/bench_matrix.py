@@ -159,6 +159,10 @@ def run_config(name, args, torch, dev):
                      "pieces": int(st["pieces"]), "long_pieces": int(st["long_pieces"])}
     del d_text, d_off, d_ids, d_tok
     torch.cuda.empty_cache()
+    if args.kernel_only:
+        log("[matrix] %s kernel %.0f MB/s (device %.3f ms, long %.3f ms), %s" % (
+            name, out["kernel"]["MBps"], out["kernel"]["ms_device"], out["kernel"]["ms_bpe_long"], out["parity"]))
+        return out
 
     # e2e: host buffers through the pinned pipeline, the C ABI with caller-owned output buffers
     # reused across calls (ctok_encode_batch), as a C / Rust caller holds them; "e2e_numpy" is
@@ -242,6 +246,7 @@ def main():
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=4.0)
     ap.add_argument("--py-docs", type=int, default=100_000)
+    ap.add_argument("--kernel-only", action="store_true", help="device-resident leg only (A/B runs)")
     args = ap.parse_args()
     os.environ.setdefault("RAYON_NUM_THREADS", str(args.threads))
     import torch
