@@ -46,6 +46,20 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
   return v;
 }
 
+// Wave minimum in uniform control flow (all 64 lanes active): DPP within each row of 16 (quad
+// swaps, half-row and row mirrors, fused into v_min), then the four row minima through
+// readlane.  About 10 instructions and no LDS round trip, against six ds_bpermute waits for the
+// shuffle form above; the long-piece rounds are latency-bound, with two reductions per round.
+__device__ __forceinline__ uint32_t wave_min_full_u32(uint32_t v) {
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0xB1, 0xF, 0xF, false));   // lane ^ 1
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x4E, 0xF, 0xF, false));   // lane ^ 2
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x141, 0xF, 0xF, false));  // row_half_mirror
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x140, 0xF, 0xF, false));  // row_mirror
+  const uint32_t a = __builtin_amdgcn_readlane(v, 0), b = __builtin_amdgcn_readlane(v, 16);
+  const uint32_t c = __builtin_amdgcn_readlane(v, 32), d = __builtin_amdgcn_readlane(v, 48);
+  return min(min(a, b), min(c, d));
+}
+
 __device__ __forceinline__ uint64_t lanemask_lt() {
   const uint32_t lane = threadIdx.x & 63;
   return lane ? (~0ull >> (64 - lane)) : 0ull;
@@ -1746,7 +1760,7 @@ __device__ uint32_t bpe_wave_dense(const Tables& t, const PairLds& P, const int3
     uint32_t lmin = kNoRank;
 #pragma unroll 8
     for (uint32_t p = lane; p < m; p += 64) lmin = min(lmin, (uint32_t)rk[p]);
-    const uint32_t r = uni(wave_min_u32(lmin));
+    const uint32_t r = uni(wave_min_full_u32(lmin));
     if (r == kNoRank) break;
     const uint32_t nid = uni(new_id_of(t, r));
     // sites: positions whose pair has rank r; lm = the leftmost
@@ -1757,7 +1771,7 @@ __device__ uint32_t bpe_wave_dense(const Tables& t, const PairLds& P, const int3
       sel[p] = site ? 1 : 0;
       lpos = min(lpos, site ? p : kNone);
     }
-    const uint32_t lm = uni(wave_min_u32(lpos));
+    const uint32_t lm = uni(wave_min_full_u32(lpos));
     const bool chain = uni(tok[lm] == tok[lm + 1] ? 1u : 0u) != 0;
     wave_sync_lds();
     if (!t.proper) {
@@ -1814,15 +1828,16 @@ __device__ uint32_t bpe_wave_dense(const Tables& t, const PairLds& P, const int3
 }
 
 // Long pieces (hundreds to thousands of tokens): positions stay put and are linked into a list
-// (nxt / prv, u16); lane l owns the contiguous segment [l*S, (l+1)*S) and keeps the minimum pair
-// rank of its segment in a register.  A round costs a 64-lane minimum, then only the lanes
-// that hold a site (or whose segment changed) walk their S positions -- instead of every round
-// sweeping and compacting the whole piece.
+// (nxt / prv, u16); lane l owns the contiguous segment [l*S, (l+1)*S), in four groups of S/4
+// positions whose ranks it keeps in registers with each group's minimum.  A round costs a
+// 64-lane minimum, then only the lanes that hold a site look at the group(s) holding it, and
+// only groups whose ranks changed are reloaded -- instead of every round sweeping and compacting
+// the whole piece.
 template <int K>
 struct SegSlice {  // per-wave LDS slice for up to 64K positions
   static constexpr uint32_t C = 64 * K;
-  static constexpr uint32_t kBytes = 13 * C + 64;
-  lds_u32* base;  // tok[C] | rk[C] | nxt[C] u16 | prv[C] u16 | sel[C] u8 | dirty[64] u8
+  static constexpr uint32_t kBytes = 13 * C + 256;
+  lds_u32* base;  // tok[C] | rk[C] | nxt[C] u16 | prv[C] u16 | sel[C] u8 | dirty[256] u8 (per group)
   __device__ __forceinline__ lds_u32* tok() const { return base; }
   __device__ __forceinline__ lds_u32* rk() const { return base + C; }
   __device__ __forceinline__ __attribute__((address_space(3))) uint16_t* nxt() const {
@@ -1840,7 +1855,8 @@ constexpr uint32_t kNoPos = 0xFFFFu;
 template <int K, bool HOT>
 __device__ uint32_t bpe_wave_seg(const Tables& t, const PairLds& P, const int32_t* s_b2id, const uint8_t* bytes,
                                  uint32_t n, const SegSlice<K>& S, uint32_t* out, uint32_t* err) {
-  static_assert(K % 4 == 0 && K <= 64, "segment width: a multiple of 4, at most 64");
+  static_assert(K % 16 == 0 && K <= 64, "segment width: a multiple of 16, at most 64");
+  constexpr uint32_t R = K / 4;  // registers per group
   const uint32_t lane = threadIdx.x & 63;
   lds_u32* tok = S.tok();
   lds_u32* rk = S.rk();
@@ -1863,11 +1879,16 @@ __device__ uint32_t bpe_wave_seg(const Tables& t, const PairLds& P, const int32_
   }
   wave_sync_lds();
   if (m == 0) return 0;
-  // lane l owns positions [l*SW, l*SW + SW): SW is a multiple of 4, so a segment's ranks are
-  // read with SW/4 independent 16-byte LDS loads into v[] (one LDS latency per scan instead of
-  // one per position); positions >= m hold kNoRank
-  const uint32_t SW = (((m + 63) / 64) + 3) & ~3u;  // <= K
+  // lane l owns positions [l*SW, l*SW + SW) in four groups of G = SW/4 positions: SW is a
+  // multiple of 16, so a group's ranks are read with G/4 independent 16-byte LDS loads into
+  // v[g*R ..] (one LDS latency per group instead of one per position); positions >= m hold
+  // kNoRank.  Group of position p (its dirty flag): p / G, by a multiply-high (p < 2^16).
+  const uint32_t SW = min((uint32_t)K, (((m + 63) / 64) + 15) & ~15u);
+  const uint32_t G = SW >> 2;
+  const uint32_t gmag = (uint32_t)(((1ull << 32) + G - 1) / G);
+  auto unit = [&](uint32_t p) { return __umulhi(p, gmag); };
   const uint32_t a0 = lane * SW;
+  auto pos = [&](uint32_t b) { return a0 + (b / R) * G + (b % R); };  // site bit -> position
   for (uint32_t k = 0; k < SW; k++) {
     const uint32_t p = a0 + k;
     uint32_t r = kNoRank;
@@ -1885,45 +1906,55 @@ __device__ uint32_t bpe_wave_seg(const Tables& t, const PairLds& P, const int32_
     }
   }
   wave_sync_lds();
-  for (uint32_t k = 0; k < SW; k++) sel[a0 + k] = 0;
-  dirty[lane] = 1;  // first round: every lane loads its segment
+  lds_u32* dirty32 = (lds_u32*)dirty;
+  dirty32[lane] = 0x01010101u;  // first round: every lane loads its groups
   uint32_t v[K];
-  uint32_t smin = kNoRank;
+  uint32_t gm[4] = {kNoRank, kNoRank, kNoRank, kNoRank};
   wave_sync_lds();
   for (;;) {
-    if (dirty[lane]) {  // (re)load this segment's ranks and their minimum
-      const uint4* src = (const uint4*)(rk + a0);
-      smin = kNoRank;
+    const uint32_t dw = dirty32[lane];
+    if (dw) {  // (re)load the changed groups' ranks and their minima
 #pragma unroll
-      for (int q = 0; q < K / 4; q++) {
-        const uint4 x = (uint32_t)(4 * q) < SW ? src[q] : make_uint4(kNoRank, kNoRank, kNoRank, kNoRank);
-        v[4 * q] = x.x;
-        v[4 * q + 1] = x.y;
-        v[4 * q + 2] = x.z;
-        v[4 * q + 3] = x.w;
+      for (int g = 0; g < 4; g++) {
+        if (dw & (0xFFu << (8 * g))) {
+          const uint4* src = (const uint4*)(rk + a0 + g * G);
+          uint32_t mn = kNoRank;
+#pragma unroll
+          for (int q = 0; q < (int)R / 4; q++) {
+            const uint4 x = (uint32_t)(4 * q) < G ? src[q] : make_uint4(kNoRank, kNoRank, kNoRank, kNoRank);
+            v[g * R + 4 * q] = x.x;
+            v[g * R + 4 * q + 1] = x.y;
+            v[g * R + 4 * q + 2] = x.z;
+            v[g * R + 4 * q + 3] = x.w;
+            mn = min(min(mn, min(x.x, x.y)), min(x.z, x.w));
+          }
+          gm[g] = mn;
+        }
       }
-#pragma unroll
-      for (int k = 0; k < K; k++) smin = min(smin, v[k]);
-      dirty[lane] = 0;
+      dirty32[lane] = 0;
     }
-    const uint32_t r = uni(wave_min_u32(smin));
+    const uint32_t smin = min(min(gm[0], gm[1]), min(gm[2], gm[3]));
+    const uint32_t r = uni(wave_min_full_u32(smin));
     if (r == kNoRank) break;
     const uint32_t nid = uni(new_id_of(t, r));
-    // this segment's sites as a bit mask (bit k: position a0 + k); the leftmost site decides
-    // the mode
+    // this segment's sites as a bit mask (bit g*R + k: position a0 + g*G + k), from the groups
+    // whose minimum is r; the leftmost site decides the mode
     uint64_t sites = 0;
-    if (smin == r) {
 #pragma unroll
-      for (int k = 0; k < K; k++) sites |= (uint64_t)(v[k] == r) << k;
+    for (int g = 0; g < 4; g++) {
+      if (gm[g] == r) {
+#pragma unroll
+        for (int k = 0; k < (int)R; k++) sites |= (uint64_t)(v[g * R + k] == r) << (g * R + k);
+      }
     }
-    const uint32_t first = sites ? a0 + (uint32_t)__builtin_ctzll(sites) : kNone;
+    const uint32_t first = sites ? pos((uint32_t)__builtin_ctzll(sites)) : kNone;
     // every site holds the same pair (rank r's), so a lane tells (x, x) from its own first site
     // (no second wave reduction on the round's critical path)
     bool chain = false;
     if (sites) chain = tok[first] == tok[nxt[first]];
     if (!t.proper) {
-      const uint32_t lm = uni(wave_min_u32(first));
-      sites = first == lm ? 1ull << (lm - a0) : 0ull;  // the leftmost site only
+      const uint32_t lm = uni(wave_min_full_u32(first));
+      sites = first == lm ? (sites & (~sites + 1)) : 0ull;  // the leftmost site only
     } else if (chain && sites) {
       // (x, x) runs: the 1st, 3rd, ... site of a run (d = sites before p in its run)
       uint64_t keep = 0, rest = sites;
@@ -1931,7 +1962,7 @@ __device__ uint32_t bpe_wave_seg(const Tables& t, const PairLds& P, const int32_
       while (rest) {
         const uint32_t k = (uint32_t)__builtin_ctzll(rest);
         rest &= rest - 1;
-        const uint32_t p = a0 + k;
+        const uint32_t p = pos(k);
         if (last != kNone && prv[p] == last) {
           d++;
         } else {  // run start, or a run entering from the previous segment: walk back
@@ -1943,7 +1974,6 @@ __device__ uint32_t bpe_wave_seg(const Tables& t, const PairLds& P, const int32_
       }
       sites = keep;
     }
-    const bool any = sites != 0;
     // A lane's sites go four at a time, the LDS reads (and in phase B the pair lookups, global
     // loads included) of the four in flight together: no read of a phase depends on a write of
     // the same phase (a site's right neighbour q is never a site; the left neighbour pp of a site
@@ -1952,7 +1982,7 @@ __device__ uint32_t bpe_wave_seg(const Tables& t, const PairLds& P, const int32_
     auto take = [&](uint64_t& rest, uint32_t (&p)[kB]) {
 #pragma unroll
       for (int i = 0; i < kB; i++) {
-        p[i] = rest ? a0 + (uint32_t)__builtin_ctzll(rest) : kNone;
+        p[i] = rest ? pos((uint32_t)__builtin_ctzll(rest)) : kNone;
         rest &= rest - 1;
       }
     };
@@ -1972,7 +2002,7 @@ __device__ uint32_t bpe_wave_seg(const Tables& t, const PairLds& P, const int32_
         rk[q[i]] = kNoRank;
         nxt[p[i]] = (uint16_t)nq[i];
         if (nq[i] != kNoPos) prv[nq[i]] = (uint16_t)p[i];
-        dirty[q[i] / SW] = 1;
+        dirty[unit(q[i])] = 1;
       }
     }
     wave_sync_lds();
@@ -2002,13 +2032,13 @@ __device__ uint32_t bpe_wave_seg(const Tables& t, const PairLds& P, const int32_
         if (p[i] == kNone) continue;
         const uint32_t rr = R[i].finish(t, err), rl = L[i].finish(t, err);
         rk[p[i]] = q[i] != kNoPos ? rr : kNoRank;
+        dirty[unit(p[i])] = 1;
         if (pp[i] != kNoPos) {
           rk[pp[i]] = rl;
-          dirty[pp[i] / SW] = 1;
+          dirty[unit(pp[i])] = 1;
         }
       }
     }
-    if (any) dirty[lane] = 1;
     wave_sync_lds();
     // (no per-round read of the panic flag: a panicking pair ranks as kNoRank, so the loop still
     // ends, and the host discards the batch -- a global load per round would double its latency)
