@@ -60,6 +60,16 @@ __device__ __forceinline__ uint32_t wave_min_full_u32(uint32_t v) {
   return min(min(a, b), min(c, d));
 }
 
+// Wave sum in uniform control flow, the same DPP row reduction as wave_min_full_u32.
+__device__ __forceinline__ uint32_t wave_sum_full_u32(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0xB1, 0xF, 0xF, false);   // lane ^ 1
+  v += (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x4E, 0xF, 0xF, false);   // lane ^ 2
+  v += (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
+  v += (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x140, 0xF, 0xF, false);  // row_mirror
+  return __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16) + __builtin_amdgcn_readlane(v, 32) +
+         __builtin_amdgcn_readlane(v, 48);
+}
+
 __device__ __forceinline__ uint64_t lanemask_lt() {
   const uint32_t lane = threadIdx.x & 63;
   return lane ? (~0ull >> (64 - lane)) : 0ull;
@@ -75,6 +85,22 @@ __device__ __forceinline__ T wave_incl_scan(T v) {
   }
   return v;
 }
+
+// u32 inclusive wave scan in uniform control flow (all 64 lanes active): DPP row shifts within
+// each row of 16, then row broadcasts 15 / 31 -- six fused v_add, against six ds_bpermute round
+// trips for the shuffle form (k_segment's and k_emit's per-round scans are on their critical
+// paths).  Preferred over the template for u32 arguments.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);  // row_shr:2
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31
+  return v;
+}
+
+__device__ __forceinline__ uint32_t lane63(uint32_t v) { return __builtin_amdgcn_readlane(v, 63); }
 
 // block-wide exclusive scan; nthreads = blockDim.x (multiple of 64, <= 1024)
 template <typename T>
@@ -463,7 +489,7 @@ __global__ __launch_bounds__(64 * kSegWaves) void k_segment(Work w, Tables t) {
   const uint32_t c = (!first && !last) ? (uint32_t)__popcll(st) : 0u;
   const uint32_t inc = wave_incl_scan(c);
   if (!first && !last) w.wpref[(size_t)tile * 64 + lane - 1] = (uint16_t)(inc - c);
-  const uint32_t np = uni((uint32_t)__shfl((int)inc, 63, 64));
+  const uint32_t np = lane63(inc);
   // where the tile's last piece ends (look-ahead lane): 0xFFFF = unknown (longer than the
   // look-ahead can tell: a long piece)
   const uint32_t tile_end =
@@ -591,17 +617,11 @@ __global__ __launch_bounds__(64 * kSegWaves) void k_segment(Work w, Tables t) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    hits += (uint32_t)__shfl_xor((int)hits, o, 64);
-    by0 += (uint32_t)__shfl_xor((int)by0, o, 64);
-    by1 += (uint32_t)__shfl_xor((int)by1, o, 64);
-    by2 += (uint32_t)__shfl_xor((int)by2, o, 64);
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) nd += (uint32_t)__shfl_xor((int)nd, o, 64);
+  hits = wave_sum_full_u32(hits);
+  by0 = wave_sum_full_u32(by0);
+  by1 = wave_sum_full_u32(by1);
+  by2 = wave_sum_full_u32(by2);
+  nd = wave_sum_full_u32(nd);
   if (lane == 0) {
     w.tile_tok[tile] = hits;  // initial token count (the merge passes add theirs atomically)
     w.tile_doc[tile] = nd;
@@ -2301,7 +2321,7 @@ __global__ __launch_bounds__(64 * kEmitWaves) void k_emit(Work w, uint32_t* __re
     }
     const uint32_t inc = wave_incl_scan(sum);
     uint32_t o = run + inc - sum;
-    run = uni(run + (uint32_t)__shfl((int)inc, 63, 64));
+    run = uni(run + lane63(inc));
     uint32_t dord = 0;  // this lane's first doc-start piece's document (direct mode)
     if (direct) {
       uint32_t nd = 0;
@@ -2309,7 +2329,7 @@ __global__ __launch_bounds__(64 * kEmitWaves) void k_emit(Work w, uint32_t* __re
       for (int k = 0; k < 4; k++) nd += (j0 + k < np && (rec[k] & kRecDoc)) ? 1u : 0u;
       const uint32_t dinc = wave_incl_scan(nd);
       dord = drun + dinc - nd;
-      drun = uni(drun + (uint32_t)__shfl((int)dinc, 63, 64));
+      drun = uni(drun + lane63(dinc));
     }
     // first ids: all loads of this lane's pieces in flight together
     // (records past np are stale: c[k] == 0 keeps them from being followed)
