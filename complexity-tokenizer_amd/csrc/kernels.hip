@@ -142,7 +142,7 @@ __device__ __forceinline__ uint32_t wave_append(uint32_t* counter, bool take) {
     const uint32_t lane = threadIdx.x & 63;
     uint32_t b = 0;
     if (lane == leader) b = atomicAdd(counter, (uint32_t)__popcll(m));
-    base = (uint32_t)__shfl((int)b, (int)leader, 64);
+    base = __builtin_amdgcn_readlane(b, leader);
   }
   return base + (uint32_t)__popcll(m & lanemask_lt());
 }
@@ -247,15 +247,20 @@ __device__ __forceinline__ int seg_cls_wide(const uint8_t* text, uint32_t B, uin
   return cls_of(c, t) | (nfc16(t, c) != 0 ? 4 : 0);
 }
 
+// Neighbour lanes' words (k_segment: lane l needs lanes l - 1 and l + 1), by DPP wave shifts
+// (wave_shr:1 / wave_shl:1, GFX9) instead of ds_bpermute: lane 0 (shr) and lane 63 (shl) keep
+// their own value, as __shfl_up / __shfl_down leave it.  Uniform control flow only.
+__device__ __forceinline__ uint32_t dpp_prev(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x138, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint32_t dpp_next(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x130, 0xF, 0xF, false);
+}
 __device__ __forceinline__ uint64_t shfl_up64(uint64_t v) {
-  const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)v, 1, 64);
-  const uint32_t hi = (uint32_t)__shfl_up((int)(uint32_t)(v >> 32), 1, 64);
-  return (uint64_t)lo | ((uint64_t)hi << 32);
+  return (uint64_t)dpp_prev((uint32_t)v) | ((uint64_t)dpp_prev((uint32_t)(v >> 32)) << 32);
 }
 __device__ __forceinline__ uint64_t shfl_down64(uint64_t v) {
-  const uint32_t lo = (uint32_t)__shfl_down((int)(uint32_t)v, 1, 64);
-  const uint32_t hi = (uint32_t)__shfl_down((int)(uint32_t)(v >> 32), 1, 64);
-  return (uint64_t)lo | ((uint64_t)hi << 32);
+  return (uint64_t)dpp_next((uint32_t)v) | ((uint64_t)dpp_next((uint32_t)(v >> 32)) << 32);
 }
 
 // Bytes s .. s + 4*NW - 1 of the text as NW little-endian words, read with NW + 1 aligned dword
@@ -606,7 +611,7 @@ __global__ __launch_bounds__(64 * kSegWaves) void k_segment(Work w, Tables t) {
         const uint32_t leader = __ffsll((unsigned long long)lm) - 1;
         uint32_t b = 0;
         if (lane == leader) b = atomicAdd(&w.counters[0], (uint32_t)__popcll(lm));
-        b = (uint32_t)__shfl((int)b, (int)leader, 64);
+        b = __builtin_amdgcn_readlane(b, leader);
         if (cls[u] == 3)
           w.long_list[b + __popcll(lm & lanemask_lt())] =
               (uint64_t)(t0 + sl[u]) | ((uint64_t)j << 32) | (doc[u] ? kLongDoc : 0ull);
