@@ -739,16 +739,27 @@ __device__ __forceinline__ uint32_t bpe_short(const Tables& t, const uint8_t* by
 
 // s_tsum[l] starts at tile t0 + l's region base for class cls (tregion, cls >= 0) or at 0: the
 // merge passes allocate their ids from it (and add the difference to tile_tok at the flush).
+// (K <= 256 tiles: the first K/64 waves scan 64 counts each, then add the earlier waves' totals;
+// the workgroup has at least K threads)
 template <int K>
 __device__ __forceinline__ uint32_t tile_share_init(const uint32_t* counts, uint32_t n_tiles, uint32_t t0,
                                                     uint32_t* s_pre, uint32_t* s_tsum, const uint2* tregion = nullptr,
                                                     int cls = -1, uint32_t* s_tbase = nullptr) {
-  static_assert(K >= 1 && K <= 64 && (K & (K - 1)) == 0, "K: power of two <= 64");
-  if (threadIdx.x < 64) {
-    const uint32_t l = threadIdx.x;
-    const bool in = l < K && t0 + l < n_tiles;
-    const uint32_t c = in ? counts[t0 + l] : 0u;
-    const uint32_t inc = wave_incl_scan(c);
+  static_assert(K >= 1 && K <= 256 && (K & (K - 1)) == 0, "K: power of two <= 256");
+  constexpr uint32_t kW = (K + 63) / 64;
+  __shared__ uint32_t s_wsum[4];
+  const uint32_t l = threadIdx.x, wv = l >> 6;
+  const bool in = l < K && t0 + l < n_tiles;
+  uint32_t c = 0, inc = 0;
+  if (wv < kW) {
+    c = in ? counts[t0 + l] : 0u;
+    inc = wave_incl_scan(c);
+    if (kW > 1 && (l & 63) == 63) s_wsum[wv] = inc;
+  }
+  if constexpr (kW > 1) __syncthreads();
+  if (wv < kW) {
+#pragma unroll
+    for (uint32_t v = 0; v + 1 < kW; v++) inc += v < wv ? s_wsum[v] : 0u;
     if (l < K) {
       s_pre[l] = inc - c;
       uint32_t b0 = 0;
@@ -756,7 +767,7 @@ __device__ __forceinline__ uint32_t tile_share_init(const uint32_t* counts, uint
       s_tsum[l] = b0;
       if (s_tbase) s_tbase[l] = b0;
     }
-    if (l == 63) s_pre[K] = inc;
+    if (l == (K < 64 ? 63u : (uint32_t)K - 1)) s_pre[K] = inc;
   }
   __syncthreads();
   return s_pre[K];
@@ -772,10 +783,10 @@ __device__ __forceinline__ uint32_t tile_of(const uint32_t* s_pre, uint32_t q) {
 }
 
 template <int K>
-__device__ __forceinline__ void tile_share_flush(const Work& w, uint32_t t0, const uint32_t* s_tsum,
+__device__ __forceinline__ void tile_share_flush(const Work& w, uint32_t t0, uint32_t t1, const uint32_t* s_tsum,
                                                  const uint32_t* s_tbase = nullptr) {
   __syncthreads();
-  if (threadIdx.x < K && t0 + threadIdx.x < w.n_tiles) {
+  if (threadIdx.x < K && t0 + threadIdx.x < t1) {
     const uint32_t v = s_tsum[threadIdx.x] - (s_tbase ? s_tbase[threadIdx.x] : 0u);
     if (v) atomicAdd(&w.tile_tok[t0 + threadIdx.x], v);
   }
@@ -856,7 +867,7 @@ __global__ __launch_bounds__(MID ? 128 : 256) void k_bpe_generic(Work w, Tables 
     if (MID) atomicAdd(&w.tile_tok[tile], cnt);
     else atomicAdd(&s_tsum[kt], cnt);
   }
-  if (!MID) tile_share_flush<kTilesGeneric>(w, t0, s_tsum);
+  if (!MID) tile_share_flush<kTilesGeneric>(w, t0, w.n_tiles, s_tsum);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1110,26 +1121,28 @@ __device__ __forceinline__ uint32_t merge_lds8(const Tables& t, const PairLds& P
 }
 
 // Workgroup-shared scratch of a merge pass.
-template <uint32_t SORTCAP>
+template <uint32_t SORTCAP, int KT = 64>
 struct PassLds {
-  uint32_t pre[65], tsum[64], tbase[64], stat[2], bcnt[4], bfill[4], chunk, next;
+  uint32_t pre[KT + 1], tsum[KT], tbase[KT], stat[2], bcnt[4], bfill[4], chunk, take, next;
   uint16_t perm[SORTCAP];  // the chunk's entries ordered by length bucket
 };
 
 // Merge pass over one length class (N = 8, 16, 32 slots), run by a persistent grid:
-// workgroups take chunks of 64 tiles from a counter (counters[ctr_chunk(class)]) and walk the chunk's
+// workgroups take chunks of 64-tile units from a counter (up to KT / 64 units at once when the
+// previous chunk left most of the workgroup idle: sparse classes) (counters[ctr_chunk(class)]) and walk the chunk's
 // class lists as one concatenated list (see tile_share_init).  Thread per piece, tokens and pair
 // ranks in registers (fully unrolled, compile-time slots).
 // `load` fills the workgroup's LDS tables (image, byte -> id); it runs at the first chunk with
 // work, so a workgroup that finds only empty lists never reads the 32..96 KiB image (`loaded`
 // is shared by the passes of one kernel).
 // L8: the <= 8-token tier runs in LDS (merge_lds8, narrow vocabularies; s_key / s_tok its state).
-template <int N, bool COMPACT, bool HOT, uint32_t NT, uint32_t SORTCAP, bool L8 = false, typename Load>
+template <int N, bool COMPACT, bool HOT, uint32_t NT, uint32_t SORTCAP, bool L8 = false, int KT = 64, typename Load>
 __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const PairLds& P, const int32_t* s_b2id,
-                                           PassLds<SORTCAP>& S, bool& loaded, Load&& load,
+                                           PassLds<SORTCAP, KT>& S, bool& loaded, Load&& load,
                                            lds_u32* s_key = nullptr, lds_u16* s_tok = nullptr) {
   using LC = LdsClass<N>;
-  constexpr int K = 64;
+  constexpr int K = KT;
+  static_assert(KT <= (int)NT, "a thread per chunk tile");
   const uint32_t tid = threadIdx.x;
   uint32_t* err = &w.counters[2];
   const uint32_t* list = class_list<N>(w);
@@ -1143,15 +1156,17 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
   // chunks of K tiles dealt dynamically (one atomic per chunk, taken by thread 0 and broadcast
   // through LDS): workgroups that start late, or whose CU is shared, take fewer chunks
   __syncthreads();
+  uint32_t take = 1;  // 64-tile units of the next chunk (workgroup-uniform)
   for (;;) {
     if (tid == 0) {
-      S.chunk = atomicAdd(&w.counters[ctr_chunk(LC::cls)], 1u);
+      S.chunk = atomicAdd(&w.counters[ctr_chunk(LC::cls)], take);
+      S.take = take;
       S.next = 0;
     }
     __syncthreads();
-    const uint32_t c0 = S.chunk * K;
+    const uint32_t c0 = S.chunk * 64;
     if (c0 >= w.n_tiles) break;
-    const uint32_t tb1 = min(w.n_tiles, c0 + K);
+    const uint32_t tb1 = min(w.n_tiles, c0 + 64 * S.take);
     const uint32_t E = tile_share_init<K>(counts, tb1, c0, S.pre, S.tsum, w.tregion, LC::cls, S.tbase);
     if (E && !loaded) {  // E is workgroup-uniform (read from LDS after a barrier)
       load();
@@ -1313,7 +1328,13 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
         if (i < E) body(e, kt, wv);
       }
     }
-    tile_share_flush<K>(w, c0, S.tsum, S.tbase);
+    tile_share_flush<K>(w, c0, tb1, S.tsum, S.tbase);
+    // size the next chunk for about two entries per thread (up to K tiles): sparse classes take
+    // several units at once, dense ones one; never more than a fair share of the units left, so
+    // the last chunks stay small (C2: 504 units for 256 workgroups)
+    const uint32_t units = (w.n_tiles + 63) / 64, next = S.chunk + S.take;
+    const uint32_t share = next < units ? (units - next) / gridDim.x : 0u;
+    take = min(min((uint32_t)K / 64, max(1u, share)), max(1u, (2 * NT * S.take + E) / (E + 1)));
     __syncthreads();
   }
   // statistics: bytes merged and ids produced by this pass (algorithmic bytes for the roofline)
@@ -1371,12 +1392,17 @@ __global__ __launch_bounds__(1024) void k_bpe_short(Work w, Tables t) {
 // main stream after class 2; both instances take chunks from the same counter, so a handful of
 // class-3 pieces (long merge chains) is done by the side instance in the shadow of the main
 // stream's passes, and a large class 3 (multilingual text) is shared by both as CUs free up.
+// Most tiles per chunk of the 17..32 B / 33..64 B passes: these classes can be sparse (C4: ~5
+// class-2 pieces per tile), where 64 tiles left most of a 512-thread workgroup idle per chunk.
+template <int CLS> struct MidCfg { static constexpr int KT = 256; };
+
 template <bool COMPACT, int CLS, bool NARROW>
 __global__ __launch_bounds__(512) void k_bpe_mid(Work w, Tables t) {
   if (spec_failed(w)) return;
+  constexpr int KT = MidCfg<CLS>::KT;
   extern __shared__ __attribute__((aligned(16))) uint4 s_img[];
   __shared__ int32_t s_b2id[256];
-  __shared__ PassLds<kSortCap> S;
+  __shared__ PassLds<kSortCap, KT> S;
   __shared__ uint32_t s_key[NARROW ? 8 * 512 : 1];
   __shared__ uint16_t s_tok[NARROW ? 8 * 512 : 1];
   // (the image is loaded up front: a lazy load pushes the 64-slot pass into scratch; the kernel
@@ -1389,8 +1415,8 @@ __global__ __launch_bounds__(512) void k_bpe_mid(Work w, Tables t) {
   for (uint32_t i = tid; i < 256; i += 512) s_b2id[i] = t.byte2id[i];
   bool loaded = true;
   const PairLds P{(const lds_u64*)s_img, (const lds_u32*)(s_img + kHotBuckets)};
-  class_pass<CLS == 2 ? 32 : 64, COMPACT, true, 512, kSortCap, NARROW>(w, t, P, s_b2id, S, loaded, [] {},
-                                                                     (lds_u32*)s_key, (lds_u16*)s_tok);
+  class_pass<CLS == 2 ? 32 : 64, COMPACT, true, 512, kSortCap, NARROW, KT>(w, t, P, s_b2id, S, loaded, [] {},
+                                                                         (lds_u32*)s_key, (lds_u16*)s_tok);
 }
 
 template <bool C, int CLS, bool NW>
