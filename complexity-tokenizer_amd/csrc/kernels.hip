@@ -2316,6 +2316,7 @@ hipError_t launch_bpe_long(const Work& w, const Tables& t, hipStream_t s, uint32
 // VGPRs alone and the record -> scratch chains of 8 waves per SIMD overlap.
 
 constexpr int kEmitWaves = 4;  // tiles per k_emit workgroup
+constexpr uint32_t kEmitStage = 1024;  // ids of one round staged in LDS (4 KiB per wave)
 
 __device__ __forceinline__ uint32_t rec_count(const Work& w, uint32_t v) {
   return (v & kRecHit) ? 1u : (v & kRecLong) ? w.long_cnt[v & kRecLongMask] : (v & 0xFFFFu);
@@ -2339,6 +2340,9 @@ __global__ __launch_bounds__(64 * kEmitWaves) void k_emit(Work w, uint32_t* __re
     return j0 < np ? *reinterpret_cast<const uint4*>(tcnt + j0) : make_uint4(0, 0, 0, 0);
   };
   uint32_t run = 0;  // ids of the earlier rounds (wave-uniform)
+  uint32_t r_first = 0;  // the current round's first id within the tile (wave-uniform)
+  __shared__ uint32_t s_stage[kEmitWaves][kEmitStage];
+  lds_u32* stage = (lds_u32*)s_stage[threadIdx.x >> 6];
   uint4 nx = load(4 * lane);
   for (uint32_t r0 = 0; r0 < np; r0 += 256) {
     const uint32_t j0 = r0 + 4 * lane;
@@ -2375,20 +2379,41 @@ __global__ __launch_bounds__(64 * kEmitWaves) void k_emit(Work w, uint32_t* __re
               : ((r & kRecAlt) ? w.lscratch + (size_t)tile * kTile : src0) + ((r >> 16) & 0xFFFu);
       v0[k] = (r & kRecHit) ? (r & kRecIdMask) : (follow ? sp[k][0] : 0u);
     }
+    // the round's ids: staged in LDS when they fit, then written out by the whole wave as 64
+    // consecutive dwords per store (whole lines; the lanes' own runs are ~5 ids apart, so direct
+    // stores touch a dozen partial lines each); else each lane stores its runs itself
+    const uint32_t r_ids = run - r_first;
+    const bool staged = r_ids <= kEmitStage;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       const uint32_t r = rec[k], cj = c[k];
       const uint64_t dst = base + o;
-      if (cj > 0 && dst < ids_cap) ids[dst] = v0[k];
-      if (cj > 1) {  // merged / long piece: the rest of its ids, four loads in flight at a time
-        const uint32_t* spk = sp[k];
-        for (uint32_t m = 1; m < cj; m += 4) {
-          uint32_t x[4];
+      if (staged) {
+        const uint32_t so = o - r_first;
+        if (cj > 0) stage[so] = v0[k];
+        if (cj > 1) {
+          const uint32_t* spk = sp[k];
+          for (uint32_t m = 1; m < cj; m += 4) {
+            uint32_t x[4];
 #pragma unroll
-          for (int i = 0; i < 4; i++) x[i] = m + i < cj ? spk[m + i] : 0u;
+            for (int i = 0; i < 4; i++) x[i] = m + i < cj ? spk[m + i] : 0u;
 #pragma unroll
-          for (int i = 0; i < 4; i++)
-            if (m + i < cj && dst + m + i < ids_cap) ids[dst + m + i] = x[i];  // the host reports CTOK_E_CAPACITY when short
+            for (int i = 0; i < 4; i++)
+              if (m + i < cj) stage[so + m + i] = x[i];
+          }
+        }
+      } else {
+        if (cj > 0 && dst < ids_cap) ids[dst] = v0[k];
+        if (cj > 1) {  // merged / long piece: the rest of its ids, four loads in flight at a time
+          const uint32_t* spk = sp[k];
+          for (uint32_t m = 1; m < cj; m += 4) {
+            uint32_t x[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) x[i] = m + i < cj ? spk[m + i] : 0u;
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+              if (m + i < cj && dst + m + i < ids_cap) ids[dst + m + i] = x[i];  // the host reports CTOK_E_CAPACITY when short
+          }
         }
       }
       if ((r & kRecDoc) && j0 + k < np) {
@@ -2398,6 +2423,14 @@ __global__ __launch_bounds__(64 * kEmitWaves) void k_emit(Work w, uint32_t* __re
       if (w.keep_first && j0 + k < np) tcnt[j0 + k] = o;  // ctok_encode_offsets
       o += cj;
     }
+    if (staged) {
+      wave_sync_lds();
+      const uint64_t d0 = base + r_first;
+      for (uint32_t i = lane; i < r_ids; i += 64)
+        if (d0 + i < ids_cap) ids[d0 + i] = stage[i];
+      wave_sync_lds();  // (the next round's staging overwrites the buffer)
+    }
+    r_first = run;
   }
 }
 
