@@ -199,18 +199,25 @@ __device__ __forceinline__ uint32_t rank_of(const Tables& t, uint32_t a, uint32_
 // doc-start bitmap
 
 // (empty documents set no bit and are counted into counters[kCtrEmptyDocs], one atomic per wave)
-__global__ void k_docstart(const uint64_t* __restrict__ off, uint32_t n_docs, uint32_t* __restrict__ bits,
-                           uint32_t* __restrict__ counters) {
+// Doc-start bitmap (zeroed first).  Offsets are sorted: a doc whose start word holds no other
+// doc's start (the previous doc's start and the next one's lie in other words) sets its bit with a
+// plain store, the rest with an atomic OR (no other doc can share a word stored plainly).
+__global__ __launch_bounds__(256) void k_docstart(const uint64_t* __restrict__ off, uint32_t n_docs,
+                                                  uint32_t* __restrict__ bits, uint32_t* __restrict__ counters) {
   const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
   bool empty = false;
   if (d < n_docs) {
-    const uint64_t a = off[d], b = off[d + 1];
-    if (a < b) atomicOr(&bits[a >> 5], 1u << (a & 31));
-    empty = a == b;
+    const uint64_t x = off[d], y = off[d + 1], p = d ? off[d - 1] : ~0ull;
+    empty = x == y;
+    if (!empty) {
+      const uint64_t wd = x >> 5;
+      if ((p >> 5) != wd && (y >> 5) != wd) bits[wd] = 1u << (x & 31);
+      else atomicOr(&bits[wd], 1u << (x & 31));
+    }
   }
-  const uint64_t m = __ballot(empty);
-  if (m && (threadIdx.x & 63) == (uint32_t)__ffsll((unsigned long long)m) - 1)
-    atomicAdd(&counters[kCtrEmptyDocs], (uint32_t)__popcll(m));
+  const uint64_t me = __ballot(empty);
+  if (me && (threadIdx.x & 63) == (uint32_t)__ffsll((unsigned long long)me) - 1)
+    atomicAdd(&counters[kCtrEmptyDocs], (uint32_t)__popcll(me));
 }
 
 hipError_t launch_docstart(const Work& w, hipStream_t s) {
@@ -647,24 +654,16 @@ hipError_t launch_segment(const Work& w, const Tables& t, hipStream_t s) {
 }
 
 // pieces in the batch (statistics only): one workgroup sums tile_np into counters[5]
-__global__ __launch_bounds__(1024) void k_count_pieces(Work w) {
+__global__ __launch_bounds__(256) void k_count_pieces(Work w) {
   if (spec_failed(w)) return;
-  __shared__ uint32_t s_red[16];
   uint32_t c = 0;
-  for (uint32_t i = threadIdx.x; i < w.n_tiles; i += 1024) c += w.tile_np[i];
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) c += (uint32_t)__shfl_xor((int)c, o, 64);
-  if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = c;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t sum = 0;
-    for (int k = 0; k < 16; k++) sum += s_red[k];
-    w.counters[5] = sum;
-  }
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < w.n_tiles; i += gridDim.x * 256) c += w.tile_np[i];
+  c = wave_sum_full_u32(c);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(&w.counters[5], c);  // (counters are zeroed per call)
 }
 
 hipError_t launch_count_pieces(const Work& w, hipStream_t s) {
-  k_count_pieces<<<1, 1024, 0, s>>>(w);
+  k_count_pieces<<<std::min<uint32_t>((w.n_tiles + 1023) / 1024, 256), 256, 0, s>>>(w);
   return hipGetLastError();
 }
 
