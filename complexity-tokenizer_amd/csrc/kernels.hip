@@ -1333,7 +1333,7 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
     // the last chunks stay small (C2: 504 units for 256 workgroups)
     const uint32_t units = (w.n_tiles + 63) / 64, next = S.chunk + S.take;
     const uint32_t share = next < units ? (units - next) / gridDim.x : 0u;
-    take = min(min((uint32_t)K / 64, max(1u, share)), max(1u, (2 * NT * S.take + E) / (E + 1)));
+    take = min(min((uint32_t)K / 64, max(1u, share)), N <= 16 ? 64u : max(1u, (2 * NT * S.take + E) / (E + 1)));
     __syncthreads();
   }
   // statistics: bytes merged and ids produced by this pass (algorithmic bytes for the roofline)
@@ -1359,6 +1359,9 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
 // left, with no kernel boundary in between.  NARROW (every id < 2^16): 960 threads, the last
 // tier's state in LDS (merge_lds8); else 1024 threads, all tiers in registers.
 template <bool NARROW> struct ShortCfg { static constexpr uint32_t NT = NARROW ? 960 : 1024; };
+// tiles per chunk of the <= 16 B passes (dense classes: ~100 + ~60 pieces per tile on C4; 128
+// tiles per chunk measured 3% slower, profiles/r02/v30_ab_short_kt128.txt)
+constexpr int kShortKT = 64;
 
 template <bool COMPACT, bool NARROW>
 __global__ __launch_bounds__(1024) void k_bpe_short(Work w, Tables t) {
@@ -1366,7 +1369,7 @@ __global__ __launch_bounds__(1024) void k_bpe_short(Work w, Tables t) {
   constexpr uint32_t NT = ShortCfg<NARROW>::NT;
   extern __shared__ __attribute__((aligned(16))) uint4 s_img[];
   __shared__ int32_t s_b2id[256];
-  __shared__ PassLds<kSortCap> S;
+  __shared__ PassLds<kSortCap, kShortKT> S;
   __shared__ uint32_t s_key[NARROW ? 8 * NT : 1];
   __shared__ uint16_t s_tok[NARROW ? 8 * NT : 1];
   const uint32_t tid = threadIdx.x;
@@ -1379,8 +1382,8 @@ __global__ __launch_bounds__(1024) void k_bpe_short(Work w, Tables t) {
   const PairLds P{(const lds_u64*)s_img, (const lds_u32*)(s_img + kHotBuckets)};
   lds_u32* sk = (lds_u32*)s_key;
   lds_u16* st = (lds_u16*)s_tok;
-  class_pass<8, COMPACT, true, NT, kSortCap, NARROW>(w, t, P, s_b2id, S, loaded, load, sk, st);
-  class_pass<16, COMPACT, true, NT, kSortCap, NARROW>(w, t, P, s_b2id, S, loaded, load, sk, st);
+  class_pass<8, COMPACT, true, NT, kSortCap, NARROW, kShortKT>(w, t, P, s_b2id, S, loaded, load, sk, st);
+  class_pass<16, COMPACT, true, NT, kSortCap, NARROW, kShortKT>(w, t, P, s_b2id, S, loaded, load, sk, st);
 }
 
 // Pieces of 17..32 bytes (CLS = 2, on the main stream after k_bpe_short) or 33..64 bytes (CLS = 3,
