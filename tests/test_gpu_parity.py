@@ -109,6 +109,41 @@ def test_llama3_sample(llama3_path):
     assert_same(ids, toff, *rc.encode_packed(text, off))
 
 
+def test_long_piece_tiers_and_order(llama3_path):
+    """Long pieces of every tier in one batch: lengths at the tier bounds (<= 256 B dense tier,
+    257..1024 and 1025..4096 B segmented tiers, > 4096 B global-memory tier) and random ones, as
+    random letters, concatenated words and single-letter repeats.  Exercises k_long_len /
+    k_long_order (length buckets, longest-first order) and the per-tier dynamic take
+    (kernels.hip), against the C oracle."""
+    with open(llama3_path) as f:
+        obj = json.load(f)
+    tok = Tokenizer.from_file(llama3_path)
+    rc = ref_c.RefC(obj)
+    rng = np.random.default_rng(77)
+    words = [w.encode() for w in "the of and tokenizer merge piece order round wave tier bucket".split()]
+    def run(n, kind):
+        if kind == 0:
+            return bytes(rng.integers(ord("a"), ord("z") + 1, size=n).astype(np.uint8))
+        if kind == 1:
+            b = b""
+            while len(b) < n:
+                b += words[int(rng.integers(len(words)))]
+            return b[:n]
+        return bytes([int(rng.integers(ord("a"), ord("z") + 1))]) * n
+    lengths = [63, 64, 65, 255, 256, 257, 1023, 1024, 1025, 2048, 4095, 4096, 4097, 5000]
+    lengths += [int(x) for x in rng.integers(65, 1500, size=150)]
+    docs = []
+    for i, n in enumerate(lengths):
+        for kind in range(3):
+            docs.append(b"x " + run(n, kind) + b" y")
+        docs.append(b"short doc %d" % i)  # ordinary pieces between the long ones
+    rng.shuffle(docs)
+    text, off = corpus.pack(docs)
+    ids, toff = tok.encode_packed(text, off, timing=True)
+    assert tok.last_stats["long_pieces"] >= 3 * 150
+    assert_same(ids, toff, *rc.encode_packed(text, off))
+
+
 def test_multi_sample(multi_path):
     with open(multi_path) as f:
         obj = json.load(f)
