@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <mutex>
 #include <type_traits>
 
 #include "ctok_internal.h"
@@ -1421,14 +1422,28 @@ __global__ __launch_bounds__(512) void k_bpe_mid(Work w, Tables t) {
                                                                          (lds_u32*)s_key, (lds_u16*)s_tok);
 }
 
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device): the attribute is set
+// on the current device's instance of the kernel, and ctok_exec.devices launches from one host
+// thread per device at once, so the flag is a per-device bit under a lock (one per kernel).
+struct LdsAttr {
+  std::mutex mu;
+  uint64_t done = 0;  // bit d: set on device d (ordinals >= 64 set it on every call)
+};
+static hipError_t lds_attr_once(LdsAttr& a, const void* fn, size_t bytes) {
+  int dev = 0;
+  HIPCHK(hipGetDevice(&dev));
+  const uint64_t bit = dev < 64 ? 1ull << dev : 0ull;
+  std::lock_guard<std::mutex> lk(a.mu);
+  if (a.done & bit) return hipSuccess;
+  HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+  a.done |= bit;
+  return hipSuccess;
+}
+
 template <bool C, int CLS, bool NW>
 static hipError_t launch_mid_t(const Work& w, const Tables& t, hipStream_t s) {
-  static bool attr = false;
-  if (!attr) {
-    HIPCHK(hipFuncSetAttribute((const void*)k_bpe_mid<C, CLS, NW>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)kLdsImageBytes));
-    attr = true;
-  }
+  static LdsAttr attr;
+  HIPCHK(lds_attr_once(attr, (const void*)k_bpe_mid<C, CLS, NW>, kLdsImageBytes));
   if (!w.n_tiles) return hipSuccess;
   k_bpe_mid<C, CLS, NW><<<min((w.n_tiles + 63) / 64, w.n_cus), 512, kLdsImageBytes, s>>>(w, t);
   return hipGetLastError();
@@ -1440,12 +1455,8 @@ static hipError_t launch_mid(const Work& w, const Tables& t, hipStream_t s) {
 
 template <bool C, bool NW>
 static hipError_t launch_short_t(const Work& w, const Tables& t, hipStream_t s) {
-  static bool attr = false;
-  if (!attr) {
-    HIPCHK(hipFuncSetAttribute((const void*)k_bpe_short<C, NW>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)kLdsImageBytes));
-    attr = true;
-  }
+  static LdsAttr attr;
+  HIPCHK(lds_attr_once(attr, (const void*)k_bpe_short<C, NW>, kLdsImageBytes));
   if (!w.n_tiles) return hipSuccess;
   k_bpe_short<C, NW><<<min((w.n_tiles + 63) / 64, w.n_cus), ShortCfg<NW>::NT, kLdsImageBytes, s>>>(w, t);
   return hipGetLastError();
@@ -2247,14 +2258,10 @@ __global__ __launch_bounds__(64 * NW) void k_bpe_wave(Work w, Tables t) {
 
 template <int K, uint32_t LO, int NW, bool HOT, bool SEG>
 static hipError_t launch_wave(const Work& w, const Tables& t, uint32_t grid, hipStream_t s) {
-  static bool attr = false;
+  static LdsAttr attr;
   const size_t slice = SEG ? SegSlice<K>::kBytes : WaveSlice<K>::kBytes;
   const size_t lds = (HOT ? kLdsImageBytes : kBloomWords * 4) + (size_t)NW * slice;
-  if (!attr) {
-    HIPCHK(hipFuncSetAttribute((const void*)k_bpe_wave<K, LO, NW, HOT, SEG>,
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    attr = true;
-  }
+  HIPCHK(lds_attr_once(attr, (const void*)k_bpe_wave<K, LO, NW, HOT, SEG>, lds));
   k_bpe_wave<K, LO, NW, HOT, SEG><<<grid, 64 * NW, lds, s>>>(w, t);
   return hipGetLastError();
 }
