@@ -164,6 +164,7 @@ SIGS = {
     "ctok_trainer_create": (ctypes.c_int, [ctypes.POINTER(TrainerConfig), ctypes.POINTER(_p)]),
     "ctok_trainer_destroy": (None, [_p]),
     "ctok_trainer_count": (ctypes.c_int, [_p, _p, _p, _u64, ctypes.c_int]),
+    "ctok_trainer_clear_counts": (ctypes.c_int, [_p, ctypes.c_int]),
     "ctok_trainer_train": (ctypes.c_int, [_p, ctypes.c_int]),
     "ctok_trainer_train_words": (ctypes.c_int, [_p, _p, _p, _p, _u64]),
     "ctok_trainer_vocab_size": (_u64, [_p]),

@@ -27,15 +27,33 @@ def _rust_lines(data: bytes, path: str):
     parts = data.split(b"\n")
     if parts[-1] == b"":
         parts.pop()
-    out = []
-    for p in parts:
-        if p.endswith(b"\r"):
-            p = p[:-1]
-        try:
-            out.append(p.decode("utf-8"))
-        except UnicodeDecodeError:
-            raise IOError("stream did not contain valid UTF-8 (%s)" % path) from None
-    return out
+    return [_line(p, path) for p in parts]
+
+
+def _line(p: bytes, path: str) -> str:
+    if p.endswith(b"\r"):
+        p = p[:-1]
+    try:
+        return p.decode("utf-8")
+    except UnicodeDecodeError:
+        raise IOError("stream did not contain valid UTF-8 (%s)" % path) from None
+
+
+def _file_line_blocks(path: str, block: int):
+    """The lines of a file as BufRead::lines yields them, in lists of about `block` bytes (the file
+    is streamed, never held whole)."""
+    with open(path, "rb") as f:  # IOError as the reference's File::open / read
+        carry = b""
+        while True:
+            data = f.read(block)
+            if not data:
+                break
+            parts = (carry + data).split(b"\n")
+            carry = parts.pop()  # the unfinished last line (b"" after a trailing newline)
+            if parts:
+                yield [_line(p, path) for p in parts]
+        if carry:
+            yield [_line(carry, path)]
 
 
 class Trainer:
@@ -92,15 +110,20 @@ class Trainer:
         if rc:
             _raise(rc)
 
-    def train(self, files):
-        """Train on text files, one text per line (src/trainer.rs:187-193, count_words :265-285)."""
+    def train(self, files, block_bytes: int = 64 << 20):
+        """Train on text files, one text per line (src/trainer.rs:187-193, count_words :265-285).
+        Files are read and counted in blocks of about `block_bytes`; on an unreadable file or a
+        line that is not UTF-8 the counts made so far are dropped and IOError is raised, as the
+        reference returns the error before anything is trained."""
         if isinstance(files, (str, bytes)):
             raise TypeError("Can't extract `str` to `Vec`")
-        lines = []
-        for p in list(files):
-            with open(p, "rb") as f:  # IOError as the reference's File::open / read
-                lines += _rust_lines(f.read(), p)
-        self._count(lines, False)
+        try:
+            for p in list(files):
+                for lines in _file_line_blocks(p, block_bytes):
+                    self._count(lines, False)
+        except BaseException:
+            _n.lib.ctok_trainer_clear_counts(self._h, 0)
+            raise
         self._train(False)
 
     def train_from_iterator(self, texts):

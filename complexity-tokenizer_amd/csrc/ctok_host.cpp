@@ -1790,6 +1790,12 @@ int ctok_create_from_tables(const ctok_tables* tb, ctok** out) {
       auto a = by_id.find(tb->merge_left[r]), b = by_id.find(tb->merge_right[r]);
       if (a == by_id.end() || b == by_id.end())
         throw_err(CTOK_E_ARG, "merge " + std::to_string(r) + " names an id that is not in the vocab");
+      // the reference joins every merge to "a b" and keeps it only when it splits on ' ' into
+      // exactly two parts (src/huggingface/mod.rs:252-264, array form :87-94): a token holding a
+      // space would be dropped silently and shift every later rank, so the table is refused
+      if (a->second.find(' ') != std::string::npos || b->second.find(' ') != std::string::npos)
+        throw_err(CTOK_E_ARG, "merge " + std::to_string(r) +
+                                  " joins a token that contains ' ': the reference's merge format cannot express it");
       merges.arr.push_back(str(a->second + " " + b->second));
     }
     for (uint64_t i = 0; i < tb->n_added; i++) {

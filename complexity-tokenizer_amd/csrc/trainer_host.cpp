@@ -19,6 +19,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <map>
@@ -162,10 +163,28 @@ struct ctok_trainer {
       throw_error(CTOK_E_DEVICE, std::string("trainer pre-tokenizer: ") + ctok_last_error());
   }
 
-  // count_batch / count_words: every word (raw bytes of a piece) of >= min_word_length chars
+  // count_batch / count_words: every word (raw bytes of a piece) of >= min_word_length chars.
+  // The texts go to the GPU pre-tokenizer in doc-aligned chunks of about kCountChunk bytes (a
+  // longer text is a chunk by itself): one encode call is limited to 3.75 GiB and sizes its
+  // workspace from its text, while count_words streams any amount (src/trainer.rs:265-285).
   void count(const uint8_t* utf8, const uint64_t* off, uint64_t n, std::unordered_map<std::string, uint32_t>& into) {
     if (!n) return;
+    if (off[0] != 0) throw_error(CTOK_E_ARG, "offsets[0] must be 0");
     ensure_pretok();
+    uint64_t chunk = 256ull << 20;
+    if (const char* e = getenv("CTOK_TRAIN_CHUNK_BYTES")) chunk = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
+    std::vector<uint64_t> coff;
+    for (uint64_t d0 = 0; d0 < n;) {
+      uint64_t d1 = d0 + 1;  // at least one text per chunk
+      while (d1 < n && off[d1 + 1] - off[d0] <= chunk) d1++;
+      coff.resize(d1 - d0 + 1);
+      for (uint64_t i = d0; i <= d1; i++) coff[i - d0] = off[i] - off[d0];
+      count_chunk(utf8 + off[d0], coff.data(), d1 - d0, into);
+      d0 = d1;
+    }
+  }
+
+  void count_chunk(const uint8_t* utf8, const uint64_t* off, uint64_t n, std::unordered_map<std::string, uint32_t>& into) {
     std::vector<uint8_t> text;
     std::vector<uint64_t> noff;
     std::vector<uint32_t> pb;
@@ -465,6 +484,8 @@ int ctok_trainer_create(const ctok_trainer_config* cfg, ctok_trainer** out) {
     tr->vmax = cfg->inl_velocity_max;
     tr->beta_max = cfg->inl_beta_max;
     tr->device = cfg->device;
+    if (cfg->n_special && !cfg->special_off) throw_error(CTOK_E_ARG, "null special_off");
+    if (cfg->n_special && cfg->special_off[cfg->n_special] && !cfg->special) throw_error(CTOK_E_ARG, "null special");
     for (uint64_t i = 0; i < cfg->n_special; i++)
       tr->specials.emplace_back(cfg->special + cfg->special_off[i], cfg->special_off[i + 1] - cfg->special_off[i]);
     *out = tr.release();
@@ -478,6 +499,13 @@ int ctok_trainer_count(ctok_trainer* tr, const uint8_t* utf8, const uint64_t* of
   return ctok_host::run_guarded([&] {
     if (!tr || (n_texts && !off)) throw_error(CTOK_E_ARG, "null argument");
     tr->count(utf8, off, n_texts, into_accumulator ? tr->acc : tr->local);
+  });
+}
+
+int ctok_trainer_clear_counts(ctok_trainer* tr, int accumulator) {
+  return ctok_host::run_guarded([&] {
+    if (!tr) throw_error(CTOK_E_ARG, "null argument");
+    (accumulator ? tr->acc : tr->local).clear();
   });
 }
 
@@ -506,7 +534,7 @@ uint64_t ctok_trainer_num_merges(const ctok_trainer* tr) { return tr ? tr->merge
 
 int ctok_trainer_json(const ctok_trainer* tr, char* buf, size_t cap, size_t* len) {
   return ctok_host::run_guarded([&] {
-    if (!tr || !len) throw_error(CTOK_E_ARG, "null argument");
+    if (!tr || !len || (cap && !buf)) throw_error(CTOK_E_ARG, "null argument");
     const std::string j = tr->to_json();
     *len = j.size();
     if (buf) std::memcpy(buf, j.data(), std::min(cap, j.size()));
@@ -527,7 +555,7 @@ int ctok_trainer_save(const ctok_trainer* tr, const char* path) {
 int ctok_trainer_initial_pairs(const ctok_trainer* tr, uint32_t* a, uint32_t* b, int64_t* count, uint64_t cap,
                                uint64_t* n) {
   return ctok_host::run_guarded([&] {
-    if (!tr || !n) throw_error(CTOK_E_ARG, "null argument");
+    if (!tr || !n || (cap && (!a || !b || !count))) throw_error(CTOK_E_ARG, "null argument");
     *n = tr->initial.size();
     for (uint64_t i = 0; i < std::min<uint64_t>(cap, tr->initial.size()); i++) {
       a[i] = (uint32_t)(tr->initial[i].first >> 32);

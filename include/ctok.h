@@ -51,7 +51,9 @@ int ctok_create_from_buffer(const char* json, size_t len, ctok** out);
  * src/huggingface/mod.rs:247-334) on the model a ByteLevel BPE tokenizer.json describes.
  *   vocab:  token i = vocab[vocab_off[i] .. vocab_off[i+1]) (its byte-level string), id vocab_id[i]
  *   merges: merge r joins the tokens with ids merge_left[r], merge_right[r] (rank order; the new
- *           token is the vocab entry of their concatenated strings, as for "a b" merge strings)
+ *           token is the vocab entry of their concatenated strings, as for "a b" merge strings);
+ *           CTOK_E_ARG when either token's string contains ' ' (the reference splits "a b" on ' '
+ *           and silently drops such a merge, src/huggingface/mod.rs:252-264)
  *   added:  content i = added[added_off[i] .. added_off[i+1]), id added_id[i], CTOK_ADDED_* flags
  *   nfc:    1 = normalizer NFC, 0 = none; add_prefix_space: ByteLevel's flag */
 enum {

@@ -57,6 +57,11 @@ void ctok_trainer_destroy(ctok_trainer* tr);
 int ctok_trainer_count(ctok_trainer* tr, const uint8_t* utf8, const uint64_t* off, uint64_t n_texts,
                        int into_accumulator);
 
+/* Drop the counts of ctok_trainer_count(tr, ..., accumulator).  train(files) counts its files in
+ * blocks as it reads them; when a later line is not UTF-8 it drops what it counted, as the
+ * reference's count_words returns the io::Error before any count is kept (src/trainer.rs:265-285). */
+int ctok_trainer_clear_counts(ctok_trainer* tr, int accumulator);
+
 /* from_accumulator = 1: Trainer.finish_training (src/trainer.rs:223-229); 0: the training step of
  * train_from_iterator / train(files) on the counts of ctok_trainer_count(..., 0).  Both drop words
  * below min_frequency, then train_from_word_freqs (:231-243). */

@@ -204,6 +204,43 @@ def test_offsets_and_word_ids(base, variant):
             tok.encode_to_encoding(t)
 
 
+def test_offsets_many_tiles_long_pieces(base):
+    """the offsets walk over a batch of many pre-tokenizer tiles (~500 KB, 3968-byte
+    tiles), with pieces longer than 64 B (the long-piece records) and pieces crossing tile
+    boundaries, enough documents that the host walk is split over its threads mid-tile."""
+    import random
+    tok, ref = pair_of(base)
+    rng = random.Random(17)
+    words = ["the", "quick", "brown", "fox", "jumps", "over", "lazy", "dog", "caf\u00e9", "na\u00efve", "1234",
+             "it's", "we're", "!!", "...", "\u4e16\u754c"]
+    texts = []
+    for k in range(2500):
+        parts = []
+        for _ in range(rng.randrange(5, 60)):
+            r = rng.random()
+            if r < 0.03:
+                parts.append("".join(rng.choice("abcdefgh") for _ in range(rng.randrange(65, 400))))
+            elif r < 0.05:
+                parts.append(" " * rng.randrange(2, 90))
+            elif r < 0.06:
+                parts.append(str(rng.randrange(10 ** 12)) * rng.randrange(6, 12))
+            else:
+                parts.append(rng.choice(words))
+        texts.append(rng.choice([" ", "\n", "  "]).join(parts))
+    ok = []
+    for t in texts:
+        try:
+            ok.append((t, ref.encode_single_to_encoding(t, 0)))
+        except ref_py.PanicException:
+            pass
+    assert len(ok) > 1200 and sum(len(t.encode()) for t, _ in ok) > 400_000
+    got = tok.encode_offsets([t for t, _ in ok])
+    for (t, want), (ids, offs, wids) in zip(ok, got):
+        assert ids == want.ids, repr(t[:80])
+        assert offs == want.offsets, repr(t[:80])
+        assert wids == want.word_ids, repr(t[:80])
+
+
 def test_offsets_lookups(base):
     """char / word lookups over the GPU offsets, as the reference computes them."""
     tok, ref = pair_of(encoding_cases.with_post_processor(base, "bert"))

@@ -147,3 +147,66 @@ def test_larger_training_and_timing():
     a, b, c = gpu.initial_pairs()
     assert {(int(x), int(y)): int(z) for x, y, z in zip(a, b, c)} == ref.initial_pairs
     assert gpu.num_merges >= 2000 - len(ref.vocab)
+
+
+def test_merge_order_pinned_without_ties():
+    """The product against the independent Counter recount of tests/test_trainer_cpu.py on counts
+    with no equal live scores (the order does not depend on the tie-break choice)."""
+    from tests.test_trainer_cpu import naive_merges, tie_free_word_freqs
+    wf = tie_free_word_freqs()
+    target = 4 + 7 + 70
+    want = naive_merges(wf, target, 4 + 7)
+    t = Trainer(vocab_size=target, min_frequency=1, inl_gate=0.0)
+    t.train_from_word_freqs({w.encode(): f for w, f in wf.items()})
+    got = [tuple(m.split(" ")) for m in json.loads(t.to_str())["model"]["merges"]]
+    assert got == want
+
+
+def test_word_counting_in_chunks_equals_one_call(monkeypatch):
+    """count() hands the texts to the GPU pre-tokenizer in doc-aligned chunks
+    (CTOK_TRAIN_CHUNK_BYTES, default 256 MB); the counts, hence the training, must not depend on
+    the chunking (chunks of a few docs here, and a doc longer than a chunk)."""
+    texts = _c1_texts(600) + ["x" * 5000 + " tail"]
+    one = Trainer(vocab_size=300, min_frequency=2)
+    one.train_from_iterator(texts)
+    monkeypatch.setenv("CTOK_TRAIN_CHUNK_BYTES", "700")
+    many = Trainer(vocab_size=300, min_frequency=2)
+    many.train_from_iterator(texts)
+    assert one.to_str() == many.to_str()
+
+
+def test_train_files_streamed_in_blocks(tmp_path):
+    """train(files) reads and counts each file in blocks (lines cut by a block edge carried
+    over); small blocks and several files give the one-block result, and the oracle's."""
+    texts = _c1_texts(400)
+    paths = []
+    for k in range(3):
+        p = tmp_path / ("f%d.txt" % k)
+        p.write_bytes(("\r\n".join(texts[k::3]) + ("\n" if k != 1 else "")).encode())
+        paths.append(str(p))
+    big = Trainer(vocab_size=300, min_frequency=2)
+    big.train(paths)
+    small = Trainer(vocab_size=300, min_frequency=2)
+    small.train(paths, block_bytes=97)
+    assert big.to_str() == small.to_str()
+    ref = trainer_ref.RefTrainer(vocab_size=300, min_frequency=2)
+    ref.train_files(paths)
+    _same(small, ref)
+
+
+def test_train_files_bad_utf8_drops_partial_counts(tmp_path):
+    """A line that is not UTF-8 after blocks were counted: IOError, and the counts made so far are
+    dropped (the reference returns the error before keeping anything, src/trainer.rs:265-285), so a
+    later training sees only its own texts."""
+    good = tmp_path / "good.txt"
+    good.write_bytes(("hello world\n" * 200).encode())
+    bad = tmp_path / "bad.txt"
+    bad.write_bytes(b"fine line\n" * 50 + b"\xff\xfe\n")
+    t = Trainer(vocab_size=60, min_frequency=1)
+    with pytest.raises(IOError):
+        t.train([str(good), str(bad)], block_bytes=64)
+    t2 = Trainer(vocab_size=60, min_frequency=1)
+    other = ["abc abd abe"] * 5
+    t.train_from_iterator(other)
+    t2.train_from_iterator(other)
+    assert t.to_str() == t2.to_str()

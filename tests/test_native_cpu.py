@@ -215,3 +215,17 @@ def test_create_from_tables_matches_json(gpt2_path):
         assert a.id_to_token(i) == b.id_to_token(i)
     with pytest.raises(ValueError):
         Tokenizer.from_tables(vocab, [(0, 10 ** 9)])
+
+
+def test_create_from_tables_rejects_tokens_with_spaces():
+    """A merge of a token whose string contains ' ' cannot be written as the reference's "a b"
+    merge string: the reference would drop it and shift every later rank
+    (src/huggingface/mod.rs:252-264), so ctok_create_from_tables refuses the table (CTOK_E_ARG)."""
+    vocab = {c: i for i, c in enumerate(toys.byte_chars())}
+    n = len(vocab)
+    vocab.update({"a b": n, "a bc": n + 1, "ab": n + 2})
+    with pytest.raises(ValueError, match="contains ' '"):
+        Tokenizer.from_tables(vocab, [(vocab["a b"], vocab["c"])])
+    # tokens without spaces still load, and a vocab entry with a space that no merge joins is fine
+    t = Tokenizer.from_tables(vocab, [(vocab["a"], vocab["b"])])
+    assert t.token_to_id("a b") == n

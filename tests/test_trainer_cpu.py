@@ -113,3 +113,86 @@ def test_trainer_missing_file_is_ioerror(tmp_path):
     p.write_bytes(b"ok\n\xff\xfe\n")
     with pytest.raises(IOError):
         Trainer().train([str(p)])
+
+
+@pytest.mark.parametrize("block", [1, 2, 3, 5, 64, 1 << 20])
+def test_file_lines_streamed_in_blocks(tmp_path, block):
+    """train(files) reads files in blocks: the lines must be BufRead::lines' for any block size
+    (src/trainer.rs:272), including CRLF pairs and multi-byte chars cut by a block edge."""
+    from complexity_tokenizer.trainer import _file_line_blocks
+    for data in (b"", b"\n", b"a\r\nb\n\nc", b"x\n", "héllo wörld\r\n日本語\n\nend".encode(), b"\r\n\r\n", b"last"):
+        p = tmp_path / "f.txt"
+        p.write_bytes(data)
+        got = [ln for blk in _file_line_blocks(str(p), block) for ln in blk]
+        assert got == trainer_ref.rust_lines(data), (data, block)
+
+
+def naive_merges(word_freqs, n_vocab_target, n_base):
+    """An independent restatement of learn_merges_heap's merge ORDER with inl_gate = 0 (score =
+    pair count): string tokens, pair counts recounted from scratch with collections.Counter
+    (no incremental deltas, no ids), the heap rebuilt every 100 merges from the true counts and
+    popped in count order while stale entries are skipped (src/trainer.rs:407-520).  It asserts
+    that no pop meets a live entry of the same score, so the result does not depend on how equal
+    scores are ordered (the reference leaves that to hash order)."""
+    import collections
+    words = [[list(w), f] for w, f in word_freqs.items()]
+
+    def counts():
+        c = collections.Counter()
+        for toks, f in words:
+            for i in range(len(toks) - 1):
+                c[(toks[i], toks[i + 1])] += f
+        return c
+
+    merges, vocab = [], n_base
+    while vocab < n_vocab_target:
+        heap = sorted(counts().items(), key=lambda kv: -kv[1])
+        hi, progressed = 0, False
+        for _ in range(100):
+            if vocab >= n_vocab_target:
+                break
+            cur = counts()
+            while hi < len(heap) and cur.get(heap[hi][0], 0) <= 0:
+                hi += 1
+            if hi == len(heap):
+                break
+            (a, b), score = heap[hi]
+            ties = [p for p, s in heap[hi + 1:] if s == score and cur.get(p, 0) > 0]
+            assert not ties, "tie at merge %d: %r and %r (score %d)" % (len(merges), (a, b), ties[0], score)
+            hi += 1
+            merges.append((a, b))
+            vocab += 1
+            progressed = True
+            for w in words:  # apply_merge_incremental's left-to-right loop (:537-577)
+                toks, i = w[0], 0
+                while i < len(toks) - 1:
+                    if toks[i] == a and toks[i + 1] == b:
+                        toks[i:i + 2] = [a + b]
+                    else:
+                        i += 1
+        if not progressed or not any(v > 0 for v in counts().values()):
+            break
+    return merges
+
+
+def tie_free_word_freqs(seed=11, n_words=300):
+    rng = random.Random(seed)
+    wf = {}
+    while len(wf) < n_words:
+        w = "".join(rng.choice("abcdefg") for _ in range(rng.randint(2, 9)))
+        wf.setdefault(w, rng.randint(1, 10 ** 7))
+    return wf
+
+
+def test_trainer_oracle_merge_order_pinned_without_ties():
+    """the oracle's merge sequence against an independent Counter recount on counts
+    with no equal live scores, so the tie-break choice cannot hide a mistake.  Two heap builds
+    (more merges than the 49 initial pairs of a 7-letter alphabet)."""
+    wf = tie_free_word_freqs()
+    n_base = 4 + 7  # the default specials + the alphabet
+    target = n_base + 70
+    want = naive_merges(wf, target, n_base)
+    assert len(want) == 70
+    ref = trainer_ref.RefTrainer(vocab_size=target, min_frequency=1, inl_gate=0.0)
+    ref.train_from_word_freqs(dict(wf))
+    assert ref.merges == want
