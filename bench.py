@@ -344,7 +344,9 @@ def main():
                          "ms_emit": round(avg("ms_emit"), 4), "ms_call": round(avg("ms_total"), 4),
                          "B_alg": int(b_alg), "achieved_GBps": round(b_alg / (ms_dev * 1e-3) / 1e9, 2),
                          "pieces": int(P), "long_pieces": int(st["long_pieces"]),
-                         "kernel_MBps": round(n_bytes / (ms_dev * 1e-3) / 1e6, 1)},
+                         "kernel_MBps": round(n_bytes / (ms_dev * 1e-3) / 1e6, 1),
+                         "workspace_bytes": int(st["workspace_bytes"]),
+                         "workspace_B_per_byte": round(st["workspace_bytes"] / max(1, n_bytes), 2)},
             "cpu_baseline": cpu,
             "parity": parity,
         }

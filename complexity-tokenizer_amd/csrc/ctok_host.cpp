@@ -238,6 +238,16 @@ struct DeviceState {
   DevBuf<uint32_t> pad_ids, pad_special, pad_ctr, pad_out[4];
   DevBuf<uint64_t> pad_tokoff, pad_rowlen, pad_in_off;
   DevBuf<uint8_t> pad_in_text;
+  // bytes of device memory held for encode calls (the workspace, not the tokenizer tables)
+  uint64_t workspace_bytes() const {
+    uint64_t b = 0;
+    auto add = [&](const auto& x) { b += (uint64_t)x.cap * sizeof(*x.p); };
+    add(docbits), add(pbits), add(tile_np), add(tile_tok), add(tile_doc), add(tcls), add(list0), add(list1);
+    add(list2), add(list3), add(tcnt), add(scratch), add(lscratch), add(counters), add(lw), add(tregion);
+    add(wpref), add(long_cnt), add(long_ord), add(long_hist), add(long_list), add(mid_list), add(scan_tmp);
+    add(doc_flag), add(ncp), add(norm_off), add(norm_text);
+    return b;
+  }
   ~DeviceState() {
     if (device >= 0) {
       (void)hipSetDevice(device);
@@ -1356,6 +1366,7 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
     st->pieces = w.n_tiles ? P : 0;
     st->long_pieces = cnt[0];
     st->tokens = ntok;
+    st->workspace_bytes = ds->workspace_bytes();
     st->nfc_docs = nfc_docs;
     for (int c = 0; c < kNumClasses; c++) {
       st->class_bytes[c] = cnt[ctr_stat(c)];
@@ -1638,6 +1649,7 @@ RangeOut encode_host_range(ctok* t, DeviceState* ds, const uint8_t* text, const 
       st->pieces += cs.pieces;
       st->long_pieces += cs.long_pieces;
       st->nfc_docs += cs.nfc_docs;
+      st->workspace_bytes = std::max(st->workspace_bytes, cs.workspace_bytes);
       st->bytes_norm += cs.bytes_norm;
       for (int q = 0; q < kNumClasses; q++) {
         st->class_bytes[q] += cs.class_bytes[q];
@@ -2105,6 +2117,7 @@ int ctok_encode_batch(const ctok* tc, const uint8_t* utf8_in, const uint64_t* do
       for (size_t g = 0; g < G; g++) {
         const ctok_stats& q = sst[g];
         stats->pieces += q.pieces, stats->long_pieces += q.long_pieces, stats->nfc_docs += q.nfc_docs;
+        stats->workspace_bytes += q.workspace_bytes;  // (shards on one device report it once each)
         stats->bytes_norm += q.bytes_norm;
         for (int c = 0; c < kNumClasses; c++)
           stats->class_bytes[c] += q.class_bytes[c], stats->class_ids[c] += q.class_ids[c];

@@ -509,10 +509,10 @@ __global__ __launch_bounds__(64 * kSegWaves) void k_segment(Work w, Tables t) {
       uni((uint32_t)__shfl((int)(st ? (uint32_t)(kTileWords * 64 + __builtin_ctzll(st))
                                     : ((uint64_t)B <= (uint64_t)t0 + kTile + 62 ? (uint32_t)(B - t0) : 0xFFFFu)),
                            63, 64));
-  // expansion state: each tile word's lane emits the starts of its not yet emitted pieces
-  uint64_t rem = (!first && !last) ? st : 0ull;
-  uint32_t jj = inc - c;
-  const uint32_t wbase = (lane - 1) * 64;
+  // expansion state: the starts of this lane's word and the pieces of the tile before it
+  const uint64_t stw = (!first && !last) ? st : 0ull;
+  const uint32_t prew = inc - c;
+  uint32_t wcur = 1;  // the first word lane that can hold the next window's first piece (wave-uniform)
 
   // ---- C: thread per piece, kSegUnroll pieces per lane per round with their LDS lookups and
   // table probes issued together (each round is one dependent global round trip)
@@ -525,13 +525,19 @@ __global__ __launch_bounds__(64 * kSegWaves) void k_segment(Work w, Tables t) {
   constexpr uint32_t W = 64 * U;  // pieces per round
   for (uint32_t j0 = 0; j0 < np; j0 += W) {
     // expansion of this round's window [j0, j0 + W]: s_pos[j - j0] = start of piece j (the
-    // entry past the window is the next round's first piece, peeked, not consumed)
-    const uint32_t jend = min(j0 + W, np);
-    while (rem && jj <= jend) {
-      s_pos[jj - j0] = (uint16_t)(wbase + __builtin_ctzll(rem));
-      if (jj == j0 + W) break;
-      rem &= rem - 1;
-      jj++;
+    // entry past the window is the next round's first piece, peeked, not consumed).  One word
+    // at a time over the whole wave: lane b writes the start at bit b of the word, its piece
+    // index from the word's prefix and the set bits below b (mbcnt) -- about ten instructions
+    // per word, against a per-lane loop over its own word's starts whose trip count is the
+    // busiest word's (~20 per round).
+    for (uint32_t wl = wcur; wl <= (uint32_t)kTileWords; wl++) {  // (wave-uniform)
+      const uint32_t pw = uni(__builtin_amdgcn_readlane(prew, wl));
+      if (pw > j0 + W) break;  // this word and the later ones start no piece of the window
+      wcur = wl;
+      const uint64_t mk = ((uint64_t)uni(__builtin_amdgcn_readlane((uint32_t)(stw >> 32), wl)) << 32) |
+                          uni(__builtin_amdgcn_readlane((uint32_t)stw, wl));
+      const uint32_t k = pw + __builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u));
+      if (((mk >> lane) & 1ull) && k >= j0 && k <= j0 + W) s_pos[k - j0] = (uint16_t)((wl - 1) * 64 + lane);
     }
     if (lane == 0 && np <= j0 + W) s_pos[np - j0] = (uint16_t)tile_end;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

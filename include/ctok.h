@@ -136,6 +136,7 @@ typedef struct ctok_stats {
   uint64_t class_bytes[4];  /* text bytes merged per length class (<= 8, 9..16, 17..32, 33..64 B) */
   uint64_t class_ids[4];    /* ids produced per length class                             */
   double ms_bpe_med;      /* k_bpe_mid<3>, main-stream instance: pieces of 33..64 bytes    */
+  uint64_t workspace_bytes; /* device workspace held by the device for this tokenizer's calls */
 } ctok_stats;
 
 /* Upper bound on the ids of a batch whose docs total `n_bytes` bytes (ids <= 3*bytes + docs:

@@ -1,14 +1,16 @@
 #!/bin/bash
-# SQ counter pass (one rocprofv3 --pmc run per variant) over a short C2 bench: instruction mix and
-# wait cycles per kernel.  usage: bash tools/pmc_sq.sh TAG [VAR=VAL ...]  (env for the variant)
+# SQ counter pass (one rocprofv3 --pmc run per call) over a short bench: instruction mix, LDS and
+# wait cycles per kernel.  usage: bash tools/pmc_sq.sh TAG CONFIG "COUNTERS" [VAR=VAL ...]
+#   CONFIG: c4 | c2; COUNTERS: at most 8 SQ_* names (one pass); env VAR=VAL for the variant.
+# Build the C4 corpus cache first (an unprofiled bench run): a --pmc run must not fork a pool.
 set -e
-TAG=$1; shift
+TAG=$1; CFG=$2; CTRS=$3; shift 3
 OUT=$(pwd)/gpurun_out/sq_$TAG
 mkdir -p "$OUT"
 ROOT=$(pwd)
 cd /tmp
-env "$@" timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU \
-  --output-format csv -d "$OUT" -o run -- python3 "$ROOT/bench.py" --config c2 --steps 3 --warmup 1 --no-cpu-baseline --no-parity \
+env "$@" timeout -s KILL 120 rocprofv3 --pmc $CTRS \
+  --output-format csv -d "$OUT" -o run -- python3 "$ROOT/bench.py" --config $CFG --steps 3 --warmup 1 --no-cpu-baseline --no-parity --corpus-workers 1 \
   > "$OUT/log.txt" 2>&1 || { tail -20 "$OUT/log.txt"; exit 1; }
 python3 - "$OUT" <<'PY'
 import csv, glob, sys, collections
