@@ -205,7 +205,7 @@ struct DeviceState {
   DevBuf<uint64_t> merge_tab, lds_image, lds16_image, merge16;
   DevBuf<uint32_t> pair0;
   DevBuf<uint32_t> piece_tab;
-  DevBuf<uint32_t> rank_newid;
+  DevBuf<uint32_t> rank_newid, eager;
   DevBuf<int32_t> byte2id;
   DevBuf<uint8_t> cls_s1, cls_s2, nfc_s1, alnum, at_bytes, at_flags;
   DevBuf<uint16_t> nfc_s2, decomp_off;
@@ -297,6 +297,7 @@ struct ctok {
   std::vector<uint32_t> piece_tab;  // 4 u32 per slot (see ctok_internal.h piece_hash)
   uint32_t piece_mask = 0;
   std::vector<uint32_t> rank_newid;
+  std::vector<uint32_t> eager_bits;  // bit v: the merge of table value v is eager (see Tables::eager)
   int32_t byte2id[256];
   std::string at_bytes;
   std::vector<uint32_t> at_off{0}, at_id;
@@ -878,6 +879,23 @@ void load_root(ctok* t, const ctj::Value& root) {
     t->proper = true;
     for (size_t z = 0; z < maxprod.size(); z++)
       if (maxprod[z] != kUnset && mincons[z] != kUnset && mincons[z] <= maxprod[z]) { t->proper = false; break; }
+    // per merge (bit at its table value: the rank, or the new id in a compact table): "eager"
+    // when a merge consuming its token ranks before it.  Only an eager merge can be followed at
+    // once by a merge of lower rank, so the long-piece rounds apply every occurrence of a
+    // non-eager merge together even when the table as a whole is not rank-monotone (tiktoken-
+    // style lists), and the leftmost one alone for an eager merge (ctok_internal.h Tables::eager).
+    t->eager_bits.assign(((t->compact ? kMaxId + 2 : valid_new.size()) + 31) / 32 + 1, 0u);
+    if (!t->proper) {
+      for (const auto& kv : ranks) {
+        const uint32_t r = kv.second;
+        if (r >= valid_new.size()) continue;
+        const uint32_t z = valid_new[r];
+        if (mincons[z] != kUnset && mincons[z] < r) {
+          const uint32_t v = t->compact ? z : r;
+          t->eager_bits[v >> 5] |= 1u << (v & 31);
+        }
+      }
+    }
   }
 
 
@@ -1089,6 +1107,7 @@ DeviceState* device_state(ctok* t, int device) {
   }
   upload(ds->pair0, t->pair0.data(), t->pair0.size(), s);
   upload(ds->rank_newid, t->rank_newid.data(), t->rank_newid.size(), s);
+  upload(ds->eager, t->eager_bits.data(), t->eager_bits.size(), s);
   upload(ds->piece_tab, t->piece_tab.data(), t->piece_tab.size(), s);
   upload(ds->byte2id, t->byte2id, 256, s);
   upload(ds->cls_s1, ct_cls_stage1, sizeof(ct_cls_stage1), s);
@@ -1117,6 +1136,7 @@ DeviceState* device_state(ctok* t, int device) {
   tb.piece_tab = (const uint4*)ds->piece_tab.p;
   tb.piece_mask = t->piece_mask;
   tb.rank_newid = ds->rank_newid.p;
+  tb.eager = ds->eager.p;
   tb.n_ranks = (uint32_t)t->rank_newid.size();
   tb.byte2id = ds->byte2id.p;
   tb.cls_s1 = ds->cls_s1.p;

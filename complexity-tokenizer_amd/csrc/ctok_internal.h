@@ -39,6 +39,7 @@ __host__ __device__ constexpr int ctr_chunk(int c) { return c < 3 ? 13 + c : 18;
 constexpr int kCtrAnyMid = 19;  // counters[19] != 0: some tile has a class-2 piece
 constexpr int kCtrAnyC3 = 20;   // counters[20] != 0: some tile has a class-3 piece
 constexpr int kCtrEmptyDocs = 21;  // counters[21]: empty documents (k_docstart); 0: k_emit writes tok_off
+constexpr int kCtrSink = 31;       // counters[31]: panic bits of lookups whose pairs need not exist (discarded)
 // Long-piece order (long_hist, u32[kLhWords], zeroed per call): pieces in descending length
 // buckets of 64 B (bucket d = 64 - (n - 1) / 64, d = 0 for n > 4096), so every wave tier's pieces
 // are a contiguous range of long_ord, longest first.
@@ -170,6 +171,11 @@ struct Tables {            // device pointers, owned by the host runtime
   const uint8_t* at_flags;  // bit0 single_word, bit1 lstrip, bit2 rstrip
   uint32_t n_at;
   uint32_t proper;          // 1: merge table is rank-monotone (parallel same-rank rounds exact)
+  const uint32_t* eager;    // bit v: the merge of table value v is "eager" -- a merge consuming its
+                            // token ranks before it (only in tables that are not rank-monotone).
+                            // A round of a non-eager merge applies all its occurrences at once:
+                            // every pair the round makes ranks after it, so the sequential loop
+                            // also applies them all, left to right, before any other merge.
   uint32_t compact;         // 1: entry values are new ids (strictly increasing in rank), else ranks
   uint32_t narrow;          // 1: every vocab id < 2^16 (the merge passes keep the last tier's tokens as u16 in LDS)
   uint32_t dbg;             // debug mode (CTOK_DBG_MODE), 0 in production

@@ -169,6 +169,23 @@ __device__ __forceinline__ int cls_of(uint32_t cp, const Tables& t) {
 }
 
 
+// A long-piece round of merge value r applies every occurrence of r at once, except when the table
+// is not rank-monotone and r's merge is eager (Tables::eager): then the leftmost one alone, as the
+// sequential loop would before a lower-ranked merge the first one enables.  (Wave-uniform r: a
+// scalar load.)
+__device__ __forceinline__ bool serial_round(const Tables& t, uint32_t r) {
+  return !t.proper && ((t.eager[r >> 5] >> (r & 31)) & 1u) != 0;
+}
+// first_cascade (the rounds of an eager merge): the sequential loop takes the sites of rank r left
+// to right, and after each one the pairs it made -- (the left neighbour, or nid when the site two
+// tokens before was merged just before; nid) and (nid, the next token as it is) -- compete with the
+// remaining sites.  While none of them ranks below r it goes on with the next site; the first site
+// that makes a lower-ranked pair is the last one it applies before that pair's merge.  So a round
+// applies the sites up to and including the first such one (all of them when there is none), which
+// is the sequential result for any merge table; the lookups of this check never set the panic flag
+// (they go to a sink counter): a pair they see is formed, and looked up again, only if its site is
+// applied.  (x, x) runs of an eager merge take the leftmost site alone.
+
 // Merge-table value of an entry: the merge priority.  Compact tables (new ids strictly increasing
 // in rank, the usual layout) store the merged token id itself, so the minimum value is both the
 // winning pair and its new id; otherwise the rank is stored and the new id is looked up.
@@ -1568,7 +1585,7 @@ __device__ __forceinline__ void merge_one(const Tables& t, const LongState<G>& L
 
 template <bool G>
 __device__ uint32_t bpe_wave(const Tables& t, const uint8_t* bytes, uint32_t n, const LongState<G>& L, uint32_t* out,
-                             uint32_t* err) {
+                             uint32_t* err, uint32_t* sink) {
   const uint32_t lane = threadIdx.x & 63;
   // initial ids, dropping bytes whose char is not in the vocab (order-preserving compaction)
   uint32_t m = 0;
@@ -1599,7 +1616,21 @@ __device__ uint32_t bpe_wave(const Tables& t, const uint8_t* bytes, uint32_t n, 
     }
     const uint32_t lm = uni(wave_min_u32(lpos));
     const uint32_t chain = uni(L.Tok(lm) == L.Tok(L.Nxt(lm)) ? 1u : 0u);
-    if (!t.proper) {
+    // sites past `cut` wait for a later round (eager merges, see first_cascade)
+    uint32_t cut = kNone;
+    if (serial_round(t, r) && !chain) {
+      uint32_t c = kNone;
+      for (uint32_t i = lane; i < m; i += 64) {
+        if (L.Rk(i) != r) continue;
+        const uint32_t pp = L.Prv(i), j = L.Nxt(i), nj = L.Nxt(j);
+        const bool left_site = pp != kNone && L.Prv(pp) != kNone && L.Rk(L.Prv(pp)) == r;
+        const uint32_t rl = pp == kNone ? kNoRank : rank_of(t, left_site ? nid : L.Tok(pp), nid, sink);
+        const uint32_t rr = nj == kNone ? kNoRank : rank_of(t, nid, L.Tok(nj), sink);
+        if (rl < r || rr < r) c = min(c, i);
+      }
+      cut = uni(wave_min_u32(c));
+    }
+    if (serial_round(t, r) && chain) {
       merge_one(t, L, lm, nid, err);  // every lane performs the same update
     } else if (chain) {
       // (x,x) runs: the sequential left-to-right order, walked by the whole wave in lockstep
@@ -1607,9 +1638,9 @@ __device__ uint32_t bpe_wave(const Tables& t, const uint8_t* bytes, uint32_t n, 
         if (uni(L.Rk(i)) == r) merge_one(t, L, i, nid, err);
       }
     } else {
-      // phase A: splice out the right token of every occurrence
+      // phase A: splice out the right token of every occurrence (up to cut)
       for (uint32_t i = lane; i < m; i += 64) {
-        if (L.Rk(i) != r) continue;
+        if (L.Rk(i) != r || (cut != kNone && i > cut)) continue;
         const uint32_t j = L.Nxt(i);
         const uint32_t nj = L.Nxt(j);
         L.sTok(i, nid);
@@ -1652,7 +1683,7 @@ template <bool G>
 __device__ uint32_t long_piece(const Tables& t, const uint8_t* bytes, uint32_t n, const LongState<G>& L,
                                uint32_t* out, uint32_t* err) {
   const uint32_t lane = threadIdx.x & 63;
-  if (t.n_at == 0) return bpe_wave<G>(t, bytes, n, L, out, err);
+  if (t.n_at == 0) return bpe_wave<G>(t, bytes, n, L, out, err, err - 2 + kCtrSink);
   uint32_t cnt = 0, pos = 0;
   while (pos < n) {  // every lane computes the same added-token split; kept in SGPRs
     int32_t best = -1;
@@ -1675,7 +1706,7 @@ __device__ uint32_t long_piece(const Tables& t, const uint8_t* bytes, uint32_t n
       if (f > 0 && (uint32_t)f < nxt) nxt = (uint32_t)f;
     }
     nxt = uni(nxt);
-    cnt = uni(cnt + bpe_wave<G>(t, bytes + pos, nxt, L, out + cnt, err));
+    cnt = uni(cnt + bpe_wave<G>(t, bytes + pos, nxt, L, out + cnt, err, err - 2 + kCtrSink));
     pos += nxt;
   }
   return cnt;
@@ -1789,7 +1820,7 @@ __device__ __forceinline__ uint32_t rank_pair(const Tables& t, const PairLds& P,
 
 template <int K, bool HOT>
 __device__ uint32_t bpe_wave_dense(const Tables& t, const PairLds& P, const int32_t* s_b2id, const uint8_t* bytes,
-                                   uint32_t n, const WaveSlice<K>& S, uint32_t* out, uint32_t* err) {
+                                   uint32_t n, const WaveSlice<K>& S, uint32_t* out, uint32_t* err, uint32_t* sink) {
   const uint32_t lane = threadIdx.x & 63;
   lds_u32* tok = S.tok();
   lds_u32* rk = S.rk();
@@ -1844,9 +1875,26 @@ __device__ uint32_t bpe_wave_dense(const Tables& t, const PairLds& P, const int3
     const uint32_t lm = uni(wave_min_full_u32(lpos));
     const bool chain = uni(tok[lm] == tok[lm + 1] ? 1u : 0u) != 0;
     wave_sync_lds();
-    if (!t.proper) {
+    if (serial_round(t, r) && chain) {
       for (uint32_t p = lane; p < m; p += 64) sel[p] = p == lm ? 1 : 0;
       wave_sync_lds();
+    } else if (serial_round(t, r)) {
+      // eager merge (first_cascade): the sites up to the first whose sequential new pairs
+      // include a lower rank
+      uint32_t c = kNone;
+      for (uint32_t p = lane; p < m; p += 64) {
+        if (!sel[p]) continue;
+        const bool left_site = p >= 2 && sel[p - 2];
+        const uint32_t rl = p == 0 ? kNoRank : rank_pair<HOT>(t, P, left_site ? nid : (uint32_t)tok[p - 1], nid, sink);
+        const uint32_t rr = p + 2 >= m ? kNoRank : rank_pair<HOT>(t, P, nid, tok[p + 2], sink);
+        if (rl < r || rr < r) c = min(c, p);
+      }
+      const uint32_t cm = uni(wave_min_full_u32(c));
+      if (cm != kNone) {
+        for (uint32_t p = lane; p < m; p += 64)
+          if (p > cm) sel[p] = 0;
+        wave_sync_lds();
+      }
     } else if (chain) {
       // (x, x): in a run of consecutive sites the sequential loop merges the 1st, 3rd, ... one
       // (the choice goes through chg, rewritten by the compaction below)
@@ -1924,7 +1972,7 @@ constexpr uint32_t kNoPos = 0xFFFFu;
 
 template <int K, bool HOT>
 __device__ uint32_t bpe_wave_seg(const Tables& t, const PairLds& P, const int32_t* s_b2id, const uint8_t* bytes,
-                                 uint32_t n, const SegSlice<K>& S, uint32_t* out, uint32_t* err) {
+                                 uint32_t n, const SegSlice<K>& S, uint32_t* out, uint32_t* err, uint32_t* sink) {
   static_assert(K % 16 == 0 && K <= 64, "segment width: a multiple of 16, at most 64");
   constexpr uint32_t R = K / 4;  // registers per group
   const uint32_t lane = threadIdx.x & 63;
@@ -2022,9 +2070,39 @@ __device__ uint32_t bpe_wave_seg(const Tables& t, const PairLds& P, const int32_
     // (no second wave reduction on the round's critical path)
     bool chain = false;
     if (sites) chain = tok[first] == tok[nxt[first]];
-    if (!t.proper) {
+    const bool eager = serial_round(t, r);
+    if (eager && __ballot(chain) != 0) {
       const uint32_t lm = uni(wave_min_full_u32(first));
       sites = first == lm ? (sites & (~sites + 1)) : 0ull;  // the leftmost site only
+    } else if (eager) {
+      // eager merge (first_cascade): the sites up to the first whose sequential new pairs
+      // include a lower rank; the left pair of a site whose left neighbour's left neighbour is
+      // a site is (nid, nid), its right pair (nid, the next token as it is now)
+      uint32_t c = kNone;
+      for (uint64_t rest = sites; rest;) {
+        const uint32_t p = pos((uint32_t)__builtin_ctzll(rest));
+        rest &= rest - 1;
+        const uint32_t pp = prv[p], q = nxt[p];
+        const uint32_t nq = nxt[q];
+        const uint32_t ppp = pp != kNoPos ? (uint32_t)prv[pp] : kNoPos;
+        const bool left_site = ppp != kNoPos && rk[ppp] == r;
+        Probe<false, HOT> pl, pr;
+        pl.start(t, P, left_site ? nid : (pp != kNoPos ? (uint32_t)tok[pp] : 0u), nid, pp != kNoPos);
+        pr.start(t, P, nid, nq != kNoPos ? (uint32_t)tok[nq] : 0u, nq != kNoPos);
+        const uint32_t rl = pp != kNoPos ? pl.finish(t, sink) : kNoRank;
+        const uint32_t rr = nq != kNoPos ? pr.finish(t, sink) : kNoRank;
+        if (rl < r || rr < r) c = min(c, p);
+      }
+      const uint32_t cm = uni(wave_min_full_u32(c));
+      if (cm != kNone) {
+        uint64_t keep = 0;
+        for (uint64_t rest = sites; rest;) {
+          const uint32_t k = (uint32_t)__builtin_ctzll(rest);
+          rest &= rest - 1;
+          if (pos(k) <= cm) keep |= 1ull << k;
+        }
+        sites = keep;
+      }
     } else if (chain && sites) {
       // (x, x) runs: the 1st, 3rd, ... site of a run (d = sites before p in its run)
       uint64_t keep = 0, rest = sites;
@@ -2251,8 +2329,9 @@ __global__ __launch_bounds__(64 * NW) void k_bpe_wave(Work w, Tables t) {
     const uint32_t j = uni((uint32_t)(e >> 32) & 0xFFFFu);
     const uint32_t doc = (e & kLongDoc) ? kRecDoc : 0u;
     uint32_t cnt;
-    if constexpr (SEG) cnt = bpe_wave_seg<K, HOT>(t, P, s_b2id, w.text + s, n, SegSlice<K>{slice}, w.lscratch + s, err);
-    else cnt = bpe_wave_dense<K, HOT>(t, P, s_b2id, w.text + s, n, WaveSlice<K>{slice}, w.lscratch + s, err);
+    uint32_t* sink = &w.counters[kCtrSink];
+    if constexpr (SEG) cnt = bpe_wave_seg<K, HOT>(t, P, s_b2id, w.text + s, n, SegSlice<K>{slice}, w.lscratch + s, err, sink);
+    else cnt = bpe_wave_dense<K, HOT>(t, P, s_b2id, w.text + s, n, WaveSlice<K>{slice}, w.lscratch + s, err, sink);
     if (lane == 0) {
       const uint32_t tile = s / kTile;
       w.long_cnt[li] = cnt;

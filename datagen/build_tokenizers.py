@@ -10,9 +10,14 @@ synthetic corpora (datagen/corpus.py), then re-laid-out in the shape of the real
                pre_tokenizer Sequence[Split(Llama-3 regex, Isolated), ByteLevel(use_regex=false)]
                                                                                     (config C3)
   multi_32k    32,000 vocab trained on the CJK + emoji + ASCII mixture              (config C5)
+  llama3_tt_128k  llama3_128k with the merge list laid out as the tiktoken -> tokenizer.json
+               conversion does for the real Llama-3 (every split of every token: 304k merges,
+               several per token, not rank-monotone)                           (config C3, wide table)
 
 Every merge is valid (both parts and their concatenation are in the vocab) and unique, so the
-reference's rank/new_id quirk (src/bpe.rs:60-69) is inert on these files.
+reference's rank/new_id quirk (src/bpe.rs:60-69) is inert on these files; in
+llama3_tt_128k several merges make the same token, as in the real file (mod.rs:252-264 keeps them
+all, each with its own rank).
 Outputs: datagen/fixtures/<name>.json.gz.   Run: python datagen/build_tokenizers.py [names...]
 """
 import gzip
@@ -115,6 +120,33 @@ def build_llama3():
     }
 
 
+def tiktoken_style_merges(vocab):
+    """The merge list a tiktoken BPE file converts to (the layout of the real Llama-3
+    tokenizer.json, ~280k merges for 128k tokens): for every token, in id (= tiktoken rank) order,
+    every split into two vocab tokens, the splits ordered by their parts' ids; all merges sorted by
+    the id of the token they make.  Several merges make the same token, so new ids are not strictly
+    increasing in rank (the loader's rank-valued "wide" table), and a merge can consume a token that
+    a later-ranked merge also makes (the table is not rank-monotone)."""
+    merges = []
+    for tok, rank in sorted(vocab.items(), key=lambda kv: kv[1]):
+        if len(tok) == 1:
+            continue
+        local = [(tok[:i], tok[i:]) for i in range(1, len(tok)) if tok[:i] in vocab and tok[i:] in vocab]
+        local.sort(key=lambda m: (vocab[m[0]], vocab[m[1]]))
+        merges += local
+    return merges  # (already in rank order: tokens were visited by id)
+
+
+def build_llama3_tiktoken():
+    """llama3_128k's vocab, added tokens and pre-tokenizer with tiktoken-style merges (304k)."""
+    with gzip.open(os.path.join(OUT, "llama3_128k.json.gz"), "rb") as f:
+        obj = json.loads(f.read())
+    merges = tiktoken_style_merges(obj["model"]["vocab"])
+    assert len(set(merges)) == len(merges)
+    obj["model"]["merges"] = [[a, b] for a, b in merges]
+    return obj
+
+
 def build_multi():
     t5, o5 = corpus.corpus_c5(120_000, seed=105)
     merges = train_merges(texts_of(t5, o5), 32_000 - 256)
@@ -128,7 +160,8 @@ def build_multi():
     }
 
 
-BUILDERS = {"gpt2_50k": build_gpt2, "llama3_128k": build_llama3, "multi_32k": build_multi}
+BUILDERS = {"gpt2_50k": build_gpt2, "llama3_128k": build_llama3, "multi_32k": build_multi,
+            "llama3_tt_128k": build_llama3_tiktoken}
 
 
 def main(names):

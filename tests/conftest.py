@@ -41,3 +41,9 @@ def multi_path(fixture_dir):
     from datagen.build_tokenizers import fixture_path
     return fixture_path("multi_32k", fixture_dir)
 
+
+
+@pytest.fixture(scope="session")
+def llama3_tt_path(fixture_dir):
+    from datagen.build_tokenizers import fixture_path
+    return fixture_path("llama3_tt_128k", fixture_dir)

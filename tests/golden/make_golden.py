@@ -73,6 +73,7 @@ CONFIGS = {  # name -> (tokenizer fixture, corpus fn)
     "C3": ("llama3_128k", corpus.corpus_c3),
     "C5": ("multi_32k", corpus.corpus_c5),
     "C5NFC": ("multi_32k", corpus.corpus_c5nfc),
+    "C3TT": ("llama3_tt_128k", corpus.corpus_c3),  # C3 with the tiktoken-style 304k-merge list
 }
 
 

@@ -5,6 +5,7 @@ restatement of the reference) for small inputs, oracle/ctok_ref.c (faithful C po
 against ref_py in tests/test_oracle.py) for large ones, plus the committed golden vectors.
 """
 import json
+import os
 
 import numpy as np
 import pytest
@@ -109,15 +110,19 @@ def test_llama3_sample(llama3_path):
     assert_same(ids, toff, *rc.encode_packed(text, off))
 
 
-def test_long_piece_tiers_and_order(llama3_path):
+@pytest.mark.parametrize("fx", ["llama3_path", "llama3_tt_path"])
+def test_long_piece_tiers_and_order(request, fx):
     """Long pieces of every tier in one batch: lengths at the tier bounds (<= 256 B dense tier,
     257..1024 and 1025..4096 B segmented tiers, > 4096 B global-memory tier) and random ones, as
     random letters, concatenated words and single-letter repeats.  Exercises k_long_len /
     k_long_order (length buckets, longest-first order) and the per-tier dynamic take
-    (kernels.hip), against the C oracle."""
-    with open(llama3_path) as f:
+    (kernels.hip), against the C oracle.  llama3_tt_path: the same vocab with the tiktoken-style
+    merge list (several merges per token, not rank-monotone): the rounds of eager merges apply
+    their sites up to the first cascade (kernels.hip first_cascade)."""
+    path = request.getfixturevalue(fx)
+    with open(path) as f:
         obj = json.load(f)
-    tok = Tokenizer.from_file(llama3_path)
+    tok = Tokenizer.from_file(path)
     rc = ref_c.RefC(obj)
     rng = np.random.default_rng(77)
     words = [w.encode() for w in "the of and tokenizer merge piece order round wave tier bucket".split()]
@@ -142,6 +147,44 @@ def test_long_piece_tiers_and_order(llama3_path):
     ids, toff = tok.encode_packed(text, off, timing=True)
     assert tok.last_stats["long_pieces"] >= 3 * 150
     assert_same(ids, toff, *rc.encode_packed(text, off))
+
+
+def test_c3_tiktoken_layout_full_corpus(llama3_tt_path):
+    """C3 (100k docs, 76 MB, 1% with 1-4 KiB runs) with the Llama-3-shaped tokenizer whose merge
+    list is laid out as the tiktoken conversion of the real Llama-3 file does it: 304k merges,
+    several per token (the loader's rank-valued wide table), not rank-monotone (src/bpe.rs:52-79
+    keeps every one with its own rank).  The whole corpus against the C oracle's digest
+    (tests/golden/digests.json C3TT; it equals C3's: the two merge lists encode the same BPE)."""
+    import hashlib
+    gold = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "digests.json")))["C3TT"]
+    tok = Tokenizer.from_file(llama3_tt_path)
+    text, off = corpus.corpus_c3()
+    assert int(off[-1]) == gold["bytes"]
+    ids, toff = tok.encode_packed(text, off, timing=True)
+    h = hashlib.sha256()
+    h.update(np.ascontiguousarray(toff, dtype="<u8").tobytes())
+    h.update(np.ascontiguousarray(ids, dtype="<u4").tobytes())
+    assert len(ids) == gold["tokens"]
+    assert h.hexdigest() == gold["sha256"]
+    assert tok.last_stats["long_pieces"] >= 1000  # (the 1% of docs with a 1-4 KiB run)
+
+
+def test_eager_cascade_rounds():
+    """toys.eager_cascade: after an "a b" merges, ("ab", "a") ranks below ("a", "b"), so a round
+    of that merge must stop at its first site whose new pairs rank lower (kernels.hip
+    first_cascade) -- in pieces of every long-piece tier (dense <= 256 B, segmented 257..4096 B,
+    global-memory > 4096 B) and in the register passes, against the C oracle."""
+    obj = toys.eager_cascade()
+    tok, rc = gpu_tok(obj), ref_c.RefC(obj)
+    rng = np.random.default_rng(5)
+    docs = []
+    for n in [2, 3, 4, 7, 20, 40, 63, 64, 65, 127, 200, 255, 256, 257, 600, 1024, 1500, 2047, 2048, 2049, 4100, 6000]:
+        docs += [b"ab" * n, b"x " + b"ab" * n + b"c" * (n % 13) + b"ab" * 3, b"ba" + b"ab" * n,
+                 bytes(rng.choice(list(b"abc"), size=2 * n).astype(np.uint8))]
+    text, off = corpus.pack(docs)
+    ids, toff = tok.encode_packed(text, off)
+    assert_same(ids, toff, *rc.encode_packed(text, off))
+    assert tok.encode("abab") == [obj["model"]["vocab"]["aba"], obj["model"]["vocab"]["b"]]
 
 
 def test_multi_sample(multi_path):

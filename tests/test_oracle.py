@@ -428,3 +428,102 @@ def test_decode_oracles_agree(name, fixture_dir):
     for skip in (False, True):
         for clean in (False, True):
             assert rc.decode_batch(batch, skip, clean, threads=4) == py.decode_batch(batch, skip, clean)
+
+
+def _eager_values(rt):
+    """Tables::eager on the oracle's tables: rank r is eager when a merge consuming its token ranks
+    before r (ctok_host.cpp's eager_bits for a rank-valued table)."""
+    mincons = {}
+    for (a, b), r in rt.merge_ranks.items():
+        if r < len(rt.merge_new_ids):
+            for c in (a, b):
+                mincons[c] = min(mincons.get(c, r), r)
+    return {r for r in set(rt.merge_ranks.values()) if r < len(rt.merge_new_ids)
+            and mincons.get(rt.merge_new_ids[r], 1 << 60) < r}
+
+
+def _rounds_bpe(rt, eager, text):
+    """The long-piece kernels' round structure in Python (kernels.hip first_cascade): per round
+    the minimum rank r and its sites; a non-eager r merges every site at once ((x, x) runs: the
+    1st, 3rd, ...); an eager r merges the sites left to right up to and including the first whose
+    sequential new pairs -- (left neighbour, or nid after a merged site two tokens before; nid)
+    and (nid, the next token as it is) -- include a rank below r; an eager (x, x) run merges its
+    leftmost site only."""
+    toks = [rt.vocab[c] for c in text if c in rt.vocab]
+    while True:
+        rk = [rt.merge_ranks.get((toks[i], toks[i + 1])) for i in range(len(toks) - 1)]
+        live = [r for r in rk if r is not None]
+        if not live:
+            return toks
+        r = min(live)
+        nid = rt.merge_new_ids[r]
+        first = rk.index(r)
+        chain = toks[first] == toks[first + 1]
+        sites, i = [], 0
+        while i < len(rk):
+            if rk[i] == r:
+                sites.append(i)
+                i += 2
+            else:
+                i += 1
+        if r in eager and chain:
+            sites = sites[:1]
+        elif r in eager:
+            for k, p in enumerate(sites):
+                left = nid if (k and sites[k - 1] == p - 2) else (toks[p - 1] if p else None)
+                rl = rt.merge_ranks.get((left, nid)) if left is not None else None
+                rr = rt.merge_ranks.get((nid, toks[p + 2])) if p + 2 < len(toks) else None
+                if (rl is not None and rl < r) or (rr is not None and rr < r):
+                    sites = sites[:k + 1]
+                    break
+        S = set(sites)
+        out, i = [], 0
+        while i < len(toks):
+            if i in S:
+                out.append(nid)
+                i += 2
+            else:
+                out.append(toks[i])
+                i += 1
+        toks = out
+
+
+def test_parallel_rounds_with_eager_rule_equal_sequential_bpe(tmp_path):
+    """The tiktoken-style Llama-3 table (several merges per token, not rank-monotone): rounds that
+    apply every site of a non-eager merge at once give the reference's sequential ids
+    (src/bpe.rs:88-153) on long letter / digit / word runs; with every merge treated as non-eager
+    (the old global rule) some pieces differ, so the eager bits are what keeps them exact."""
+    from datagen.build_tokenizers import fixture_path
+    with open(fixture_path("llama3_tt_128k", str(tmp_path))) as f:
+        rt = ref_py.RefTokenizer(json.load(f))
+    eager = _eager_values(rt)
+    assert eager, "the tiktoken-style table should have eager merges"
+    rng = random.Random(9)
+    bm = ref_py.bytes_to_unicode()
+    words = ["the", "quick", "brown", "information", "tion", "ing", "abc", "aaaa", "1234567"]
+    wrong_without = 0
+    for k in range(400):
+        kind = k % 4
+        n = rng.randrange(20, 300)
+        if kind == 0:
+            s = "".join(rng.choice("abcdefghij") for _ in range(n))
+        elif kind == 1:
+            s = "".join(rng.choice("0123456789") for _ in range(n))
+        elif kind == 2:
+            s = "".join(rng.choice(words) for _ in range(n // 5))
+        else:
+            s = rng.choice("ab") * n + "".join(rng.choice("ab") for _ in range(n))
+        text = "".join(bm[b] for b in s.encode())
+        want = rt.bpe(text)
+        assert _rounds_bpe(rt, eager, text) == want, s[:60]
+        wrong_without += _rounds_bpe(rt, set(), text) != want
+    # (on this BPE-trained vocab the all-at-once rule happens to agree too; the toy table of
+    # toys.eager_cascade is one where it does not)
+    rt = ref_py.RefTokenizer(toys.eager_cascade())
+    eager = _eager_values(rt)
+    ab = rt.merge_ranks[(rt.vocab["a"], rt.vocab["b"])]
+    assert ab in eager
+    for s in ("abab", "ababab", "xabababab", "abcabab", "ab" * 40 + "c" * 9 + "ba" * 7):
+        want = rt.bpe(s)
+        assert _rounds_bpe(rt, eager, s) == want, s
+    assert _rounds_bpe(rt, set(), "abab") != rt.bpe("abab")

@@ -65,3 +65,17 @@ def with_invalid_merges(base_obj, seed, n_bad=50, tail_only=False):
             ms.insert(pos, "zz%dq qq%dz" % (k, k))
         o["model"]["merges"] = ms
     return derived(base_obj, m)
+
+
+def eager_cascade():
+    """A table where applying every site of a merge at once differs from the sequential loop:
+    ("ab", "a") ranks before ("a", "b"), so after the first "a b" of "abab" merges the new pair
+    ("ab", "a") is the minimum, and it takes the next site's "a" (sequential: [aba, b]; every
+    site at once: [ab, ab]).  Also "b a" and the byte merges of "c" runs, so pieces mix cascading
+    and ordinary rounds."""
+    chars = byte_chars()
+    vocab = {c: i for i, c in enumerate(chars)}
+    for t in ("ab", "aba", "ba", "cc", "cccc", "abab", "abc"):
+        vocab[t] = len(vocab)
+    merges = [("ab", "a"), ("a", "b"), ("b", "a"), ("c", "c"), ("cc", "cc"), ("ab", "ab"), ("ab", "c")]
+    return tok_json(vocab, merges)

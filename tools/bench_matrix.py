@@ -57,6 +57,8 @@ CONFIGS = {  # name: (tokenizer fixture, datagen.corpus generator, description)
     "c1": ("gpt2_50k", "corpus_c1", "C1: 1k ASCII docs 1-64 B"),
     "c2": ("gpt2_50k", "corpus_c2", "C2: 1M ASCII docs 96-160 B"),
     "c3": ("llama3_128k", "corpus_c3", "C3: 100k docs 16 B-4 KiB, Llama-3-shaped 128k vocab"),
+    "c3tt": ("llama3_tt_128k", "corpus_c3", "C3 with the tiktoken-style Llama-3 merge list (304k merges, several per "
+             "token: rank-valued wide table, not rank-monotone)"),
     "c5": ("multi_32k", "corpus_c5", "C5: 1M multilingual docs 64-512 B (CJK + emoji + ASCII), 32k vocab"),
     "c5nfc": ("multi_32k", "corpus_c5nfc", "C5-NFC: C5 with NFC-active text in 3% of the docs (GPU NFC path)"),
 }

@@ -19,7 +19,7 @@ from complexity_tokenizer import Tokenizer  # noqa: E402
 def main():
     d = tempfile.mkdtemp()
     out = {}
-    for name in ("gpt2_50k", "multi_32k", "llama3_128k"):
+    for name in ("gpt2_50k", "multi_32k", "llama3_128k", "llama3_tt_128k"):
         p = fixture_path(name, d)
         ts = []
         for _ in range(5):
