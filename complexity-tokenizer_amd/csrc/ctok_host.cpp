@@ -152,7 +152,7 @@ struct DevBuf {
     if (n <= cap && p) return;
     if (p) (void)hipFree(p);
     p = nullptr;
-    size_t want = std::max<size_t>(n + n / 4, 1024);
+    size_t want = std::max<size_t>(n + n / 16, 1024);  // (grow-only; a little slack for the next call)
     HIPTRY(hipMalloc((void**)&p, want * sizeof(T)));
     cap = want;
   }
@@ -213,11 +213,12 @@ struct DeviceState {
   DevBuf<uint64_t> comp_key;
   Tables t{};
   // workspace
-  DevBuf<uint32_t> docbits, pbits, tile_np, tile_tok, tile_doc, tcls, list0, list1, list2, list3, tcnt, scratch, lscratch, counters, lw;
+  DevBuf<uint32_t> docbits, pbits, tile_np, tile_tok, tile_doc, tcls, list0, list1, list2, list3, tcnt, scratch, counters;
+  DevBuf<uint32_t> lids, lw, long_pos, lw_pos, lwn, rend, cps;
   DevBuf<uint64_t> tregion;
   DevBuf<uint16_t> wpref;
   DevBuf<uint32_t> long_cnt, long_ord, long_hist;
-  DevBuf<uint64_t> long_list, mid_list, scan_tmp;
+  DevBuf<uint64_t> long_list, mid_list, scan_tmp, scan_tmp2;
   DevBuf<uint32_t> doc_flag, ncp;
   DevBuf<uint64_t> norm_off;
   DevBuf<uint8_t> norm_text;
@@ -243,8 +244,9 @@ struct DeviceState {
     uint64_t b = 0;
     auto add = [&](const auto& x) { b += (uint64_t)x.cap * sizeof(*x.p); };
     add(docbits), add(pbits), add(tile_np), add(tile_tok), add(tile_doc), add(tcls), add(list0), add(list1);
-    add(list2), add(list3), add(tcnt), add(scratch), add(lscratch), add(counters), add(lw), add(tregion);
-    add(wpref), add(long_cnt), add(long_ord), add(long_hist), add(long_list), add(mid_list), add(scan_tmp);
+    add(list2), add(list3), add(tcnt), add(scratch), add(counters), add(lids), add(lw), add(tregion), add(rend);
+    add(wpref), add(long_cnt), add(long_ord), add(long_hist), add(long_pos), add(lw_pos), add(lwn), add(long_list);
+    add(mid_list), add(scan_tmp), add(scan_tmp2), add(cps);
     add(doc_flag), add(ncp), add(norm_off), add(norm_text);
     return b;
   }
@@ -1213,6 +1215,9 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   // combining class; ASCII never is).  Only a flagged batch pays for the check + normalise
   // passes and a second run.
   bool speculate = t->nfc && !t->add_prefix_space && n_bytes && !getenv("CTOK_NO_NFC_SPECULATION");
+  // lean list capacities first; a call whose lists outgrow them runs again with the safe ones
+  static const bool always_safe = getenv("CTOK_SAFE_CAPACITIES") != nullptr;
+  bool safe = always_safe;
   for (;;) {
   if (timing) HIPTRY(hipEventRecord(ds->ev[0], s));
 
@@ -1238,9 +1243,9 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
     if (!t->nfc) HIPTRY(hipMemsetAsync(ds->doc_flag.p, 0, (n_docs + 1) * 4, s));
     ds->ncp.ensure(n_docs + 1);
     ds->norm_off.ensure(n_docs + 2);
-    ds->lw.ensure(4 * n_bytes + 64);
+    ds->cps.ensure(4 * n_bytes + 64);
     STEP("norm0", launch_norm(d_text, d_off, (uint32_t)n_docs, ds->doc_flag.p, t->add_prefix_space, t->nfc && nfc_docs, tb,
-                       ds->lw.p, ds->ncp.p, ds->norm_off.p, nullptr, 0, s));
+                       ds->cps.p, ds->ncp.p, ds->norm_off.p, nullptr, 0, s));
     ds->scan_tmp.ensure(scan_tmp_elems(n_docs + 1) + 64);
     HIPTRY(scan_u64(ds->norm_off.p, n_docs, ds->scan_tmp.p, ds->scan_tmp.cap, s));
     HIPTRY(hipMemcpyAsync(ds->host, ds->norm_off.p + n_docs, 8, hipMemcpyDeviceToHost, s));
@@ -1249,7 +1254,7 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
     if (nb >= 0xF0000000ull) throw_err(CTOK_E_ARG, "normalised batch exceeds 3.75 GiB; split the batch");
     ds->norm_text.ensure(nb + 16);
     STEP("norm1", launch_norm(d_text, d_off, (uint32_t)n_docs, ds->doc_flag.p, t->add_prefix_space, t->nfc && nfc_docs, tb,
-                       ds->lw.p, ds->ncp.p, ds->norm_off.p, ds->norm_text.p, 1, s));
+                       ds->cps.p, ds->ncp.p, ds->norm_off.p, ds->norm_text.p, 1, s));
     text = ds->norm_text.p;
     off = ds->norm_off.p;
     B = nb;
@@ -1275,8 +1280,18 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   ds->tile_np.ensure(nt + 8);
   ds->tile_tok.ensure(nt + 8);
   ds->tile_doc.ensure(nt + 8);
+  // Workspace sized from what the call needs (ctok_stats.workspace_bytes): the class-0 lists lean
+  // (kCap0Lean per tile, the rest of a tile's class-0 pieces spill to the long list), the
+  // dropped-byte list small (it only fills when the vocab lacks some byte chars), the long pieces'
+  // ids and global-memory state sized from launch_long_prep's totals (none without long pieces).
+  // A list that outgrows its lean capacity sets counters[kCtrOverflow]: the call runs again with
+  // the safe capacities (every class-0 piece listed, a dropped-byte entry per byte).
+  w.k0 = safe ? kCap0 : kCap0Lean;
+  w.long_cap = (uint32_t)(B / kShortMax + nt + 8);
+  w.mid_cap = (uint32_t)(safe ? B + 8 : std::min<uint64_t>(B + 8, std::max<uint64_t>(65536, B / 256)));
   ds->tcls.ensure(kNumClasses * nt + 8);
-  ds->list0.ensure(nt * kCap0 + 8);
+  ds->list0.ensure(nt * w.k0 + 8);
+  ds->rend.ensure(kNumClasses * nt + 8);
   if (tb.n_at == 0) {
     ds->list1.ensure(nt * kCap1 + 8);
     ds->list2.ensure(nt * kCap2 + 8);
@@ -1284,14 +1299,12 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   }
   ds->tcnt.ensure(nt * kTileSlots + 8);
   ds->scratch.ensure(nt * kTileSlots + 8);  // per tile: the class regions of the register passes
-  ds->lscratch.ensure(B + 64);             // long / generic-pass pieces, by text offset
   ds->tregion.ensure(nt + 8);
-  ds->long_list.ensure(B / kShortMax + nt + 8);
-  ds->long_cnt.ensure(B / kShortMax + nt + 8);
-  ds->long_ord.ensure(B / kShortMax + nt + 8);
+  ds->long_list.ensure(w.long_cap + 8);
+  ds->long_cnt.ensure(w.long_cap + 8);
+  ds->long_ord.ensure(w.long_cap + 8);
   ds->long_hist.ensure(kLhWords);
-  ds->mid_list.ensure(B / 2 + 8);
-  ds->lw.ensure(4 * B + 64);
+  ds->mid_list.ensure(w.mid_cap + 8);
   ds->scan_tmp.ensure(scan_tmp_elems(std::max<uint64_t>(nt + 1, n_docs + 1)) + 64);
   w.docbits = ds->docbits.p;
   w.pbits = ds->pbits.p;
@@ -1309,12 +1322,11 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   w.long_hist = ds->long_hist.p;
   w.tcnt = ds->tcnt.p;
   w.scratch = ds->scratch.p;
-  w.lscratch = ds->lscratch.p;
+  w.rend = ds->rend.p;
   w.tregion = (uint2*)ds->tregion.p;
   w.long_list = ds->long_list.p;
   w.mid_list = ds->mid_list.p;
   w.counters = ds->counters.p;
-  w.lw = ds->lw.p;
   w.scan_tmp = (uint32_t*)ds->scan_tmp.p;
   w.scan_tmp_cap = ds->scan_tmp.cap * 2;
 
@@ -1355,8 +1367,29 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
     if (e == hipSuccess) break;
     if (e != hipErrorNotReady) throw_err(CTOK_E_DEVICE, std::string("hipEventQuery: ") + hipGetErrorString(e));
   }
-  if (!(speculate && seg_cnt[12]))  // (a failed NFC speculation discards this pass: nothing to launch)
-    STEP("bpe_long", launch_bpe_long(w, tb, ds->side, seg_cnt[0], seg_cnt[kCtrAnyC3] != 0));
+  if (!(speculate && seg_cnt[12])) {  // (a failed NFC speculation discards this pass: nothing to launch)
+    const uint32_t n_long = std::min<uint32_t>((uint32_t)seg_cnt[0], w.long_cap);
+    if (n_long) {
+      // lengths, order and places of the long pieces, then lids / lw sized from their totals
+      ds->long_pos.ensure(n_long + 8);
+      ds->lw_pos.ensure(n_long + 8);
+      ds->lwn.ensure(n_long + 8);
+      ds->scan_tmp2.ensure(scan_tmp_elems(n_long + 1) + 64);
+      w.long_pos = ds->long_pos.p;
+      w.lw_pos = ds->lw_pos.p;
+      STEP("long_prep", launch_long_prep(w, tb, ds->side, n_long, ds->lwn.p, (uint32_t*)ds->scan_tmp2.p,
+                                         ds->scan_tmp2.cap * 2));
+      volatile uint32_t* tot = (volatile uint32_t*)(ds->host + 96);
+      HIPTRY(hipMemcpyAsync((void*)tot, ds->long_pos.p + n_long, 4, hipMemcpyDeviceToHost, ds->side));
+      HIPTRY(hipMemcpyAsync((void*)(tot + 1), ds->lw_pos.p + n_long, 4, hipMemcpyDeviceToHost, ds->side));
+      spin_sync(ds, ds->side);
+      ds->lids.ensure((uint64_t)tot[0] + 64);
+      ds->lw.ensure(4 * (uint64_t)tot[1] + 64);
+      w.lids = ds->lids.p;
+      w.lw = ds->lw.p;
+    }
+    STEP("bpe_long", launch_bpe_long(w, tb, ds->side, n_long, seg_cnt[kCtrAnyC3] != 0));
+  }
   HIPTRY(hipEventRecord(ds->ev_join, ds->side));
   HIPTRY(hipStreamWaitEvent(s, ds->ev_join, 0));
   if (timing) HIPTRY(hipEventRecord(ds->ev[5], s));
@@ -1373,6 +1406,10 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   for (int i = 0; i < kNumCounters; i++) cnt[i] = ((volatile uint32_t*)(ds->host + 1))[i];
   if (speculate && cnt[12]) {  // a code point NFC may change: check, normalise, run again
     speculate = false;
+    continue;
+  }
+  if ((cnt[kCtrOverflow] || cnt[0] > w.long_cap) && !safe) {  // a lean list overflowed: run again safe
+    safe = true;
     continue;
   }
   const uint32_t P = cnt[5];

@@ -29,8 +29,12 @@ constexpr int kSegUnroll = 4;           // pieces per lane per routing round in 
 constexpr int kShortMax = 32;      // pieces up to this many bytes: classes 0..2 (and the generic pass)
 constexpr int kMedMax = 64;        // class 3: 33..64 B, still thread-per-piece (64 register slots)
 // Per-tile piece lists by length class: <= 8 B (whole-piece probe missed), 9..16 B, 17..32 B,
-// 33..64 B.  Capacities are the most pieces of that class that can start in one tile.
+// 33..64 B.  Capacities of classes 1..3 are the most pieces of that class that can start in one
+// tile; class 0 holds Work::k0 entries per tile (kCap0Lean normally: a tile's further class-0
+// pieces go to the long list, whose dense wave tier merges pieces of any length; kCap0 in the
+// safe rerun after a list overflowed).
 constexpr uint32_t kCap0 = kTile, kCap1 = (kTile + 8) / 9, kCap2 = (kTile + 16) / 17, kCap3 = (kTile + 32) / 33;
+constexpr uint32_t kCap0Lean = 1040;  // (65 lines per tile: a power-of-two stride put every tile's list on one memory channel)
 constexpr int kNumClasses = 4;
 constexpr int kNumCounters = 32;
 // counters[] slots of class pass c: bytes merged / ids produced (statistics), next chunk
@@ -40,6 +44,9 @@ constexpr int kCtrAnyMid = 19;  // counters[19] != 0: some tile has a class-2 pi
 constexpr int kCtrAnyC3 = 20;   // counters[20] != 0: some tile has a class-3 piece
 constexpr int kCtrEmptyDocs = 21;  // counters[21]: empty documents (k_docstart); 0: k_emit writes tok_off
 constexpr int kCtrSink = 31;       // counters[31]: panic bits of lookups whose pairs need not exist (discarded)
+constexpr int kCtrOverflow = 25;   // counters[25] != 0: a list outgrew its lean capacity (the host reruns the call safe)
+constexpr int kCtrLongIds = 26;    // counters[26]: long-piece id slots reserved (k_long_len: a piece's bytes)
+constexpr int kCtrLwWords = 27;    // counters[27]: global-memory long-piece state reserved (4 u32 per byte)
 // Long-piece order (long_hist, u32[kLhWords], zeroed per call): pieces in descending length
 // buckets of 64 B (bucket d = 64 - (n - 1) / 64, d = 0 for n > 4096), so every wave tier's pieces
 // are a contiguous range of long_ord, longest first.
@@ -58,13 +65,13 @@ constexpr uint64_t kLongDoc = 1ull << 63, kMidDoc = 1ull << 44;
 
 // Piece record (tcnt[tile][j], u32), written by whichever pass finishes piece j:
 //   kRecHit | id            one id, the whole-piece probe's (no scratch entry)
-//   kRecLong | li           long piece li: count long_cnt[li], ids at scratch[(u32)long_list[li] ..]
-//   count | pos << 16       merged piece (<= 64 B, register passes): ids at scratch[tile * kTileSlots + pos ..]
-//                           (pos: a slot of the tile's region for the piece's length class, see tregion)
-//   kRecAlt | count | start << 16   piece of the generic pass: ids at lscratch[tile * kTile + start ..]
+//   kRecLong | li           long piece li: count long_cnt[li], ids at lids[long_pos[li] ..]
+//   count | pos << 16       merged piece (<= 64 B: register passes, generic pass): ids at
+//                           scratch[tile * kTileSlots + pos ..] (pos: a slot of the tile's region
+//                           for the piece's length class, see tregion)
 // | kRecDoc when the piece starts a document: k_emit then leaves the piece's first id within the
 // tile in its slot (for k_tokoff).
-constexpr uint32_t kRecHit = 0x80000000u, kRecLong = 0x40000000u, kRecDoc = 0x20000000u, kRecAlt = 0x10000000u;
+constexpr uint32_t kRecHit = 0x80000000u, kRecLong = 0x40000000u, kRecDoc = 0x20000000u;
 constexpr uint32_t kRecIdMask = (1u << kIdBits) - 1u, kRecLongMask = kRecDoc - 1u;
 // Per-tile id regions of the register merge passes in scratch (kTileSlots u32 per tile): class c
 // (c = 0..3) starts at the total bytes of the tile's class lists < c (ids <= bytes), packed as
@@ -200,7 +207,8 @@ struct Work {              // device pointers, sized by the host for one call
   uint32_t* tile_tok;      // [n_tiles + 1] tokens per tile, scanned in place to the tile's first id
   uint32_t* tile_doc;      // [n_tiles + 1] documents starting in the tile, scanned to the tile's first doc
   uint32_t* tcls;          // [kNumClasses][n_tiles] entries of each class list
-  uint32_t* list0;         // [n_tiles * kCap0] (also every <= 32 B piece when added tokens can match)
+  uint32_t* list0;         // [n_tiles * k0] (also every <= 32 B piece when added tokens can match)
+  uint32_t k0;             // class-0 entries per tile (kCap0Lean, or kCap0 in the safe rerun)
   uint32_t* list1;         // [n_tiles * kCap1]
   uint32_t* list2;         // [n_tiles * kCap2]
   uint32_t* list3;         // [n_tiles * kCap3]
@@ -210,8 +218,13 @@ struct Work {              // device pointers, sized by the host for one call
   uint32_t* long_ord;      // long-list indices in descending length buckets (k_long_order)
   uint32_t* long_hist;     // [kLhWords] bucket counts | their exclusive scan | fill cursors | per-tier take counters
   uint32_t* scratch;       // [n_tiles * kTileSlots] ids of the register passes' pieces, per tile and class region
-  uint32_t* lscratch;      // [n_bytes + 64] ids of a long / generic-pass piece starting at byte s at lscratch[s ..]
+  uint32_t* lids;          // ids of the long pieces: piece li's at lids[long_pos[li] ..] (sized after k_long_len)
+  uint32_t* long_pos;      // [long capacity] id slot of long piece li (k_long_len: reserved from counters[kCtrLongIds])
+  uint32_t* lw_pos;        // [long capacity] global-memory tier state of long piece li at lw + 4 * lw_pos[li]
+  uint32_t* rend;          // [kNumClasses][n_tiles] end of the consumed part of each class region (merge passes;
+                           // the dropped-byte pass allocates after it)
   uint2* tregion;          // [n_tiles] class region bases of the tile in scratch (region_base)
+  uint32_t long_cap, mid_cap;  // long_list / mid_list entries (appends past them set counters[kCtrOverflow])
   uint64_t* long_list;     // pieces > kMedMax B (> kShortMax B in generic mode), or of unknown length
                            // at a tile end: s | j << 32
   uint64_t* mid_list;      // pieces with dropped bytes for the generic kernel: s | j << 32 | n << 48
@@ -219,7 +232,7 @@ struct Work {              // device pointers, sized by the host for one call
                            // [5] pieces (stats), [ctr_stat(c)], [ctr_stat(c) + 1]: bytes merged /
                            // ids produced by class pass c (stats), [12] NFC speculation failed,
                            // [ctr_chunk(c)] next chunk of class pass c, [kCtrAnyMid], [kCtrAnyC3]
-  uint32_t* lw;            // long-piece workspace: 4 * n_bytes u32
+  uint32_t* lw;            // global-memory long-piece state (4 u32 per byte of the pieces > 4 KiB), sized after k_long_len
   uint32_t* scan_tmp;      // scan partials
   uint64_t scan_tmp_cap;
 };
@@ -308,6 +321,10 @@ hipError_t launch_segment(const Work& w, const Tables& t, hipStream_t s);
 hipError_t launch_count_pieces(const Work& w, hipStream_t s);
 // cls 0: classes 0 and 1; 2: classes 2 and 3; 3: dropped-byte pieces (mid_list)
 hipError_t launch_bpe_class(const Work& w, const Tables& t, int cls, hipStream_t s);
+// long-piece preparation (side stream): lengths, order, id places (long_pos) and global-memory
+// state places (lw_pos); long_pos[n_long] / lw_pos[n_long] = the totals the host sizes lids / lw by
+hipError_t launch_long_prep(const Work& w, const Tables& t, hipStream_t s, uint32_t n_long, uint32_t* lwn,
+                            uint32_t* tmp, uint64_t tmp_cap);
 // long-piece tiers (side stream): n_long = k_segment's long-list length, any_c3 = a class-3
 // piece exists (the side instance of the 33..64 B pass); grids sized for them, nothing when empty
 hipError_t launch_bpe_long(const Work& w, const Tables& t, hipStream_t s, uint32_t n_long, bool any_c3);

@@ -133,6 +133,10 @@ __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_re
 // k_segment return at once instead of merging text that will be re-encoded.
 __device__ __forceinline__ bool spec_failed(const Work& w) { return w.nfc_watch && uni(w.counters[12]) != 0; }
 
+// pieces in the long list (k_segment counts them all; past long_cap they were not stored and the
+// host reruns the call with the safe capacities)
+__device__ __forceinline__ uint32_t long_count(const Work& w) { return min(w.counters[0], w.long_cap); }
+
 // wave-aggregated append to an LDS counter: returns this lane's slot (lanes with take == false
 // get garbage).  One ds_add per wave instead of one per lane.
 __device__ __forceinline__ uint32_t wave_append(uint32_t* counter, bool take) {
@@ -617,15 +621,31 @@ __global__ __launch_bounds__(64 * kSegWaves) void k_segment(Work w, Tables t) {
       }
       if (j < np) tcnt[j] = rec;  // every piece's slot: whole coalesced lines
     }
+    {  // the tile's class-0 list is full: the rest of its class-0 pieces go to the long list (one
+       // uniform test per round; the per-piece fix-up only in the rare round that crosses w.k0)
+      uint32_t tot0 = n0;
+#pragma unroll
+      for (int u = 0; u < U; u++) tot0 += (uint32_t)__popcll(__ballot(cls[u] == 0));
+      if (tot0 > w.k0) {
+        uint32_t c = n0;
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          const uint64_t m = __ballot(cls[u] == 0);
+          if (cls[u] == 0 && c + __popcll(m & lanemask_lt()) >= w.k0) cls[u] = 3;
+          c += (uint32_t)__popcll(m);
+        }
+      }
+    }
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const uint32_t j = j0 + 64 * u + lane;
       const uint32_t e = list_entry(sl[u], j, n[u]) | (doc[u] ? kEntDoc : 0u);
       {  // the wave owns its tile's lists: running counts in scalar registers, no atomics
-        const uint64_t m0 = __ballot(cls[u] == 0), m1 = __ballot(cls[u] == 1), m2 = __ballot(cls[u] == 2);
+        const uint64_t m0 = __ballot(cls[u] == 0);
+        const uint64_t m1 = __ballot(cls[u] == 1), m2 = __ballot(cls[u] == 2);
         const uint64_t m3 = __ballot(cls[u] == 6);
         const uint64_t below = lanemask_lt();
-        if (cls[u] == 0) w.list0[(size_t)tile * kCap0 + n0 + __popcll(m0 & below)] = e;
+        if (cls[u] == 0) w.list0[(size_t)tile * w.k0 + n0 + __popcll(m0 & below)] = e;
         if (cls[u] == 1) w.list1[(size_t)tile * kCap1 + n1 + __popcll(m1 & below)] = e;
         if (cls[u] == 2) w.list2[(size_t)tile * kCap2 + n2 + __popcll(m2 & below)] = e;
         if (cls[u] == 6) w.list3[(size_t)tile * kCap3 + n3 + __popcll(m3 & below)] = e;
@@ -643,9 +663,10 @@ __global__ __launch_bounds__(64 * kSegWaves) void k_segment(Work w, Tables t) {
         uint32_t b = 0;
         if (lane == leader) b = atomicAdd(&w.counters[0], (uint32_t)__popcll(lm));
         b = __builtin_amdgcn_readlane(b, leader);
-        if (cls[u] == 3)
-          w.long_list[b + __popcll(lm & lanemask_lt())] =
-              (uint64_t)(t0 + sl[u]) | ((uint64_t)j << 32) | (doc[u] ? kLongDoc : 0ull);
+        const uint32_t li = b + __popcll(lm & lanemask_lt());
+        if (cls[u] == 3 && li < w.long_cap)
+          w.long_list[li] = (uint64_t)(t0 + sl[u]) | ((uint64_t)j << 32) | (doc[u] ? kLongDoc : 0ull);
+        if (lane == leader && b + __popcll(lm) > w.long_cap) atomicOr(&w.counters[kCtrOverflow], 1u);
       }
     }
     // every lane has read this round's s_pos before the next round's expansion overwrites it
@@ -666,6 +687,8 @@ __global__ __launch_bounds__(64 * kSegWaves) void k_segment(Work w, Tables t) {
     // the lists hold pieces that start in the tile and end within its 62-byte look-ahead)
     w.tregion[tile] = make_uint2(by0 | ((by0 + by1) << 16), by0 + by1 + by2);
   }
+  if (lane < kNumClasses)  // (the merge passes move them to the end of what they consumed)
+    w.rend[(size_t)lane * w.n_tiles + tile] = lane == 0 ? 0u : lane == 1 ? by0 : lane == 2 ? by0 + by1 : by0 + by1 + by2;
   if (lane < kNumClasses)
     w.tcls[(size_t)lane * w.n_tiles + tile] = lane == 0 ? n0 : lane == 1 ? n1 : lane == 2 ? n2 : n3;
   if (lane == 0 && n2) w.counters[kCtrAnyMid] = 1;  // plain stores: every writer stores 1
@@ -807,11 +830,12 @@ __device__ __forceinline__ uint32_t tile_of(const uint32_t* s_pre, uint32_t q) {
 
 template <int K>
 __device__ __forceinline__ void tile_share_flush(const Work& w, uint32_t t0, uint32_t t1, const uint32_t* s_tsum,
-                                                 const uint32_t* s_tbase = nullptr) {
+                                                 const uint32_t* s_tbase = nullptr, int cls = -1) {
   __syncthreads();
   if (threadIdx.x < K && t0 + threadIdx.x < t1) {
     const uint32_t v = s_tsum[threadIdx.x] - (s_tbase ? s_tbase[threadIdx.x] : 0u);
     if (v) atomicAdd(&w.tile_tok[t0 + threadIdx.x], v);
+    if (cls >= 0 && v) w.rend[(size_t)cls * w.n_tiles + t0 + threadIdx.x] = s_tsum[threadIdx.x];
   }
 }
 
@@ -837,7 +861,7 @@ __global__ __launch_bounds__(MID ? 128 : 256) void k_bpe_generic(Work w, Tables 
   uint32_t E, t0 = 0;
   if (MID) {
     __syncthreads();
-    E = w.counters[4];
+    E = min(w.counters[4], w.mid_cap);
   } else {
     t0 = blockIdx.x * kTilesGeneric;
     E = tile_share_init<kTilesGeneric>(w.tcls, w.n_tiles, t0, s_pre, s_tsum);
@@ -855,14 +879,18 @@ __global__ __launch_bounds__(MID ? 128 : 256) void k_bpe_generic(Work w, Tables 
     } else {
       kt = tile_of<kTilesGeneric>(s_pre, q);
       tile = t0 + kt;
-      const uint32_t e = w.list0[(size_t)tile * kCap0 + (q - s_pre[kt])];
+      const uint32_t e = w.list0[(size_t)tile * w.k0 + (q - s_pre[kt])];
       s = tile * kTile + (e & 0xFFFu);
       j = ent_j(e);
       n = ent_len(e);
       doc = (e & kEntDoc) ? kRecDoc : 0u;
     }
     const uint8_t* bytes = w.text + s;
-    uint32_t* out = w.lscratch + s;
+    // ids go to the tile's region of the piece's length class, after what the merge passes used
+    // there (the region holds the bytes of every piece of the class: ids <= bytes)
+    const uint32_t cl = n <= 8 ? 0u : n <= 16 ? 1u : n <= 32 ? 2u : 3u;
+    const uint32_t pos = atomicAdd(&w.rend[(size_t)(MID ? cl : 0u) * w.n_tiles + tile], n);
+    uint32_t* out = w.scratch + (size_t)tile * kTileSlots + pos;
     uint32_t cnt = 0;
     if (t.n_at == 0) {
       cnt = bpe_short<NT>(t, bytes, n, s_b2id, s_tok, s_rk, tid, out, err);
@@ -886,7 +914,7 @@ __global__ __launch_bounds__(MID ? 128 : 256) void k_bpe_generic(Work w, Tables 
         pos += nxt;
       }
     }
-    w.tcnt[(size_t)tile * kTileSlots + j] = rec_short(cnt, s - tile * kTile) | doc | kRecAlt;
+    w.tcnt[(size_t)tile * kTileSlots + j] = rec_short(cnt, pos) | doc;
     if (MID) atomicAdd(&w.tile_tok[tile], cnt);
     else atomicAdd(&s_tsum[kt], cnt);
   }
@@ -1039,6 +1067,10 @@ template <int N>
 __device__ __forceinline__ const uint32_t* class_list(const Work& w) {
   return N == 8 ? w.list0 : N == 16 ? w.list1 : N == 32 ? w.list2 : w.list3;
 }
+template <int N>
+__device__ __forceinline__ uint32_t class_cap(const Work& w) {
+  return N == 8 ? w.k0 : LdsClass<N>::cap;
+}
 
 // The merge loop on the first N register slots of tk / rk (compile-time indices only, so the
 // arrays stay in registers): branch-free over the slots, the lowest (rank, position) pair is
@@ -1169,6 +1201,7 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
   const uint32_t tid = threadIdx.x;
   uint32_t* err = &w.counters[2];
   const uint32_t* list = class_list<N>(w);
+  const uint32_t cap = class_cap<N>(w);
   const uint32_t* counts = w.tcls + (size_t)LC::cls * w.n_tiles;
   uint32_t st_bytes = 0, st_ids = 0;
   if (tid < 2) S.stat[tid] = 0;
@@ -1202,7 +1235,7 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
       __syncthreads();
       for (uint32_t q = tid; q < E; q += NT) {  // bucket sizes (one LDS add per wave and bucket)
         const uint32_t kt = tile_of<K>(S.pre, q);
-        const uint32_t b = bucket(ent_len(list[(size_t)(c0 + kt) * LC::cap + (q - S.pre[kt])]));
+        const uint32_t b = bucket(ent_len(list[(size_t)(c0 + kt) * cap + (q - S.pre[kt])]));
 #pragma unroll
         for (uint32_t bb = 0; bb < 4; bb++) {
           const uint64_t m = __ballot(b == bb);
@@ -1221,7 +1254,7 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
       __syncthreads();
       for (uint32_t q = tid; q < E; q += NT) {  // scatter entry numbers into bucket order
         const uint32_t kt = tile_of<K>(S.pre, q);
-        const uint32_t b = bucket(ent_len(list[(size_t)(c0 + kt) * LC::cap + (q - S.pre[kt])]));
+        const uint32_t b = bucket(ent_len(list[(size_t)(c0 + kt) * cap + (q - S.pre[kt])]));
 #pragma unroll
         for (uint32_t bb = 0; bb < 4; bb++) {
           const uint32_t slot = wave_append(&S.bfill[bb], b == bb);
@@ -1233,7 +1266,7 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
     auto entry = [&](uint32_t i, uint32_t& kt) {
       const uint32_t q = sorted ? (uint32_t)S.perm[i] : i;
       kt = tile_of<K>(S.pre, q);
-      return list[(size_t)(c0 + kt) * LC::cap + (q - S.pre[kt])];
+      return list[(size_t)(c0 + kt) * cap + (q - S.pre[kt])];
     };
     auto start_of = [&](uint32_t e, uint32_t kt) { return (c0 + kt) * kTile + (e & 0xFFFu); };
     // one piece: list entry e of chunk tile kt, its first N bytes in wv
@@ -1253,8 +1286,11 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
           }
         }
         if (missing) {  // a byte char absent from the vocab is dropped: generic path
-          w.mid_list[atomicAdd(&w.counters[4], 1u)] =
-              (uint64_t)s | ((uint64_t)j << 32) | ((uint64_t)n << 48) | ((e & kEntDoc) ? kMidDoc : 0ull);
+          const uint32_t mi = atomicAdd(&w.counters[4], 1u);
+          if (mi < w.mid_cap)
+            w.mid_list[mi] = (uint64_t)s | ((uint64_t)j << 32) | ((uint64_t)n << 48) | ((e & kEntDoc) ? kMidDoc : 0ull);
+          else
+            atomicOr(&w.counters[kCtrOverflow], 1u);
           return;
         }
         // initial pair ranks: every initial pair is a byte pair, one load each from the 256 x 256
@@ -1351,7 +1387,7 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
         if (i < E) body(e, kt, wv);
       }
     }
-    tile_share_flush<K>(w, c0, tb1, S.tsum, S.tbase);
+    tile_share_flush<K>(w, c0, tb1, S.tsum, S.tbase, LC::cls);
     // size the next chunk for about two entries per thread (up to K tiles): sparse classes take
     // several units at once, dense ones one; never more than a fair share of the units left, so
     // the last chunks stay small (C2: 504 units for 256 workgroups)
@@ -1739,10 +1775,9 @@ __global__ __launch_bounds__(256) void k_bpe_long(Work w, Tables t) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_long[];
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wid = uni(threadIdx.x >> 6);
-  const uint32_t n_long = uni(w.counters[0]);
+  const uint32_t n_long = uni(long_count(w));
   const uint32_t n_waves = gridDim.x * (blockDim.x >> 6);
   uint32_t* err = &w.counters[2];
-  const uint32_t B = w.n_bytes;
   for (uint32_t li = uni(blockIdx.x * (blockDim.x >> 6) + wid); li < n_long; li += n_waves) {
     const uint64_t e = w.long_list[li];
     const uint32_t s = uni((uint32_t)e);
@@ -1754,10 +1789,11 @@ __global__ __launch_bounds__(256) void k_bpe_long(Work w, Tables t) {
     const uint32_t gmin = (t.n_at != 0 || t.dbg == 7) ? kLdsPos : kWaveMax;
     if (GMEM != (n > gmin)) continue;
     const uint8_t* bytes = w.text + s;
-    uint32_t* out = w.lscratch + s;
+    uint32_t* out = w.lids + w.long_pos[li];
     uint32_t cnt;
     if constexpr (GMEM) {
-      LongState<true> L{w.lw + s, w.lw + (size_t)B + s, w.lw + 2 * (size_t)B + s, w.lw + 3 * (size_t)B + s};
+      uint32_t* lw = w.lw + 4 * (size_t)w.lw_pos[li];
+      LongState<true> L{lw, lw + n, lw + 2 * (size_t)n, lw + 3 * (size_t)n};
       cnt = long_piece<true>(t, bytes, n, L, out, err);
     } else {
       lds_u32* lds = (lds_u32*)s_long + wid * 4 * kLdsPos;
@@ -2216,10 +2252,12 @@ __device__ uint32_t bpe_wave_seg(const Tables& t, const PairLds& P, const int32_
 // dealt to the dense tier by a static stride over the long list.
 constexpr uint32_t kDenseMax = 256;
 
-__global__ __launch_bounds__(256) void k_long_len(Work w) {
+// (lwn[li]: the piece's length when the global-memory tier takes it (> gmin bytes), else 0; its
+// scan places the pieces' state in lw, the scan of long_cnt places their ids in lids)
+__global__ __launch_bounds__(256) void k_long_len(Work w, uint32_t* lwn, uint32_t gmin) {
   __shared__ uint32_t s_hist[kLhBuckets];
   const uint32_t lane = threadIdx.x & 63;
-  const uint32_t n_long = uni(w.counters[0]);
+  const uint32_t n_long = uni(long_count(w));
   const uint32_t n_waves = gridDim.x * 4;
   if (threadIdx.x < (uint32_t)kLhBuckets) s_hist[threadIdx.x] = 0;
   __syncthreads();
@@ -2228,6 +2266,7 @@ __global__ __launch_bounds__(256) void k_long_len(Work w) {
     const uint32_t n = uni(piece_end(w, s) - s);
     if (lane == 0) {
       w.long_cnt[li] = n;
+      lwn[li] = n > gmin ? n : 0u;
       if (n > kDenseMax) atomicAdd(&s_hist[long_bucket(n)], 1u);
     }
   }
@@ -2239,7 +2278,7 @@ __global__ __launch_bounds__(256) void k_long_len(Work w) {
 __global__ __launch_bounds__(256) void k_long_order(Work w) {
   __shared__ uint32_t s_scan[kLhBuckets + 1], s_cnt[kLhBuckets], s_base[kLhBuckets];
   const uint32_t tid = threadIdx.x;
-  const uint32_t n_long = w.counters[0];
+  const uint32_t n_long = long_count(w);
   if (tid == 0) {
     uint32_t a = 0;
     for (int d = 0; d < kLhBuckets; d++) {
@@ -2281,7 +2320,7 @@ __global__ __launch_bounds__(64 * NW) void k_bpe_wave(Work w, Tables t) {
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   const uint32_t wid = uni(tid >> 6);
   static_assert(SEG ? LO >= kDenseMax : HI <= kDenseMax, "ordered tiers: > kDenseMax B; dense tier: <= kDenseMax B");
-  const uint32_t n_long = uni(w.counters[0]);
+  const uint32_t n_long = uni(long_count(w));
   const uint32_t lo = SEG ? uni(w.long_hist[kLhScan + kLhBuckets - HI / 64]) : 0u;
   const uint32_t hi = SEG ? uni(w.long_hist[kLhScan + kLhBuckets - LO / 64]) : n_long;
   // (a workgroup past the tier's piece count has nothing to take: return before the image load;
@@ -2330,8 +2369,9 @@ __global__ __launch_bounds__(64 * NW) void k_bpe_wave(Work w, Tables t) {
     const uint32_t doc = (e & kLongDoc) ? kRecDoc : 0u;
     uint32_t cnt;
     uint32_t* sink = &w.counters[kCtrSink];
-    if constexpr (SEG) cnt = bpe_wave_seg<K, HOT>(t, P, s_b2id, w.text + s, n, SegSlice<K>{slice}, w.lscratch + s, err, sink);
-    else cnt = bpe_wave_dense<K, HOT>(t, P, s_b2id, w.text + s, n, WaveSlice<K>{slice}, w.lscratch + s, err, sink);
+    uint32_t* out = w.lids + w.long_pos[li];
+    if constexpr (SEG) cnt = bpe_wave_seg<K, HOT>(t, P, s_b2id, w.text + s, n, SegSlice<K>{slice}, out, err, sink);
+    else cnt = bpe_wave_dense<K, HOT>(t, P, s_b2id, w.text + s, n, WaveSlice<K>{slice}, out, err, sink);
     if (lane == 0) {
       const uint32_t tile = s / kTile;
       w.long_cnt[li] = cnt;
@@ -2351,6 +2391,23 @@ static hipError_t launch_wave(const Work& w, const Tables& t, uint32_t grid, hip
   return hipGetLastError();
 }
 
+// Long-piece preparation (side stream): lengths and the tiers' order (k_long_len, k_long_order),
+// then the places of every piece's ids in lids (scan of the lengths: ids <= bytes) and of the
+// global-memory tier's state in lw (scan of lwn).  long_pos[n_long] / lw_pos[n_long] hold the
+// totals, which the host reads back to size lids and lw before it launches the tiers.
+hipError_t launch_long_prep(const Work& w, const Tables& t, hipStream_t s, uint32_t n_long, uint32_t* lwn,
+                            uint32_t* tmp, uint64_t tmp_cap) {
+  if (n_long == 0) return hipSuccess;
+  auto cap = [](uint32_t want, uint32_t most) { return std::max(1u, std::min(want, most)); };
+  const bool added = t.n_at != 0 || t.dbg == 7;
+  HIPCHK(hipMemsetAsync(w.long_hist, 0, kLhWords * sizeof(uint32_t), s));
+  k_long_len<<<cap((n_long + 3) / 4, 4 * w.n_cus), 256, 0, s>>>(w, lwn, added ? kLdsPos : kWaveMax);
+  if (!added) k_long_order<<<cap((n_long + 255) / 256, w.n_cus), 256, 0, s>>>(w);
+  HIPCHK(hipGetLastError());
+  HIPCHK(scan_u32(w.long_cnt, w.long_pos, n_long, nullptr, tmp, tmp_cap, s));
+  return scan_u32(lwn, w.lw_pos, n_long, nullptr, tmp, tmp_cap, s);
+}
+
 hipError_t launch_bpe_long(const Work& w, const Tables& t, hipStream_t s, uint32_t n_long, bool any_c3) {
   auto cap = [](uint32_t want, uint32_t most) { return std::max(1u, std::min(want, most)); };
   if (t.n_at != 0 || t.dbg == 7) {
@@ -2367,14 +2424,11 @@ hipError_t launch_bpe_long(const Work& w, const Tables& t, hipStream_t s, uint32
     // dense wave tiers: <= 256 B (4 waves per workgroup, Bloom filter only, 43 KiB of LDS: fits
     // next to a merge-pass workgroup), 257..1024 B (segmented, 2 waves per workgroup with the
     // whole image) and 1025..4096 B (segmented, 2 waves with the Bloom filter); longer pieces:
-    // GMEM linked list.  Grids: at most one wave per long piece.  k_long_len / k_long_order first
-    // (lengths, the longest-first order of the segmented tiers' pieces).
+    // GMEM linked list.  Grids: at most one wave per long piece.  (launch_long_prep first: the
+    // lengths, the longest-first order of the segmented tiers' pieces, the id places.)
     // The long list holds pieces > kMedMax B and pieces whose end lies past the tile's look-ahead
-    // (>= 63 B: they can be shorter than kMedMax), so the first tier starts at 1 B.
-    HIPCHK(hipMemsetAsync(w.long_hist, 0, kLhWords * sizeof(uint32_t), s));
-    k_long_len<<<cap((n_long + 3) / 4, 4 * w.n_cus), 256, 0, s>>>(w);
-    k_long_order<<<cap((n_long + 255) / 256, w.n_cus), 256, 0, s>>>(w);
-    HIPCHK(hipGetLastError());
+    // (>= 63 B: they can be shorter than kMedMax), and a tile's class-0 pieces past its list's
+    // capacity, so the first tier starts at 1 B.
     HIPCHK((launch_wave<4, 0, 4, false, false>(w, t, cap((n_long + 3) / 4, 2 * w.n_cus), s)));
     if (t.dbg == 10) {  // A/B: 257..1024 B four waves per CU
       HIPCHK((launch_wave<16, 256, 4, true, true>(w, t, cap((n_long + 3) / 4, w.n_cus), s)));
@@ -2469,8 +2523,8 @@ __global__ __launch_bounds__(64 * kEmitWaves) void k_emit(Work w, uint32_t* __re
       const uint32_t r = rec[k];
       const bool follow = c[k] != 0 && !(r & kRecHit);
       sp[k] = !follow ? src0
-              : (r & kRecLong) ? w.lscratch + (uint32_t)w.long_list[r & kRecLongMask]
-              : ((r & kRecAlt) ? w.lscratch + (size_t)tile * kTile : src0) + ((r >> 16) & 0xFFFu);
+              : (r & kRecLong) ? w.lids + w.long_pos[r & kRecLongMask]
+              : src0 + ((r >> 16) & 0xFFFu);
       v0[k] = (r & kRecHit) ? (r & kRecIdMask) : (follow ? sp[k][0] : 0u);
     }
     // the round's ids: staged in LDS when they fit, then written out by the whole wave as 64

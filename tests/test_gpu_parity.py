@@ -187,6 +187,58 @@ def test_eager_cascade_rounds():
     assert tok.encode("abab") == [obj["model"]["vocab"]["aba"], obj["model"]["vocab"]["b"]]
 
 
+def _consonant_pair_docs(n, seed=8):
+    """Docs of " qx" pieces (two consonants: ~94% are not single tokens of the gpt2 fixture), about
+    1250 class-0 pieces per 3968-byte tile."""
+    rng = np.random.default_rng(seed)
+    cons = np.frombuffer(b"bcdfghjklmnpqrstvwxz", dtype=np.uint8)
+    return [b" " + b" ".join(bytes(x) for x in rng.choice(cons, size=(1500, 2))) for _ in range(n)]
+
+
+def test_class0_list_spill_to_long_list(gpt2):
+    """Tiles with more than kCap0Lean (1040) pieces of <= 8 B that are not single tokens: the
+    class-0 list keeps 1040 of a tile's pieces, the rest go to the long list and its dense wave
+    tier (ctok_internal.h kCap0Lean); against the C oracle.  40 such docs among 2.5 MB of C2 text
+    spill ~10k pieces, within the lean long list (B/32 entries)."""
+    _, tok, rc = gpt2
+    text, off = corpus.corpus_c2(20_000, seed=12)
+    docs = [bytes(text[off[i]:off[i + 1]]) for i in range(len(off) - 1)]
+    tok.encode_packed(text, off, timing=True)
+    base = tok.last_stats["long_pieces"]  # the corpus's own long pieces
+    adv = _consonant_pair_docs(40)
+    docs = docs[:5000] + adv[:20] + docs[5000:] + adv[20:]
+    text, off = corpus.pack(docs)
+    ids, toff = tok.encode_packed(text, off, timing=True)
+    assert tok.last_stats["long_pieces"] > base + 5000  # the spilled pieces (3 bytes each)
+    assert_same(ids, toff, *rc.encode_packed(text, off))
+
+
+def test_class0_spill_overflow_reruns_safe(gpt2):
+    """Only such docs: the spilled pieces outgrow the lean long list, the call runs again with the
+    safe capacities (every class-0 piece listed; no spill, so no long pieces)."""
+    _, tok, rc = gpt2
+    text, off = corpus.pack(_consonant_pair_docs(300))
+    ids, toff = tok.encode_packed(text, off, timing=True)
+    assert tok.last_stats["long_pieces"] == 0
+    assert_same(ids, toff, *rc.encode_packed(text, off))
+
+
+@pytest.mark.parametrize("n_docs", [20_000, 200_000])
+def test_dropped_byte_chars(gpt2, n_docs):
+    """A vocab without the byte chars of 'q', 'x', 'z': the reference drops those chars
+    (src/bpe.rs:94-97), so pieces holding them take the dropped-byte pass (k_bpe_generic MID: ids
+    in the tile's class region after the merge passes' ids).  200k docs overflow the lean
+    dropped-byte list (65536 entries): the call runs again with the safe capacities."""
+    obj, _, _ = gpt2
+    obj = json.loads(json.dumps(obj))
+    for c in "qxz":
+        del obj["model"]["vocab"][c]
+    tok, rc = gpu_tok(obj), ref_c.RefC(obj)
+    text, off = corpus.corpus_c2(n_docs, seed=41)
+    ids, toff = tok.encode_packed(text, off)
+    assert_same(ids, toff, *rc.encode_packed(text, off))
+
+
 def test_multi_sample(multi_path):
     with open(multi_path) as f:
         obj = json.load(f)
