@@ -8,6 +8,7 @@
 //   pre-tokenizer     src/huggingface/parsing.rs:92-190; src/pretokenizers.rs:71-126, :298-302
 //   vocab getters     src/vocab.rs:34-100, src/huggingface/mod.rs:856-866
 //   decode            src/huggingface/mod.rs:698-785, src/decoders.rs:74-119, parsing.rs:272-364
+#include <emmintrin.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -159,7 +160,7 @@ struct DevBuf {
   ~DevBuf() { if (p) (void)hipFree(p); }
 };
 
-// Pinned (page-locked) host buffer: the staging side of the host-buffer pipeline.
+// Pinned (page-locked) host buffer: the landing side of the 16-bit id copies.
 template <typename T>
 struct PinBuf {
   T* p = nullptr;
@@ -176,15 +177,16 @@ struct PinBuf {
 };
 
 // Double-buffered host-buffer pipeline of one device (ctok_encode_batch): chunk c's text is
-// staged into pin_in[c & 1] and copied to d_in[c & 1] on the copy stream while chunk c - 1 is
-// encoded; its ids come back through d_ids / pin_ids[c & 1] while chunk c + 1 is encoded.
+// copied from the caller's buffer to d_in[c & 1] on the up stream while chunk c - 1 is encoded;
+// its ids come back from d_ids[c & 1] into the caller's buffer while chunk c + 1 is encoded.
 struct HostPipe {
   hipStream_t up = nullptr, down = nullptr;  // H2D and D2H copy streams (both directions at once)
   hipEvent_t ev_h2d[2] = {}, ev_enc[2] = {}, ev_d2h[2] = {};
   hipEvent_t ev_t[4] = {};  // timing of the first chunk's H2D and the last chunk's D2H
-  PinBuf<uint8_t> pin_in[2];
-  PinBuf<uint64_t> pin_off[2], pin_tokoff[2];
-  PinBuf<uint32_t> pin_ids[2];
+  DevBuf<uint16_t> d_ids16[2];    // 16-bit wire format (ids16 tokenizers): ids, and tok_off as u32
+  DevBuf<uint32_t> d_toff32[2];
+  PinBuf<uint16_t> pin_ids16[2];
+  PinBuf<uint32_t> pin_toff32[2];
   DevBuf<uint8_t> d_in[2];
   DevBuf<uint64_t> d_off[2], d_tokoff[2];
   DevBuf<uint32_t> d_ids[2];
@@ -220,6 +222,11 @@ struct DeviceState {
   DevBuf<uint32_t> long_cnt, long_ord, long_hist;
   DevBuf<uint64_t> long_list, mid_list, scan_tmp, scan_tmp2;
   DevBuf<uint32_t> doc_flag, ncp;
+  // NFC splice (nfc_splice): flagged-doc ranks / sub-batch positions, the speculative pass's
+  // output, the sub-batch and its output
+  DevBuf<uint32_t> spl_rank, spl_ids, sub_ids;
+  DevBuf<uint64_t> spl_pos, spl_toff, sub_off, sub_toff;
+  DevBuf<uint8_t> sub_text;
   DevBuf<uint64_t> norm_off;
   DevBuf<uint8_t> norm_text;
   bool last_norm = false;  // the last encode ran on norm_text / norm_off (last_B bytes)
@@ -248,6 +255,7 @@ struct DeviceState {
     add(wpref), add(long_cnt), add(long_ord), add(long_hist), add(long_pos), add(lw_pos), add(lwn), add(long_list);
     add(mid_list), add(scan_tmp), add(scan_tmp2), add(cps);
     add(doc_flag), add(ncp), add(norm_off), add(norm_text);
+    add(spl_rank), add(spl_ids), add(sub_ids), add(spl_pos), add(spl_toff), add(sub_off), add(sub_toff), add(sub_text);
     return b;
   }
   ~DeviceState() {
@@ -307,6 +315,7 @@ struct ctok {
   bool proper = true;
   bool compact = false;
   bool narrow = false;  // every vocab id < 2^16
+  bool ids16 = false;   // every id encode can emit (vocab and added tokens) < 2^16: 16-bit ids on PCIe
   // decode (src/huggingface/mod.rs:710-747): decoder kind, per-id decoded bytes
   int decoder = 1;                  // 1 ByteLevel, 0 raw concatenation (unknown decoder type), -1 unsupported
   std::string decoder_name;         // for the unsupported message
@@ -1055,6 +1064,8 @@ void load_root(ctok* t, const ctj::Value& root) {
     t->at_flags.push_back(e.second.second);
   }
 
+  t->ids16 = t->narrow;
+  for (uint32_t id : t->at_id) t->ids16 = t->ids16 && id < 0xFFFFu;
   t->nfc = parse_normalizer(root.get("normalizer")) != 0;
   std::vector<std::pair<char, bool>> chain;
   parse_pre_tokenizer(root.get("pre_tokenizer"), chain, 0);
@@ -1198,11 +1209,67 @@ double now_ms() {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-// The pipeline on device-resident buffers.  Returns the token count.
 uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const uint64_t* d_off, uint64_t n_docs,
                        uint64_t n_bytes, uint32_t* d_ids, uint64_t ids_cap, uint64_t* d_tok_off, hipStream_t s,
                        bool timing, ctok_stats* st, bool split_added = true, bool segment_only = false,
-                       bool keep_first = false) {
+                       bool keep_first = false, bool no_spec = false);
+
+// NFC splice: the speculative pass over the raw text finished but flagged a code point NFC may
+// change (src/normalizers.rs:45-47 normalises every document).  Only the documents holding such
+// code points (k_nfc_check's flags, a superset of those NFC changes) are gathered into a
+// sub-batch, encoded normalised, and their ids replace the pass's in d_ids / d_tok_off; the
+// others' ids are already right (NFC leaves them unchanged, and pieces never cross documents).
+// Returns the token count; *n_flagged = the flagged documents.
+uint64_t nfc_splice(ctok* t, DeviceState* ds, const uint8_t* d_text, const uint64_t* d_off, uint64_t n_docs,
+                    uint64_t n_bytes, uint32_t* d_ids, uint64_t ids_cap, uint64_t* d_tok_off, uint64_t ntok_main,
+                    hipStream_t s, uint64_t* n_flagged) {
+  const Tables& tb = ds->t;
+  ds->doc_flag.ensure(n_docs + 1);
+  HIPTRY(hipMemsetAsync(ds->doc_flag.p, 0, (n_docs + 1) * 4, s));
+  HIPTRY(hipMemsetAsync(ds->counters.p + 3, 0, 4, s));
+  HIPTRY(launch_nfc_check(d_text, n_bytes, d_off, (uint32_t)n_docs, tb, ds->doc_flag.p, ds->counters.p + 3, s));
+  // ranks of the flagged docs, their places in the sub-batch
+  ds->spl_rank.ensure(n_docs + 1);
+  ds->spl_pos.ensure(n_docs + 1);
+  ds->scan_tmp.ensure(scan_tmp_elems(n_docs + 1) + 64);
+  HIPTRY(scan_u32(ds->doc_flag.p, ds->spl_rank.p, n_docs, nullptr, (uint32_t*)ds->scan_tmp.p, ds->scan_tmp.cap * 2, s));
+  HIPTRY(launch_flag_len(d_off, ds->doc_flag.p, n_docs, ds->spl_pos.p, s));
+  HIPTRY(scan_u64(ds->spl_pos.p, n_docs, ds->scan_tmp.p, ds->scan_tmp.cap, s));
+  volatile uint64_t* h = (volatile uint64_t*)(ds->host + 100);
+  HIPTRY(hipMemcpyAsync((void*)h, ds->spl_pos.p + n_docs, 8, hipMemcpyDeviceToHost, s));
+  HIPTRY(hipMemcpyAsync((void*)(h + 1), ds->spl_rank.p + n_docs, 4, hipMemcpyDeviceToHost, s));
+  spin_sync(ds, s);
+  const uint64_t SB = h[0], F = (uint32_t)h[1];
+  *n_flagged = F;
+  if (F == 0) return ntok_main;
+  // the flagged docs' raw text as a sub-batch (16-byte aligned, zero padded)
+  ds->sub_text.ensure(SB + 16);
+  ds->sub_off.ensure(F + 1);
+  HIPTRY(launch_gather_flagged(d_text, d_off, ds->spl_rank.p, ds->spl_pos.p, n_docs, ds->sub_text.p, ds->sub_off.p, s));
+  HIPTRY(hipMemcpyAsync(ds->sub_off.p + F, ds->spl_pos.p + n_docs, 8, hipMemcpyDeviceToDevice, s));
+  HIPTRY(hipMemsetAsync(ds->sub_text.p + SB, 0, 16, s));
+  // the pass's output, read by the splice
+  ds->spl_ids.ensure(ntok_main + 1);
+  ds->spl_toff.ensure(n_docs + 1);
+  if (ntok_main) HIPTRY(hipMemcpyAsync(ds->spl_ids.p, d_ids, ntok_main * 4, hipMemcpyDeviceToDevice, s));
+  HIPTRY(hipMemcpyAsync(ds->spl_toff.p, d_tok_off, (n_docs + 1) * 8, hipMemcpyDeviceToDevice, s));
+  // the sub-batch: NFC check + normalise + encode (no speculation: every doc in it is flagged)
+  ds->sub_ids.ensure(ctok_ids_bound(t, SB, F));
+  ds->sub_toff.ensure(F + 1);
+  encode_device(t, ds, ds->sub_text.p, ds->sub_off.p, F, SB, ds->sub_ids.p, ds->sub_ids.cap, ds->sub_toff.p, s, false,
+                nullptr, true, false, false, true);
+  ds->scan_tmp.ensure(scan_tmp_elems(n_docs + 1) + 64);
+  HIPTRY(launch_splice(ds->spl_rank.p, ds->spl_toff.p, ds->spl_ids.p, ds->sub_toff.p, ds->sub_ids.p, n_docs, d_ids,
+                       ids_cap, d_tok_off, ds->scan_tmp.p, ds->scan_tmp.cap, s));
+  HIPTRY(hipMemcpyAsync((void*)h, d_tok_off + n_docs, 8, hipMemcpyDeviceToHost, s));
+  spin_sync(ds, s);
+  return h[0];
+}
+
+// The pipeline on device-resident buffers.  Returns the token count.
+uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const uint64_t* d_off, uint64_t n_docs,
+                       uint64_t n_bytes, uint32_t* d_ids, uint64_t ids_cap, uint64_t* d_tok_off, hipStream_t s,
+                       bool timing, ctok_stats* st, bool split_added, bool segment_only, bool keep_first, bool no_spec) {
   if (n_bytes >= 0xF0000000ull) throw_err(CTOK_E_ARG, "a single call is limited to < 3.75 GiB of text; split the batch");
   if (n_docs >= 0xF0000000ull) throw_err(CTOK_E_ARG, "too many documents in one call");
   // split_added = false: encode_to_encoding's words go straight to BpeTokenizer::encode, with
@@ -1214,7 +1281,10 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   // let k_segment flag any code point that NFC might change (NFC_QC != Yes or a non-zero
   // combining class; ASCII never is).  Only a flagged batch pays for the check + normalise
   // passes and a second run.
-  bool speculate = t->nfc && !t->add_prefix_space && n_bytes && !getenv("CTOK_NO_NFC_SPECULATION");
+  bool speculate = t->nfc && !t->add_prefix_space && n_bytes && !no_spec && !getenv("CTOK_NO_NFC_SPECULATION");
+  // a flagged pass is finished and only its flagged docs are encoded again (nfc_splice), except
+  // where the whole batch's pass state is read afterwards (offsets, the trainer's pre-tokenizer)
+  const bool splice = d_ids && !keep_first && !segment_only && !getenv("CTOK_NFC_RERUN");
   // lean list capacities first; a call whose lists outgrow them runs again with the safe ones
   static const bool always_safe = getenv("CTOK_SAFE_CAPACITIES") != nullptr;
   bool safe = always_safe;
@@ -1271,7 +1341,7 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   w.n_words = (uint32_t)((B + 31) / 32);
   w.n_tiles = (uint32_t)((B + kTile - 1) / kTile);
   w.n_cus = ds->n_cus;
-  w.nfc_watch = speculate ? 1u : 0u;
+  w.nfc_watch = speculate ? (splice ? 2u : 1u) : 0u;
   w.keep_first = keep_first ? 1u : 0u;
   const size_t nt = w.n_tiles;
   ds->docbits.ensure(w.n_words + 8);
@@ -1287,6 +1357,13 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   // A list that outgrows its lean capacity sets counters[kCtrOverflow]: the call runs again with
   // the safe capacities (every class-0 piece listed, a dropped-byte entry per byte).
   w.k0 = safe ? kCap0 : kCap0Lean;
+  // merge-pass work units: 64 tiles, or 16 for batches under 8192 tiles (32 MB), which 64-tile
+  // units spread over too few CUs (3.8 MB: 0.41 -> 0.30 ms per call; from 16 MB up 64 is faster,
+  // profiles/r03/v16_ab_unit.txt)
+  static const uint32_t unit_env = getenv("CTOK_UNIT") ? (uint32_t)atoi(getenv("CTOK_UNIT")) : 0u;
+  w.unit = unit_env == 8 || unit_env == 16 || unit_env == 32 || unit_env == 64 ? unit_env
+           : nt >= 8192                                                        ? 64u
+                                                                               : 16u;
   w.long_cap = (uint32_t)(B / kShortMax + nt + 8);
   w.mid_cap = (uint32_t)(safe ? B + 8 : std::min<uint64_t>(B + 8, std::max<uint64_t>(65536, B / 256)));
   ds->tcls.ensure(kNumClasses * nt + 8);
@@ -1367,7 +1444,7 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
     if (e == hipSuccess) break;
     if (e != hipErrorNotReady) throw_err(CTOK_E_DEVICE, std::string("hipEventQuery: ") + hipGetErrorString(e));
   }
-  if (!(speculate && seg_cnt[12])) {  // (a failed NFC speculation discards this pass: nothing to launch)
+  if (!(w.nfc_watch == 1 && seg_cnt[12])) {  // (a failed NFC speculation discards this pass: nothing to launch)
     const uint32_t n_long = std::min<uint32_t>((uint32_t)seg_cnt[0], w.long_cap);
     if (n_long) {
       // lengths, order and places of the long pieces, then lids / lw sized from their totals
@@ -1401,16 +1478,27 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   HIPTRY(hipMemcpyAsync(ds->host, d_tok_off + n_docs, 8, hipMemcpyDeviceToHost, s));
   HIPTRY(hipMemcpyAsync(ds->host + 1, ds->counters.p, kNumCounters * 4, hipMemcpyDeviceToHost, s));
   spin_sync(ds, s);
-  const uint64_t ntok = ((volatile uint64_t*)ds->host)[0];
+  uint64_t ntok = ((volatile uint64_t*)ds->host)[0];
   uint32_t cnt[kNumCounters];
   for (int i = 0; i < kNumCounters; i++) cnt[i] = ((volatile uint32_t*)(ds->host + 1))[i];
-  if (speculate && cnt[12]) {  // a code point NFC may change: check, normalise, run again
+  if (w.nfc_watch == 1 && cnt[12]) {  // a code point NFC may change: check, normalise, run again
     speculate = false;
     continue;
   }
   if ((cnt[kCtrOverflow] || cnt[0] > w.long_cap) && !safe) {  // a lean list overflowed: run again safe
     safe = true;
     continue;
+  }
+  if (w.nfc_watch == 2 && cnt[12]) {
+    if (ntok > ids_cap) {  // the pass's ids did not all fit the output: run again normalised
+      speculate = false;
+      continue;
+    }
+    ntok = nfc_splice(t, ds, d_text, d_off, n_docs, n_bytes, d_ids, ids_cap, d_tok_off, ntok, s, &nfc_docs);
+    if (timing) {
+      HIPTRY(hipEventRecord(ds->ev[11], s));
+      HIPTRY(hipEventSynchronize(ds->ev[11]));
+    }
   }
   const uint32_t P = cnt[5];
   if (cnt[2] & kErrPanic)
@@ -1443,7 +1531,7 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
       st->ms_bpe_short = el(1, 9);
       st->ms_bpe_long = el(9, 5);
       st->ms_emit = el(3, 6);
-      st->ms_device = el(0, 6);
+      st->ms_device = w.nfc_watch == 2 && cnt[12] ? el(0, 11) : el(0, 6);
     }
   }
   return ntok;
@@ -1558,32 +1646,31 @@ uint64_t decode_device(ctok* t, DeviceState* ds, const uint32_t* d_ids, const ui
 //
 // ctok_encode_batch on host memory.  The batch is cut into chunks of about `chunk` text bytes
 // (whole documents); per chunk c (slot c & 1):
-//   stage   host threads copy the chunk's text into pinned pin_in and its rebased offsets into
-//           pin_off, then the copy stream moves them to d_in / d_off           (ev_h2d)
+//   stage   the up stream copies the chunk's text from the caller's buffer to d_in and its
+//           offsets to d_off, made chunk-relative on the device                  (ev_h2d)
 //   encode  the encode stream waits for ev_h2d (and for the D2H of chunk c - 2, which used the
-//           same d_ids), runs encode_device                                    (ev_enc)
-//   drain   the copy stream moves ids / tok_off to pinned pin_ids / pin_tokoff (ev_d2h), host
-//           threads copy them to the caller's ids (at the running token base) and tok_off.
+//           same d_ids), runs encode_device, adds the running token base to tok_off (ev_enc)
+//   drain   the down stream copies ids / tok_off straight into the caller's ids (at the running
+//           token base) and tok_off                                              (ev_d2h)
 // stage(c + 1) and drain(c - 1) run on helper threads while encode(c) runs, so PCIe traffic in
-// both directions and the host copies overlap the kernels.  The caller's buffers are never
-// registered: pinning them costs more per call than the staging copies.
+// both directions overlaps the kernels.  The copies touch the caller's pageable memory directly:
+// the runtime pins it in place at the link's rate (56-57 GB/s each way on the MI355X box, the same
+// as from hipHostMalloc memory; profiles/r03/pcie_probe.txt), so staging through pinned buffers
+// only added two host memcpys per byte (round 2: 16.3 GB/s E2E on C2).
 
-// memcpy split over up to `nt` threads (the calling thread takes the first part)
-void par_copy(void* dst, const void* src, size_t n, unsigned nt) {
-  constexpr size_t kMin = 4u << 20;
-  unsigned k = (unsigned)std::min<size_t>(nt, std::max<size_t>(1, n / kMin));
-  if (k <= 1) {
-    if (n) std::memcpy(dst, src, n);
-    return;
+// dst[i] = src[i] for i < n, with non-temporal 16-byte stores (the caller's ids are written once
+// and not read back here: no read-for-ownership of their lines)
+void widen16(uint32_t* dst, const uint16_t* src, size_t n) {
+  size_t i = 0;
+  for (; i < n && ((uintptr_t)(dst + i) & 15u); i++) dst[i] = src[i];
+  const __m128i z = _mm_setzero_si128();
+  for (; i + 8 <= n; i += 8) {
+    const __m128i v = _mm_loadu_si128((const __m128i*)(src + i));
+    _mm_stream_si128((__m128i*)(dst + i), _mm_unpacklo_epi16(v, z));
+    _mm_stream_si128((__m128i*)(dst + i + 4), _mm_unpackhi_epi16(v, z));
   }
-  const size_t per = (n + k - 1) / k;
-  std::vector<std::thread> th;
-  for (unsigned i = 1; i < k; i++) {
-    const size_t a = i * per, b = std::min(n, a + per);
-    if (a < b) th.emplace_back([=] { std::memcpy((char*)dst + a, (const char*)src + a, b - a); });
-  }
-  std::memcpy(dst, src, std::min(n, per));
-  for (auto& x : th) x.join();
+  for (; i < n; i++) dst[i] = src[i];
+  _mm_sfence();
 }
 
 HostPipe* host_pipe(DeviceState* ds) {
@@ -1616,11 +1703,19 @@ RangeOut encode_host_range(ctok* t, DeviceState* ds, const uint8_t* text, const 
   if (d1 <= d0) return r;
   HostPipe* P = host_pipe(ds);
   hipStream_t s = ds->stream;
-  // chunk boundaries: whole docs, about `chunk` bytes each (a longer doc is a chunk by itself)
+  // chunk boundaries: whole docs, about `chunk` bytes each (a longer doc is a chunk by itself),
+  // ramped: the first chunks grow from chunk / 8 and the last ones shrink to it, so the first
+  // upload and the last download, which nothing overlaps, are short
+  static const bool no_ramp = getenv("CTOK_NO_CHUNK_RAMP") != nullptr;
+  const uint64_t c_min = std::max<uint64_t>(chunk / 8, 1u << 20);
+  uint64_t want = no_ramp ? chunk : c_min;
   std::vector<uint64_t> cut{d0};
   while (cut.back() < d1) {
-    const uint64_t a = cut.back();
-    const uint64_t* e = std::upper_bound(off + a + 1, off + d1 + 1, off[a] + chunk);
+    const uint64_t a = cut.back(), left = off[d1] - off[a];
+    uint64_t sz = no_ramp ? chunk : std::min(std::min(want, chunk), std::max(c_min, left / 2));
+    if (left < sz + c_min) sz = left;  // no small remainder
+    want = std::min(2 * want, chunk);
+    const uint64_t* e = std::upper_bound(off + a + 1, off + d1 + 1, off[a] + sz);
     uint64_t b = (uint64_t)(e - off) - 1;  // last doc end <= off[a] + chunk
     if (b <= a) b = a + 1;
     cut.push_back(std::min(b, d1));
@@ -1631,33 +1726,95 @@ RangeOut encode_host_range(ctok* t, DeviceState* ds, const uint8_t* text, const 
   double ms_med = 0;
 
   // stage / drain run on helper threads: each makes the shard's device current first (the HIP
-  // current device is per thread)
+  // current device is per thread).  Both copy straight between the caller's (pageable) buffers
+  // and the device: the runtime pins the pages in place and copies at the link's rate, as fast as
+  // from pinned memory (profiles/r03/pcie_probe.txt), so there is no staging copy on the host.
+  static const bool trace = getenv("CTOK_PIPE_TRACE") != nullptr;
+  const double tr0 = now_ms();
+  auto TR = [&](const char* what, size_t c) { if (trace) fprintf(stderr, "[pipe] %8.3f %s %zu\n", now_ms() - tr0, what, c); };
   auto stage = [&](size_t c) {
+    TR("stage<", c);
     HIPTRY(hipSetDevice(ds->device));
     const int k = (int)(c & 1);
     const uint64_t a = cut[c], b = cut[c + 1], n = b - a, B = off[b] - off[a];
-    HIPTRY(hipEventSynchronize(P->ev_h2d[k]));  // chunk c - 2's H2D from these pinned buffers
-    P->pin_in[k].ensure(B + 16);
-    P->pin_off[k].ensure(n + 1);
-    par_copy(P->pin_in[k].p, text + off[a], B, nthreads);
-    std::memset(P->pin_in[k].p + B, 0, 16);
-    for (uint64_t i = 0; i <= n; i++) P->pin_off[k].p[i] = off[a + i] - off[a];
+    // (d_in[k] / d_off[k] were last read by chunk c - 2's encode, which has returned)
     if (timing && c == 0) HIPTRY(hipEventRecord(P->ev_t[0], P->up));
-    HIPTRY(hipMemcpyAsync(P->d_in[k].p, P->pin_in[k].p, B + 16, hipMemcpyHostToDevice, P->up));
-    HIPTRY(hipMemcpyAsync(P->d_off[k].p, P->pin_off[k].p, (n + 1) * 8, hipMemcpyHostToDevice, P->up));
+    if (B) HIPTRY(hipMemcpyAsync(P->d_in[k].p, text + off[a], B, hipMemcpyHostToDevice, P->up));
+    HIPTRY(hipMemsetAsync(P->d_in[k].p + B, 0, 16, P->up));
+    HIPTRY(hipMemcpyAsync(P->d_off[k].p, off + a, (n + 1) * 8, hipMemcpyHostToDevice, P->up));
+    HIPTRY(shift_u64(P->d_off[k].p, n + 1, (uint64_t)0 - off[a], P->up));  // chunk-relative offsets
     if (timing && c == 0) HIPTRY(hipEventRecord(P->ev_t[1], P->up));
     HIPTRY(hipEventRecord(P->ev_h2d[k], P->up));
+    if (trace) { HIPTRY(hipEventSynchronize(P->ev_h2d[k])); TR("stage>", c); }
   };
+  // ids16 tokenizers: the ids cross the link as u16 and tok_off as u32 (k_wire16), into pinned
+  // buffers, and host threads widen them into the caller's buffers (which also first-touches
+  // fresh output pages on several threads); the link is the E2E bound (56 GB/s for both
+  // directions together), and this moves 2 B per id instead of 4
+  const bool w16 = t->ids16 && !getenv("CTOK_WIRE32");
   auto drain = [&](size_t c) {
     HIPTRY(hipSetDevice(ds->device));
     const int k = (int)(c & 1);
     const uint64_t a = cut[c], n = cut[c + 1] - a;
-    HIPTRY(hipEventSynchronize(P->ev_d2h[k]));
     const uint64_t b0 = base[c], nt = ntok[c];
-    if (b0 < cap) par_copy(ids + b0, P->pin_ids[k].p, std::min(nt, cap - b0) * 4, nthreads);
-    const uint64_t* to = P->pin_tokoff[k].p;
-    uint64_t* dst = tok_off + (a - d0);
-    for (uint64_t i = 1; i <= n; i++) dst[i] = b0 + to[i];
+    const uint64_t nc = b0 < cap ? std::min(nt, cap - b0) : 0;  // ids that fit the caller's buffer
+    uint64_t* dst_off = tok_off + (a - d0);
+    HIPTRY(hipStreamWaitEvent(P->down, P->ev_enc[k], 0));  // chunk c's ids and tok_off
+    if (timing && c + 1 == C) HIPTRY(hipEventRecord(P->ev_t[2], P->down));
+    if (w16) {
+      P->pin_ids16[k].ensure(nt + 8);
+      P->pin_toff32[k].ensure(n + 1);
+      if (nc) HIPTRY(hipMemcpyAsync(P->pin_ids16[k].p, P->d_ids16[k].p, nc * 2, hipMemcpyDeviceToHost, P->down));
+      HIPTRY(hipMemcpyAsync(P->pin_toff32[k].p, P->d_toff32[k].p, (n + 1) * 4, hipMemcpyDeviceToHost, P->down));
+    } else {
+      if (nc) HIPTRY(hipMemcpyAsync(ids + b0, P->d_ids[k].p, nc * 4, hipMemcpyDeviceToHost, P->down));
+      if (n) HIPTRY(hipMemcpyAsync(dst_off + 1, P->d_tokoff[k].p + 1, n * 8, hipMemcpyDeviceToHost, P->down));
+    }
+    if (timing && c + 1 == C) HIPTRY(hipEventRecord(P->ev_t[3], P->down));
+    HIPTRY(hipEventRecord(P->ev_d2h[k], P->down));
+    TR("drain<", c);
+    HIPTRY(hipEventSynchronize(P->ev_d2h[k]));
+    TR("d2h>", c);
+  };
+  // widen(c) (w16): chunk c's 16-bit ids / 32-bit tok_off from the pinned slot into the caller's
+  // buffers, on up to nthreads threads.  Runs on its own thread, overlapping the next chunks'
+  // copies; joined before the slot is drained into again (wid[c & 1]) and at the end.
+  auto widen = [&](size_t c) {
+    const int k = (int)(c & 1);
+    const uint64_t a = cut[c], n = cut[c + 1] - a;
+    const uint64_t b0 = base[c], nt = ntok[c];
+    const uint64_t nc = b0 < cap ? std::min(nt, cap - b0) : 0;
+    const uint16_t* src = P->pin_ids16[k].p;
+    uint32_t* dst = ids + b0;
+    const unsigned nw = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(nthreads, nc >> 20));
+    const uint64_t per = (nc + nw - 1) / nw;
+    std::vector<std::thread> th;
+    for (unsigned i = 1; i < nw; i++)
+      th.emplace_back([=] { const uint64_t lo = std::min(nc, i * per); widen16(dst + lo, src + lo, std::min(nc, lo + per) - lo); });
+    widen16(dst, src, std::min(nc, per));
+    const uint32_t* to = P->pin_toff32[k].p;
+    uint64_t* dst_off = tok_off + (a - d0);
+    for (uint64_t i = 1; i <= n; i++) dst_off[i] = b0 + to[i];
+    for (auto& x : th) x.join();
+    TR("widen>", c);
+  };
+  std::thread wid[2];
+  std::exception_ptr ex_wid[2];
+  struct WidJoiner {
+    std::thread* w;
+    ~WidJoiner() {
+      for (int i = 0; i < 2; i++)
+        if (w[i].joinable()) w[i].join();
+    }
+  } wid_joiner{wid};
+  auto start_widen = [&](size_t c) {
+    wid[c & 1] = std::thread([&, c] {
+      try { widen(c); } catch (...) { ex_wid[c & 1] = std::current_exception(); }
+    });
+  };
+  auto join_widen = [&](int k) {
+    if (wid[k].joinable()) wid[k].join();
+    if (ex_wid[k]) std::rethrow_exception(ex_wid[k]);
   };
   // device buffers sized for the largest chunk up front (no reallocation while copies are in flight)
   {
@@ -1671,19 +1828,25 @@ RangeOut encode_host_range(ctok* t, DeviceState* ds, const uint8_t* text, const 
       P->d_off[k].ensure(maxD + 1);
       P->d_tokoff[k].ensure(maxD + 1);
       P->d_ids[k].ensure(ctok_ids_bound(t, maxB, maxD));
+      if (w16) {
+        P->d_ids16[k].ensure(ctok_ids_bound(t, maxB, maxD));
+        P->d_toff32[k].ensure(maxD + 1);
+      }
     }
   }
   stage(0);
   for (size_t c = 0; c < C; c++) {
     const int k = (int)(c & 1);
     const uint64_t a = cut[c], n = cut[c + 1] - a, B = off[cut[c + 1]] - off[a];
-    // helper threads; an exception inside one is rethrown here after the join
+    // helper threads: chunk c + 1 goes up and chunk c - 1 comes down while chunk c is encoded;
+    // an exception inside one is rethrown here after the join
     std::exception_ptr ex_stage, ex_drain;
     std::thread th_stage, th_drain;
     if (c + 1 < C)
       th_stage = std::thread([&, c] {
         try { stage(c + 1); } catch (...) { ex_stage = std::current_exception(); }
       });
+    if (c >= 1) join_widen((int)((c - 1) & 1));  // (widen(c - 3) read the pinned slot drain(c - 1) fills)
     if (c >= 1)
       th_drain = std::thread([&, c] {
         try { drain(c - 1); } catch (...) { ex_drain = std::current_exception(); }
@@ -1699,9 +1862,11 @@ RangeOut encode_host_range(ctok* t, DeviceState* ds, const uint8_t* text, const 
     HIPTRY(hipStreamWaitEvent(s, P->ev_h2d[k], 0));
     HIPTRY(hipStreamWaitEvent(s, P->ev_d2h[k], 0));  // chunk c - 2's ids have left d_ids[k]
     ctok_stats cs{};
+    TR("enc<", c);
     ntok[c] = encode_device(t, ds, P->d_in[k].p, P->d_off[k].p, n, B, P->d_ids[k].p, P->d_ids[k].cap,
                             P->d_tokoff[k].p, s, timing, &cs);
     base[c + 1] = base[c] + ntok[c];
+    TR("enc>", c);
     if (st) {
       st->pieces += cs.pieces;
       st->long_pieces += cs.long_pieces;
@@ -1716,22 +1881,22 @@ RangeOut encode_host_range(ctok* t, DeviceState* ds, const uint8_t* text, const 
       ms_em += cs.ms_emit, ms_seg += cs.ms_segment, ms_lo += cs.ms_bpe_lo, ms_hi += cs.ms_bpe_hi;
       ms_med += cs.ms_bpe_med;
     }
-    if (th_drain.joinable()) th_drain.join();  // pin_ids[k ^ 1] is free again
-    if (ex_drain) std::rethrow_exception(ex_drain);
-    // D2H of chunk c (encode_device returned, so its ids are complete)
-    P->pin_ids[k].ensure(ntok[c] + 1);
-    P->pin_tokoff[k].ensure(n + 1);
+    if (w16)
+      HIPTRY(wire16(P->d_ids[k].p, ntok[c], P->d_ids16[k].p, P->d_tokoff[k].p, n + 1, P->d_toff32[k].p, s));
+    else
+      HIPTRY(shift_u64(P->d_tokoff[k].p + 1, n, base[c], s));  // batch-relative tok_off
     HIPTRY(hipEventRecord(P->ev_enc[k], s));
-    HIPTRY(hipStreamWaitEvent(P->down, P->ev_enc[k], 0));
-    if (timing && c + 1 == C) HIPTRY(hipEventRecord(P->ev_t[2], P->down));
-    if (ntok[c]) HIPTRY(hipMemcpyAsync(P->pin_ids[k].p, P->d_ids[k].p, ntok[c] * 4, hipMemcpyDeviceToHost, P->down));
-    HIPTRY(hipMemcpyAsync(P->pin_tokoff[k].p, P->d_tokoff[k].p, (n + 1) * 8, hipMemcpyDeviceToHost, P->down));
-    if (timing && c + 1 == C) HIPTRY(hipEventRecord(P->ev_t[3], P->down));
-    HIPTRY(hipEventRecord(P->ev_d2h[k], P->down));
+    if (th_drain.joinable()) th_drain.join();
+    if (ex_drain) std::rethrow_exception(ex_drain);
+    if (c >= 1 && w16) start_widen(c - 1);
     if (th_stage.joinable()) th_stage.join();
     if (ex_stage) std::rethrow_exception(ex_stage);
   }
+  join_widen((int)((C - 1) & 1));
   drain(C - 1);
+  if (w16) widen(C - 1);
+  join_widen(0);
+  join_widen(1);
   r.ntok = base[C];
   r.overflow = r.ntok > cap;
   if (st && timing) {
@@ -2070,7 +2235,7 @@ int ctok_encode_batch(const ctok* tc, const uint8_t* utf8_in, const uint64_t* do
     if (exec && exec->devices && exec->n_devices > 0) devs.assign(exec->devices, exec->devices + exec->n_devices);
     else devs.push_back(exec ? exec->device : 0);
     const bool timing = exec && (exec->flags & CTOK_F_TIMING);
-    const uint64_t chunk = (uint64_t)(exec && exec->chunk_mb ? exec->chunk_mb : 32u) << 20;
+    const uint64_t chunk = (uint64_t)(exec && exec->chunk_mb ? exec->chunk_mb : 64u) << 20;
     const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
     const unsigned nthr = exec && exec->host_threads ? exec->host_threads
                                                      : std::max(1u, std::min(8u, hw / (2u * (unsigned)devs.size())));

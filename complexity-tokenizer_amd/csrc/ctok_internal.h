@@ -198,8 +198,9 @@ struct Work {              // device pointers, sized by the host for one call
   uint32_t n_words;
   uint32_t n_tiles;
   uint32_t n_cus;          // compute units of the device (persistent merge-pass grid)
-  uint32_t nfc_watch;      // 1: the text was not NFC-checked; k_segment sets counters[12] on a
-                           // code point NFC might change
+  uint32_t nfc_watch;      // 1, 2: the text was not NFC-checked; k_segment sets counters[12] on a
+                           // code point NFC might change; 1: the later passes then stop (the call
+                           // runs again normalised), 2: they finish (the flagged docs are spliced)
   uint32_t keep_first;     // 1: k_emit leaves every piece's first id within its tile in tcnt (not
                            // only doc-start pieces'), for ctok_encode_offsets
   uint16_t* wpref;         // [n_tiles * 64] pieces of the tile before each 64-byte word
@@ -224,7 +225,8 @@ struct Work {              // device pointers, sized by the host for one call
   uint32_t* rend;          // [kNumClasses][n_tiles] end of the consumed part of each class region (merge passes;
                            // the dropped-byte pass allocates after it)
   uint2* tregion;          // [n_tiles] class region bases of the tile in scratch (region_base)
-  uint32_t long_cap, mid_cap;  // long_list / mid_list entries (appends past them set counters[kCtrOverflow])
+  uint32_t long_cap, mid_cap;
+  uint32_t unit;  // tiles per work unit of the register merge passes (8..64; chunks take 1..KT / unit units)  // long_list / mid_list entries (appends past them set counters[kCtrOverflow])
   uint64_t* long_list;     // pieces > kMedMax B (> kShortMax B in generic mode), or of unknown length
                            // at a tile end: s | j << 32
   uint64_t* mid_list;      // pieces with dropped bytes for the generic kernel: s | j << 32 | n << 48
@@ -334,5 +336,18 @@ hipError_t scan_u32(const uint32_t* in, uint32_t* out, uint64_t n_max, const uin
                     uint32_t* tmp, uint64_t tmp_cap, hipStream_t s);
 hipError_t scan_u64(uint64_t* inout, uint64_t n, uint64_t* tmp, uint64_t tmp_cap, hipStream_t s);
 uint64_t scan_tmp_elems(uint64_t n_max);
+hipError_t shift_u64(uint64_t* p, uint64_t n, uint64_t delta, hipStream_t s);  // p[0, n) += delta
+// NFC splice (see kernels.hip): len[d] = flagged doc d's bytes (else 0); flagged docs' bytes
+// gathered to the sub-batch; the output's counts, offsets (out_off[0..n_docs]) and ids
+hipError_t launch_flag_len(const uint64_t* off, const uint32_t* flag, uint64_t n_docs, uint64_t* len, hipStream_t s);
+hipError_t launch_gather_flagged(const uint8_t* text, const uint64_t* off, const uint32_t* rank, const uint64_t* sub_pos,
+                                 uint64_t n_docs, uint8_t* sub_text, uint64_t* sub_off, hipStream_t s);
+hipError_t launch_splice(const uint32_t* rank, const uint64_t* main_off, const uint32_t* main_ids, const uint64_t* sub_off,
+                         const uint32_t* sub_ids, uint64_t n_docs, uint32_t* ids, uint64_t ids_cap, uint64_t* out_off,
+                         uint64_t* tmp, uint64_t tmp_cap, hipStream_t s);
+// ids16[i] = ids[i] (i < n_ids; every id < 2^16), toff32[i] = toff[i] (i < n_off; every value < 2^32);
+// ids must be 16-byte aligned (DevBuf allocations are)
+hipError_t wire16(const uint32_t* ids, uint64_t n_ids, uint16_t* ids16, const uint64_t* toff, uint64_t n_off,
+                  uint32_t* toff32, hipStream_t s);
 
 }  // namespace ctok_dev

@@ -131,7 +131,7 @@ __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_re
 // NFC speculation failed in k_segment (a code point NFC might change): the rest of this pass is
 // discarded (the host checks, normalises and runs the pipeline again), so the kernels after
 // k_segment return at once instead of merging text that will be re-encoded.
-__device__ __forceinline__ bool spec_failed(const Work& w) { return w.nfc_watch && uni(w.counters[12]) != 0; }
+__device__ __forceinline__ bool spec_failed(const Work& w) { return w.nfc_watch == 1 && uni(w.counters[12]) != 0; }
 
 // pieces in the long list (k_segment counts them all; past long_cap they were not stored and the
 // host reruns the call with the safe capacities)
@@ -1183,7 +1183,7 @@ struct PassLds {
 };
 
 // Merge pass over one length class (N = 8, 16, 32 slots), run by a persistent grid:
-// workgroups take chunks of 64-tile units from a counter (up to KT / 64 units at once when the
+// workgroups take chunks of w.unit-tile units from a counter (up to KT / w.unit units at once when the
 // previous chunk left most of the workgroup idle: sparse classes) (counters[ctr_chunk(class)]) and walk the chunk's
 // class lists as one concatenated list (see tile_share_init).  Thread per piece, tokens and pair
 // ranks in registers (fully unrolled, compile-time slots).
@@ -1212,7 +1212,8 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
   // chunks of K tiles dealt dynamically (one atomic per chunk, taken by thread 0 and broadcast
   // through LDS): workgroups that start late, or whose CU is shared, take fewer chunks
   __syncthreads();
-  uint32_t take = 1;  // 64-tile units of the next chunk (workgroup-uniform)
+  uint32_t take = 1;  // units of the next chunk (workgroup-uniform)
+  const uint32_t U = w.unit;
   for (;;) {
     if (tid == 0) {
       S.chunk = atomicAdd(&w.counters[ctr_chunk(LC::cls)], take);
@@ -1220,9 +1221,9 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
       S.next = 0;
     }
     __syncthreads();
-    const uint32_t c0 = S.chunk * 64;
+    const uint32_t c0 = S.chunk * U;
     if (c0 >= w.n_tiles) break;
-    const uint32_t tb1 = min(w.n_tiles, c0 + 64 * S.take);
+    const uint32_t tb1 = min(w.n_tiles, c0 + U * S.take);
     const uint32_t E = tile_share_init<K>(counts, tb1, c0, S.pre, S.tsum, w.tregion, LC::cls, S.tbase);
     if (E && !loaded) {  // E is workgroup-uniform (read from LDS after a barrier)
       load();
@@ -1391,9 +1392,9 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
     // size the next chunk for about two entries per thread (up to K tiles): sparse classes take
     // several units at once, dense ones one; never more than a fair share of the units left, so
     // the last chunks stay small (C2: 504 units for 256 workgroups)
-    const uint32_t units = (w.n_tiles + 63) / 64, next = S.chunk + S.take;
+    const uint32_t units = (w.n_tiles + U - 1) / U, next = S.chunk + S.take;
     const uint32_t share = next < units ? (units - next) / gridDim.x : 0u;
-    take = min(min((uint32_t)K / 64, max(1u, share)), N <= 16 ? 64u : max(1u, (2 * NT * S.take + E) / (E + 1)));
+    take = min(min((uint32_t)K / U, max(1u, share)), N <= 16 ? 64u : max(1u, (2 * NT * S.take + E) / (E + 1)));
     __syncthreads();
   }
   // statistics: bytes merged and ids produced by this pass (algorithmic bytes for the roofline)
@@ -1470,7 +1471,13 @@ __global__ __launch_bounds__(512) void k_bpe_mid(Work w, Tables t) {
   // (the image is loaded up front: a lazy load pushes the 64-slot pass into scratch; the kernel
   // returns at once when k_segment found no piece of its class)
   if (w.counters[CLS == 2 ? kCtrAnyMid : kCtrAnyC3] == 0) return;
-  if (__atomic_load_n(&w.counters[ctr_chunk(CLS)], __ATOMIC_RELAXED) * 64ull >= w.n_tiles) return;
+  // every chunk already taken (the other instance of class 3 got there first): one read for the
+  // whole workgroup, so its waves leave together (a wave that stayed would find thread 0 gone)
+  __shared__ uint32_t s_left;
+  if (threadIdx.x == 0)
+    s_left = (uint64_t)__atomic_load_n(&w.counters[ctr_chunk(CLS)], __ATOMIC_RELAXED) * w.unit < w.n_tiles;
+  __syncthreads();
+  if (!s_left) return;
   const uint32_t tid = threadIdx.x;
   const uint4* img = NARROW ? t.lds16_image : t.lds_image;
   for (uint32_t i = tid; i < kLdsImageBytes / 16; i += 512) s_img[i] = img[i];
@@ -1504,7 +1511,7 @@ static hipError_t launch_mid_t(const Work& w, const Tables& t, hipStream_t s) {
   static LdsAttr attr;
   HIPCHK(lds_attr_once(attr, (const void*)k_bpe_mid<C, CLS, NW>, kLdsImageBytes));
   if (!w.n_tiles) return hipSuccess;
-  k_bpe_mid<C, CLS, NW><<<min((w.n_tiles + 63) / 64, w.n_cus), 512, kLdsImageBytes, s>>>(w, t);
+  k_bpe_mid<C, CLS, NW><<<min((w.n_tiles + w.unit - 1) / w.unit, w.n_cus), 512, kLdsImageBytes, s>>>(w, t);
   return hipGetLastError();
 }
 template <bool C, int CLS>
@@ -1517,7 +1524,7 @@ static hipError_t launch_short_t(const Work& w, const Tables& t, hipStream_t s) 
   static LdsAttr attr;
   HIPCHK(lds_attr_once(attr, (const void*)k_bpe_short<C, NW>, kLdsImageBytes));
   if (!w.n_tiles) return hipSuccess;
-  k_bpe_short<C, NW><<<min((w.n_tiles + 63) / 64, w.n_cus), ShortCfg<NW>::NT, kLdsImageBytes, s>>>(w, t);
+  k_bpe_short<C, NW><<<min((w.n_tiles + w.unit - 1) / w.unit, w.n_cus), ShortCfg<NW>::NT, kLdsImageBytes, s>>>(w, t);
   return hipGetLastError();
 }
 template <bool C>
@@ -2715,6 +2722,128 @@ hipError_t scan_u32(const uint32_t* in, uint32_t* out, uint64_t n_max, const uin
 
 hipError_t scan_u64(uint64_t* inout, uint64_t n, uint64_t* tmp, uint64_t tmp_cap, hipStream_t s) {
   return scan_impl<uint64_t>(inout, inout, n, nullptr, tmp, tmp_cap, s);
+}
+
+// ------------------------------------------------------------------------------------------
+// NFC splice (ctok_host.cpp nfc_splice): after a speculative pass over raw text flagged code
+// points NFC may change, only the documents holding them are normalised and encoded again, as a
+// sub-batch, and their ids replace the speculative pass's in the output.  rank[d] = flagged docs
+// before d (exclusive scan of the NFC-check flags; doc d is flagged when rank[d + 1] > rank[d]).
+
+// len[d] = bytes of doc d if it is flagged, else 0 (scanned to the sub-batch offsets)
+__global__ __launch_bounds__(256) void k_flag_len(const uint64_t* __restrict__ off, const uint32_t* __restrict__ flag,
+                                                  uint64_t n_docs, uint64_t* __restrict__ len) {
+  for (uint64_t d = (uint64_t)blockIdx.x * 256 + threadIdx.x; d < n_docs; d += (uint64_t)gridDim.x * 256)
+    len[d] = flag[d] ? off[d + 1] - off[d] : 0;
+}
+
+// one wavefront per flagged doc: its bytes to sub_text at sub_pos[d], its start to sub_off[rank[d]]
+__global__ __launch_bounds__(256) void k_gather_flagged(const uint8_t* __restrict__ text, const uint64_t* __restrict__ off,
+                                                        const uint32_t* __restrict__ rank, const uint64_t* __restrict__ sub_pos,
+                                                        uint64_t n_docs, uint8_t* __restrict__ sub_text,
+                                                        uint64_t* __restrict__ sub_off) {
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint64_t d = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 6; d < n_docs; d += ((uint64_t)gridDim.x * 256) >> 6) {
+    const uint32_t r = rank[d];
+    if (rank[d + 1] == r) continue;  // (wave-uniform)
+    const uint64_t a = off[d], n = off[d + 1] - a, p = sub_pos[d];
+    if (lane == 0) sub_off[r] = p;
+    for (uint64_t i = lane; i < n; i += 64) sub_text[p + i] = text[a + i];
+  }
+}
+
+// cnt[d] = ids of doc d in the spliced output: the sub-batch's for a flagged doc, else the
+// speculative pass's (scanned in place to the output tok_off)
+__global__ __launch_bounds__(256) void k_splice_count(const uint32_t* __restrict__ rank, const uint64_t* __restrict__ main_off,
+                                                      const uint64_t* __restrict__ sub_off, uint64_t n_docs,
+                                                      uint64_t* __restrict__ cnt) {
+  for (uint64_t d = (uint64_t)blockIdx.x * 256 + threadIdx.x; d < n_docs; d += (uint64_t)gridDim.x * 256) {
+    const uint32_t r = rank[d];
+    cnt[d] = rank[d + 1] != r ? sub_off[r + 1] - sub_off[r] : main_off[d + 1] - main_off[d];
+  }
+}
+
+// one wavefront per doc: its ids from the sub-batch or the speculative pass to out_off[d]
+__global__ __launch_bounds__(256) void k_splice_copy(const uint32_t* __restrict__ rank, const uint64_t* __restrict__ main_off,
+                                                     const uint32_t* __restrict__ main_ids, const uint64_t* __restrict__ sub_off,
+                                                     const uint32_t* __restrict__ sub_ids, const uint64_t* __restrict__ out_off,
+                                                     uint64_t n_docs, uint32_t* __restrict__ ids, uint64_t ids_cap) {
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint64_t d = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 6; d < n_docs; d += ((uint64_t)gridDim.x * 256) >> 6) {
+    const uint32_t r = rank[d];
+    const bool f = rank[d + 1] != r;
+    const uint32_t* src = f ? sub_ids + sub_off[r] : main_ids + main_off[d];
+    const uint64_t o = out_off[d], n = out_off[d + 1] - o;
+    for (uint64_t i = lane; i < n; i += 64)
+      if (o + i < ids_cap) ids[o + i] = src[i];
+  }
+}
+
+static uint32_t grid_for(uint64_t threads) {
+  return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((threads + 255) / 256, 16384));
+}
+
+hipError_t launch_flag_len(const uint64_t* off, const uint32_t* flag, uint64_t n_docs, uint64_t* len, hipStream_t s) {
+  if (!n_docs) return hipSuccess;
+  k_flag_len<<<grid_for(n_docs), 256, 0, s>>>(off, flag, n_docs, len);
+  return hipGetLastError();
+}
+
+hipError_t launch_gather_flagged(const uint8_t* text, const uint64_t* off, const uint32_t* rank, const uint64_t* sub_pos,
+                                 uint64_t n_docs, uint8_t* sub_text, uint64_t* sub_off, hipStream_t s) {
+  if (!n_docs) return hipSuccess;
+  k_gather_flagged<<<grid_for(64 * n_docs), 256, 0, s>>>(text, off, rank, sub_pos, n_docs, sub_text, sub_off);
+  return hipGetLastError();
+}
+
+hipError_t launch_splice(const uint32_t* rank, const uint64_t* main_off, const uint32_t* main_ids, const uint64_t* sub_off,
+                         const uint32_t* sub_ids, uint64_t n_docs, uint32_t* ids, uint64_t ids_cap, uint64_t* out_off,
+                         uint64_t* tmp, uint64_t tmp_cap, hipStream_t s) {
+  if (!n_docs) return hipSuccess;
+  k_splice_count<<<grid_for(n_docs), 256, 0, s>>>(rank, main_off, sub_off, n_docs, out_off);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  e = scan_u64(out_off, n_docs, tmp, tmp_cap, s);
+  if (e != hipSuccess) return e;
+  k_splice_copy<<<grid_for(64 * n_docs), 256, 0, s>>>(rank, main_off, main_ids, sub_off, sub_ids, out_off, n_docs, ids, ids_cap);
+  return hipGetLastError();
+}
+
+// p[i] += delta (mod 2^64) for i < n: a host-buffer chunk's doc offsets made chunk-relative, its
+// tok_off made batch-relative, on the device before the direct copies
+__global__ __launch_bounds__(256) void k_shift_u64(uint64_t* __restrict__ p, uint64_t n, uint64_t delta) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) p[i] += delta;
+}
+
+// The 16-bit wire format of the host-buffer pipeline (ids16 tokenizers): ids[0, n_ids) as u16
+// and tok_off[0, n_off) (chunk-relative, < 2^32) as u32, so the D2H copies move 2 B per id
+// instead of 4.  Eight ids per thread: two 16-byte loads, one 16-byte store.
+__global__ __launch_bounds__(256) void k_wire16(const uint32_t* __restrict__ ids, uint64_t n_ids, uint16_t* __restrict__ ids16,
+                                                const uint64_t* __restrict__ toff, uint64_t n_off,
+                                                uint32_t* __restrict__ toff32) {
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  const uint64_t n8 = n_ids / 8;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += stride) {
+    const uint4 a = reinterpret_cast<const uint4*>(ids)[2 * i], b = reinterpret_cast<const uint4*>(ids)[2 * i + 1];
+    reinterpret_cast<uint4*>(ids16)[i] = make_uint4(a.x | (a.y << 16), a.z | (a.w << 16), b.x | (b.y << 16), b.z | (b.w << 16));
+  }
+  for (uint64_t i = 8 * n8 + (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n_ids; i += stride) ids16[i] = (uint16_t)ids[i];
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n_off; i += stride) toff32[i] = (uint32_t)toff[i];
+}
+
+hipError_t wire16(const uint32_t* ids, uint64_t n_ids, uint16_t* ids16, const uint64_t* toff, uint64_t n_off,
+                  uint32_t* toff32, hipStream_t s) {
+  const uint64_t work = std::max<uint64_t>(n_ids / 8, n_off);
+  const uint32_t g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((work + 255) / 256, 8192));
+  k_wire16<<<g, 256, 0, s>>>(ids, n_ids, ids16, toff, n_off, toff32);
+  return hipGetLastError();
+}
+
+hipError_t shift_u64(uint64_t* p, uint64_t n, uint64_t delta, hipStream_t s) {
+  if (n == 0 || delta == 0) return hipSuccess;
+  const uint32_t g = (uint32_t)std::min<uint64_t>((n + 255) / 256, 4096);
+  k_shift_u64<<<g, 256, 0, s>>>(p, n, delta);
+  return hipGetLastError();
 }
 
 // ------------------------------------------------------------------------------------------

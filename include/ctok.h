@@ -113,8 +113,8 @@ typedef struct ctok_exec {
   const int* devices;     /* shard the batch over these devices (contiguous doc ranges balanced by
                              bytes, one host thread each, no collective); NULL = { device }      */
   int n_devices;
-  uint32_t chunk_mb;      /* pipeline chunk: MiB of text per H2D -> encode -> D2H step (0 = 32)  */
-  uint32_t host_threads;  /* staging memcpy threads per device (0 = auto)                       */
+  uint32_t chunk_mb;      /* pipeline chunk: MiB of text per H2D -> encode -> D2H step (0 = 64)  */
+  uint32_t host_threads;  /* host threads widening 16-bit ids per device (0 = auto)            */
 } ctok_exec;
 
 #define CTOK_F_TIMING 1u  /* record per-kernel HIP events (fills ctok_stats.ms_*) */
@@ -145,8 +145,10 @@ uint64_t ctok_ids_bound(const ctok* tok, uint64_t n_bytes, uint64_t n_docs);
 
 /* Tokenizer.encode_batch(texts) on host buffers   src/bindings/tokenizer.rs:207-210
  *   -> HuggingFaceTokenizer::encode_batch          src/huggingface/mod.rs:694-696
- * The batch moves through pinned staging in chunks (exec->chunk_mb): the H2D copy of the next
- * chunk and the D2H copy of the previous one overlap the kernels of the current one.  With
+ * The batch moves in chunks (exec->chunk_mb, ramped from 1/8 of it at both ends) copied straight
+ * from / to the caller's buffers: the H2D copy of the next chunk and the D2H copy of the previous
+ * one overlap the kernels of the current one (ids cross the link as 16-bit values when every id
+ * the tokenizer can emit is < 2^16, widened into `ids` by host threads).  With
  * exec->devices, each device encodes its own byte-balanced doc range the same way (the
  * reference's rayon par_iter over docs, one GPU per range instead of one core per doc).
  * utf8[doc_off[d] .. doc_off[d+1]) is document d (valid UTF-8, doc_off[0] == 0,

@@ -251,8 +251,9 @@ def test_multi_sample(multi_path):
 
 def test_multi_nfc_sample(multi_path):
     """C5-NFC: 5% of 20k multilingual docs carry NFC-active text (decomposed Latin, conjoining
-    jamo, Devanagari / Arabic / Hebrew / Thai marks): the k_segment speculation fails and the GPU
-    NFC path (k_nfc_check -> k_norm -> the pipeline again) runs."""
+    jamo, Devanagari / Arabic / Hebrew / Thai marks): the k_segment speculation flags them, and
+    the flagged docs are normalised (k_nfc_check -> k_norm) and encoded again as a sub-batch
+    whose ids are spliced into the speculative pass's output."""
     with open(multi_path) as f:
         obj = json.load(f)
     tok = Tokenizer.from_file(multi_path)
@@ -349,6 +350,31 @@ def test_nfc_speculation_redo(gpt2):
         want = rc.encode_batch(docs)
         assert got == want, "batch with tail %r differs" % tail
         assert tok.last_stats is None or tok.last_stats.get("nfc_docs", 0) == (1 if tail else 0)
+
+
+@pytest.mark.parametrize("mode", ["splice", "rerun"])
+def test_nfc_splice_positions(gpt2, monkeypatch, mode):
+    """NFC-active docs (decomposed accents that NFC composes: fewer bytes, other tokens; marks
+    that stay) at the first, last and middle positions, in runs, beside empty docs, among ASCII
+    docs: the speculative pass finishes and only the flagged docs are encoded again, normalised,
+    and spliced in (ctok_host.cpp nfc_splice); "rerun" is the whole-batch path it replaces.
+    Both against the C oracle."""
+    obj, tok, rc = gpt2
+    if mode == "rerun":
+        monkeypatch.setenv("CTOK_NFC_RERUN", "1")
+    text, off = corpus.corpus_c2(5_000, seed=78)
+    base = [d.decode() for d in corpus.unpack(text, off)]
+    act = ["cafe\u0301 A\u030a", "n\u0303o e\u0301e\u0301 \u1100\u1161\u11a8", "\u0915\u093c x",
+           "\u00e9\u0301", "plain e\u0301" * 40]
+    docs = [act[0]] + base[:100] + [act[1], act[2]] + base[100:2000] + ["", act[3], ""] + base[2000:] + [act[4]]
+    got = tok.encode_batch(docs)
+    assert got == rc.encode_batch(docs)
+    assert tok.last_stats is None or tok.last_stats.get("nfc_docs", 0) >= 5
+    ids, toff = tok.encode_packed(*corpus.pack([d.encode() for d in docs]), timing=True)
+    assert tok.last_stats["nfc_docs"] >= 5
+    assert_same(ids, toff, *rc.encode_packed(*corpus.pack([d.encode() for d in docs])))
+    only = [act[1], act[4], act[0]]  # every doc flagged
+    assert tok.encode_batch(only) == rc.encode_batch(only)
 
 
 def test_from_tables_encodes_like_from_file(gpt2_path):
