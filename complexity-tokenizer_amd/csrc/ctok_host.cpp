@@ -227,6 +227,7 @@ struct DeviceState {
   DevBuf<uint32_t> spl_rank, spl_ids, sub_ids;
   DevBuf<uint64_t> spl_pos, spl_toff, sub_off, sub_toff;
   DevBuf<uint8_t> sub_text;
+  DevBuf<uint32_t> nfc_bits;  // k_segment's NFC word flags (speculative passes)
   DevBuf<uint64_t> norm_off;
   DevBuf<uint8_t> norm_text;
   bool last_norm = false;  // the last encode ran on norm_text / norm_off (last_B bytes)
@@ -255,7 +256,7 @@ struct DeviceState {
     add(wpref), add(long_cnt), add(long_ord), add(long_hist), add(long_pos), add(lw_pos), add(lwn), add(long_list);
     add(mid_list), add(scan_tmp), add(scan_tmp2), add(cps);
     add(doc_flag), add(ncp), add(norm_off), add(norm_text);
-    add(spl_rank), add(spl_ids), add(sub_ids), add(spl_pos), add(spl_toff), add(sub_off), add(sub_toff), add(sub_text);
+    add(nfc_bits), add(spl_rank), add(spl_ids), add(sub_ids), add(spl_pos), add(spl_toff), add(sub_off), add(sub_toff), add(sub_text);
     return b;
   }
   ~DeviceState() {
@@ -1212,7 +1213,7 @@ double now_ms() {
 uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const uint64_t* d_off, uint64_t n_docs,
                        uint64_t n_bytes, uint32_t* d_ids, uint64_t ids_cap, uint64_t* d_tok_off, hipStream_t s,
                        bool timing, ctok_stats* st, bool split_added = true, bool segment_only = false,
-                       bool keep_first = false, bool no_spec = false);
+                       bool keep_first = false, bool all_nfc = false);
 
 // NFC splice: the speculative pass over the raw text finished but flagged a code point NFC may
 // change (src/normalizers.rs:45-47 normalises every document).  Only the documents holding such
@@ -1223,11 +1224,9 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
 uint64_t nfc_splice(ctok* t, DeviceState* ds, const uint8_t* d_text, const uint64_t* d_off, uint64_t n_docs,
                     uint64_t n_bytes, uint32_t* d_ids, uint64_t ids_cap, uint64_t* d_tok_off, uint64_t ntok_main,
                     hipStream_t s, uint64_t* n_flagged) {
-  const Tables& tb = ds->t;
+  (void)n_bytes;
   ds->doc_flag.ensure(n_docs + 1);
-  HIPTRY(hipMemsetAsync(ds->doc_flag.p, 0, (n_docs + 1) * 4, s));
-  HIPTRY(hipMemsetAsync(ds->counters.p + 3, 0, 4, s));
-  HIPTRY(launch_nfc_check(d_text, n_bytes, d_off, (uint32_t)n_docs, tb, ds->doc_flag.p, ds->counters.p + 3, s));
+  HIPTRY(launch_flag_docs(d_off, n_docs, ds->nfc_bits.p, ds->doc_flag.p, s));
   // ranks of the flagged docs, their places in the sub-batch
   ds->spl_rank.ensure(n_docs + 1);
   ds->spl_pos.ensure(n_docs + 1);
@@ -1257,7 +1256,7 @@ uint64_t nfc_splice(ctok* t, DeviceState* ds, const uint8_t* d_text, const uint6
   ds->sub_ids.ensure(ctok_ids_bound(t, SB, F));
   ds->sub_toff.ensure(F + 1);
   encode_device(t, ds, ds->sub_text.p, ds->sub_off.p, F, SB, ds->sub_ids.p, ds->sub_ids.cap, ds->sub_toff.p, s, false,
-                nullptr, true, false, false, true);
+                nullptr, true, false, false, true);  // (all_nfc: every doc of the sub-batch is normalised)
   ds->scan_tmp.ensure(scan_tmp_elems(n_docs + 1) + 64);
   HIPTRY(launch_splice(ds->spl_rank.p, ds->spl_toff.p, ds->spl_ids.p, ds->sub_toff.p, ds->sub_ids.p, n_docs, d_ids,
                        ids_cap, d_tok_off, ds->scan_tmp.p, ds->scan_tmp.cap, s));
@@ -1269,7 +1268,7 @@ uint64_t nfc_splice(ctok* t, DeviceState* ds, const uint8_t* d_text, const uint6
 // The pipeline on device-resident buffers.  Returns the token count.
 uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const uint64_t* d_off, uint64_t n_docs,
                        uint64_t n_bytes, uint32_t* d_ids, uint64_t ids_cap, uint64_t* d_tok_off, hipStream_t s,
-                       bool timing, ctok_stats* st, bool split_added, bool segment_only, bool keep_first, bool no_spec) {
+                       bool timing, ctok_stats* st, bool split_added, bool segment_only, bool keep_first, bool all_nfc) {
   if (n_bytes >= 0xF0000000ull) throw_err(CTOK_E_ARG, "a single call is limited to < 3.75 GiB of text; split the batch");
   if (n_docs >= 0xF0000000ull) throw_err(CTOK_E_ARG, "too many documents in one call");
   // split_added = false: encode_to_encoding's words go straight to BpeTokenizer::encode, with
@@ -1281,7 +1280,9 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   // let k_segment flag any code point that NFC might change (NFC_QC != Yes or a non-zero
   // combining class; ASCII never is).  Only a flagged batch pays for the check + normalise
   // passes and a second run.
-  bool speculate = t->nfc && !t->add_prefix_space && n_bytes && !no_spec && !getenv("CTOK_NO_NFC_SPECULATION");
+  // all_nfc (nfc_splice's sub-batch of flagged docs): no speculation and no check, every doc is
+  // normalised
+  bool speculate = t->nfc && !t->add_prefix_space && n_bytes && !all_nfc && !getenv("CTOK_NO_NFC_SPECULATION");
   // a flagged pass is finished and only its flagged docs are encoded again (nfc_splice), except
   // where the whole batch's pass state is read afterwards (offsets, the trainer's pre-tokenizer)
   const bool splice = d_ids && !keep_first && !segment_only && !getenv("CTOK_NFC_RERUN");
@@ -1298,7 +1299,12 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   uint64_t B = n_bytes;
   uint64_t nfc_docs = 0;
   bool norm = t->add_prefix_space;
-  if (t->nfc && n_bytes && !speculate) {
+  if (t->nfc && n_bytes && all_nfc) {
+    ds->doc_flag.ensure(n_docs + 1);
+    HIPTRY(hipMemsetD32Async((hipDeviceptr_t)ds->doc_flag.p, 1, n_docs + 1, s));
+    nfc_docs = n_docs;
+    norm = true;
+  } else if (t->nfc && n_bytes && !speculate) {
     ds->doc_flag.ensure(n_docs + 1);
     HIPTRY(hipMemsetAsync(ds->doc_flag.p, 0, (n_docs + 1) * 4, s));
     STEP("nfc_check", launch_nfc_check(d_text, n_bytes, d_off, (uint32_t)n_docs, tb, ds->doc_flag.p, ds->counters.p + 3, s));
@@ -1342,6 +1348,12 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   w.n_tiles = (uint32_t)((B + kTile - 1) / kTile);
   w.n_cus = ds->n_cus;
   w.nfc_watch = speculate ? (splice ? 2u : 1u) : 0u;
+  if (w.nfc_watch == 2) {
+    const uint64_t nw32 = (B + 2047) / 2048 + 8;
+    ds->nfc_bits.ensure(nw32);
+    HIPTRY(hipMemsetAsync(ds->nfc_bits.p, 0, nw32 * 4, s));
+    w.nfc_bits = ds->nfc_bits.p;
+  }
   w.keep_first = keep_first ? 1u : 0u;
   const size_t nt = w.n_tiles;
   ds->docbits.ensure(w.n_words + 8);

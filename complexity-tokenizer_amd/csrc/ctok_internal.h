@@ -201,6 +201,8 @@ struct Work {              // device pointers, sized by the host for one call
   uint32_t nfc_watch;      // 1, 2: the text was not NFC-checked; k_segment sets counters[12] on a
                            // code point NFC might change; 1: the later passes then stop (the call
                            // runs again normalised), 2: they finish (the flagged docs are spliced)
+  uint32_t* nfc_bits;      // nfc_watch: bit g set when 64-byte word g holds the start of a code point
+                           // NFC might change (zeroed by the host; nfc_splice flags docs from it)
   uint32_t keep_first;     // 1: k_emit leaves every piece's first id within its tile in tcnt (not
                            // only doc-start pieces'), for ctok_encode_offsets
   uint16_t* wpref;         // [n_tiles * 64] pieces of the tile before each 64-byte word
@@ -339,6 +341,7 @@ uint64_t scan_tmp_elems(uint64_t n_max);
 hipError_t shift_u64(uint64_t* p, uint64_t n, uint64_t delta, hipStream_t s);  // p[0, n) += delta
 // NFC splice (see kernels.hip): len[d] = flagged doc d's bytes (else 0); flagged docs' bytes
 // gathered to the sub-batch; the output's counts, offsets (out_off[0..n_docs]) and ids
+hipError_t launch_flag_docs(const uint64_t* off, uint64_t n_docs, const uint32_t* nfc_bits, uint32_t* flag, hipStream_t s);
 hipError_t launch_flag_len(const uint64_t* off, const uint32_t* flag, uint64_t n_docs, uint64_t* len, hipStream_t s);
 hipError_t launch_gather_flagged(const uint8_t* text, const uint64_t* off, const uint32_t* rank, const uint64_t* sub_pos,
                                  uint64_t n_docs, uint8_t* sub_text, uint64_t* sub_off, hipStream_t s);

@@ -481,7 +481,10 @@ __global__ __launch_bounds__(64 * kSegWaves) void k_segment(Work w, Tables t) {
         set_class(cl, bits);
       }
     }
-    if (nfc_bad && w.nfc_watch) atomicOr(&w.counters[12], 1u);
+    if (nfc_bad && w.nfc_watch) {
+      atomicOr(&w.counters[12], 1u);
+      if (w.nfc_watch == 2 && g >= 0) atomicOr(&w.nfc_bits[g >> 5], 1u << (g & 31));  // (splice mode only)
+    }
   }
   // contraction letters only where an apostrophe could use them (this word's or the previous
   // word's last two bytes)
@@ -2730,6 +2733,27 @@ hipError_t scan_u64(uint64_t* inout, uint64_t n, uint64_t* tmp, uint64_t tmp_cap
 // sub-batch, and their ids replace the speculative pass's in the output.  rank[d] = flagged docs
 // before d (exclusive scan of the NFC-check flags; doc d is flagged when rank[d + 1] > rank[d]).
 
+// flag[d] = 1 when a 64-byte word overlapping doc d holds the start of a code point NFC might
+// change (k_segment's nfc_bits; a word shared with a neighbour flags both docs: a superset, and
+// NFC leaves an unflagged doc unchanged, so encoding it normalised gives the same ids)
+__global__ __launch_bounds__(256) void k_flag_docs(const uint64_t* __restrict__ off, uint64_t n_docs,
+                                                   const uint32_t* __restrict__ bits, uint32_t* __restrict__ flag) {
+  for (uint64_t d = (uint64_t)blockIdx.x * 256 + threadIdx.x; d < n_docs; d += (uint64_t)gridDim.x * 256) {
+    const uint64_t a = off[d], b = off[d + 1];
+    uint32_t f = 0;
+    if (b > a) {
+      const uint64_t g0 = a >> 6, g1 = (b - 1) >> 6;  // words [g0, g1]
+      for (uint64_t q = g0 >> 5; q <= (g1 >> 5) && !f; q++) {
+        uint32_t m = bits[q];
+        if (q == (g0 >> 5)) m &= ~0u << (g0 & 31);
+        if (q == (g1 >> 5)) m &= (g1 & 31) == 31 ? ~0u : (2u << (g1 & 31)) - 1u;
+        f = m != 0;
+      }
+    }
+    flag[d] = f;
+  }
+}
+
 // len[d] = bytes of doc d if it is flagged, else 0 (scanned to the sub-batch offsets)
 __global__ __launch_bounds__(256) void k_flag_len(const uint64_t* __restrict__ off, const uint32_t* __restrict__ flag,
                                                   uint64_t n_docs, uint64_t* __restrict__ len) {
@@ -2779,8 +2803,14 @@ __global__ __launch_bounds__(256) void k_splice_copy(const uint32_t* __restrict_
   }
 }
 
-static uint32_t grid_for(uint64_t threads) {
-  return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((threads + 255) / 256, 16384));
+static uint32_t grid_for(uint64_t threads, uint64_t max_blocks = 16384) {
+  return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((threads + 255) / 256, max_blocks));
+}
+
+hipError_t launch_flag_docs(const uint64_t* off, uint64_t n_docs, const uint32_t* nfc_bits, uint32_t* flag, hipStream_t s) {
+  if (!n_docs) return hipSuccess;
+  k_flag_docs<<<grid_for(n_docs), 256, 0, s>>>(off, n_docs, nfc_bits, flag);
+  return hipGetLastError();
 }
 
 hipError_t launch_flag_len(const uint64_t* off, const uint32_t* flag, uint64_t n_docs, uint64_t* len, hipStream_t s) {
@@ -2792,7 +2822,7 @@ hipError_t launch_flag_len(const uint64_t* off, const uint32_t* flag, uint64_t n
 hipError_t launch_gather_flagged(const uint8_t* text, const uint64_t* off, const uint32_t* rank, const uint64_t* sub_pos,
                                  uint64_t n_docs, uint8_t* sub_text, uint64_t* sub_off, hipStream_t s) {
   if (!n_docs) return hipSuccess;
-  k_gather_flagged<<<grid_for(64 * n_docs), 256, 0, s>>>(text, off, rank, sub_pos, n_docs, sub_text, sub_off);
+  k_gather_flagged<<<grid_for(64 * n_docs, 1u << 20), 256, 0, s>>>(text, off, rank, sub_pos, n_docs, sub_text, sub_off);
   return hipGetLastError();
 }
 
@@ -2805,7 +2835,7 @@ hipError_t launch_splice(const uint32_t* rank, const uint64_t* main_off, const u
   if (e != hipSuccess) return e;
   e = scan_u64(out_off, n_docs, tmp, tmp_cap, s);
   if (e != hipSuccess) return e;
-  k_splice_copy<<<grid_for(64 * n_docs), 256, 0, s>>>(rank, main_off, main_ids, sub_off, sub_ids, out_off, n_docs, ids, ids_cap);
+  k_splice_copy<<<grid_for(64 * n_docs, 1u << 20), 256, 0, s>>>(rank, main_off, main_ids, sub_off, sub_ids, out_off, n_docs, ids, ids_cap);
   return hipGetLastError();
 }
 
@@ -2987,51 +3017,95 @@ __device__ uint32_t nfc_reorder_compose(const Tables& t, uint32_t* buf, uint32_t
   return comp;
 }
 
-// NFC of s[0, n) into buf (capacity 4n code points); returns the code point count.  A code point
+__device__ __forceinline__ uint32_t u8size(uint32_t cp) { return cp < 0x80 ? 1 : cp < 0x800 ? 2 : cp < 0x10000 ? 3 : 4; }
+
+// NFC of s[0, n) into buf (capacity 4n code points) by one wavefront; returns the code point
+// count, *len_out its UTF-8 bytes, *first_out the first code point (0 if none).  A code point
 // with nfc16 == 0 (ccc 0 and NFC_QC Yes) is a normalisation boundary: nothing after it combines
 // with anything before it, and it is unchanged unless a following code point combines with it.
 // So only the segments around unstable code points are normalised -- from the boundary before
-// the first (popped back from the output) to the next boundary -- and everything else is copied:
-// the decomposition / composition table searches run for a few code points of a document, not for
-// all of them.  Output in buf[0 ..) (<= 1.5 n code points), segment workspace in buf[2n ..).
-__device__ uint32_t nfc_doc(const Tables& t, const uint8_t* s, uint32_t n, uint32_t* buf) {
+// the first (popped back from the output) to the next boundary -- and everything else is copied.
+// The wave walks the document in 64-byte windows: every lane decodes the code point starting at
+// its byte and looks up its nfc16 (one round of loads per window instead of one per code point),
+// the stable code points before the window's first unstable one are appended together, and lane
+// 0 normalises the segment there (decomposition / composition table searches for a few code
+// points).  Segment workspace in buf[2n ..).
+__device__ uint32_t nfc_doc(const Tables& t, const uint8_t* s, uint32_t n, uint32_t* buf, uint64_t* len_out,
+                            uint32_t* first_out) {
+  const uint32_t lane = threadIdx.x & 63;
   uint32_t* tmp = buf + 2 * (size_t)n;
-  uint32_t k = 0;
-  bool last_boundary = false;  // buf[k - 1] is a boundary code point copied through
+  uint32_t k = 0, first = 0, last = 0;  // wave-uniform: output count, first / last output code point
+  uint64_t len = 0;
+  bool lb = false;  // the last output code point is a boundary copied through
   for (uint32_t i = 0; i < n;) {
-    uint32_t cp;
-    const int len = dev_decode(s, n, i, &cp);
-    if (nfc16(t, cp) == 0) {
-      buf[k++] = cp;
-      last_boundary = true;
-      i += len;
+    const uint32_t p = i + lane;
+    uint32_t cp = 0;
+    bool st = false, un = false;
+    if (p < n) {
+      st = (s[p] & 0xC0) != 0x80;
+      if (st) {
+        dev_decode(s, n, p, &cp);
+        un = nfc16(t, cp) != 0;
+      }
+    }
+    const uint64_t S = __ballot(st), U = __ballot(st && un);
+    const uint64_t keep = U ? S & ((1ull << __builtin_ctzll(U)) - 1ull) : S;  // stable, before the first unstable
+    const bool mine = (keep >> lane) & 1ull;
+    if (mine) buf[k + __popcll(keep & lanemask_lt())] = cp;
+    if (keep) {
+      if (k == 0) first = __builtin_amdgcn_readlane(cp, __builtin_ctzll(keep));
+      last = __builtin_amdgcn_readlane(cp, 63 - __builtin_clzll(keep));
+      k += (uint32_t)__popcll(keep);
+      len += wave_sum_full_u32(mine ? u8size(cp) : 0u);  // (phase 1 writes u8size bytes per code point)
+      lb = true;
+    }
+    if (!U) {
+      i += 64;
       continue;
     }
-    uint32_t m = 0;
-    if (last_boundary) m = nfc_decompose(t, buf[--k], tmp);  // the segment starts at the boundary before
-    while (i < n) {
-      uint32_t c;
-      const int l = dev_decode(s, n, i, &c);
-      if (nfc16(t, c) == 0) break;  // the next boundary ends the segment
-      m += nfc_decompose(t, c, tmp + m);
-      i += l;
+    uint32_t j = i + (uint32_t)__builtin_ctzll(U);
+    if (lane == 0) {
+      uint32_t m = 0;
+      if (lb) {  // the boundary before joins the segment
+        k--;
+        len -= u8size(last);
+        m = nfc_decompose(t, last, tmp);
+      }
+      while (j < n) {
+        uint32_t c;
+        const int ll = dev_decode(s, n, j, &c);
+        if (nfc16(t, c) == 0) break;  // the next boundary ends the segment
+        m += nfc_decompose(t, c, tmp + m);
+        j += ll;
+      }
+      m = nfc_reorder_compose(t, tmp, m);
+      if (k == 0 && m) first = tmp[0];
+      for (uint32_t q = 0; q < m; q++) {
+        buf[k++] = tmp[q];
+        len += u8size(tmp[q]);
+      }
+      if (m) last = tmp[m - 1];
     }
-    m = nfc_reorder_compose(t, tmp, m);
-    for (uint32_t j = 0; j < m; j++) buf[k++] = tmp[j];
-    last_boundary = false;
+    k = __builtin_amdgcn_readlane(k, 0);
+    j = __builtin_amdgcn_readlane(j, 0);
+    first = __builtin_amdgcn_readlane(first, 0);
+    last = __builtin_amdgcn_readlane(last, 0);
+    len = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(len >> 32), 0) << 32) | __builtin_amdgcn_readlane((uint32_t)len, 0);
+    lb = false;
+    i = j;
   }
+  *len_out = len;
+  *first_out = k ? first : 0u;
   return k;
 }
 
-__device__ __forceinline__ uint32_t u8size(uint32_t cp) { return cp < 0x80 ? 1 : cp < 0x800 ? 2 : cp < 0x10000 ? 3 : 4; }
 
 // phase 0: new_len[d] = normalised length (flagged docs: NFC code points left in cp_scratch)
 // phase 1: write the normalised text at new_off[d] (new_len scanned into offsets)
 // Normalisation (NFC of the flagged documents, optional prefix space), a wavefront per
 // document: phase 0 sizes each output document, phase 1 (after a scan) writes it.  An unflagged
 // document is copied by the whole wave (consecutive lanes, consecutive bytes); a flagged one is
-// decomposed / reordered / composed by lane 0 (nfc_doc), rare by construction (the host runs
-// this only when some code point NFC might change occurs).
+// normalised by the wave (nfc_doc) into code points, which phase 1 writes as UTF-8.
 constexpr int kNormWaves = 4;
 
 __global__ __launch_bounds__(64 * kNormWaves) void k_norm(const uint8_t* __restrict__ text,
@@ -3047,34 +3121,41 @@ __global__ __launch_bounds__(64 * kNormWaves) void k_norm(const uint8_t* __restr
   const bool flagged = nfc && uni(doc_flag[d]) != 0;
   uint32_t* buf = cp_scratch + 4 * a;
   if (phase == 0) {
-    if (lane != 0) return;
     uint64_t len;
     uint32_t first;
     if (flagged) {
-      const uint32_t k = nfc_doc(t, text + a, n, buf);
-      ncp[d] = k;
-      len = 0;
-      for (uint32_t i = 0; i < k; i++) len += u8size(buf[i]);
-      first = k ? buf[0] : 0;
+      const uint32_t k = nfc_doc(t, text + a, n, buf, &len, &first);
+      if (lane == 0) ncp[d] = k;
     } else {
       len = n;
       first = n ? text[a] : 0;
     }
     if (add_prefix && len > 0 && first != ' ') len += 1;  // src/pretokenizers.rs:163-167
-    newv[d] = len;
+    if (lane == 0) newv[d] = len;
     return;
   }
   uint8_t* o = out + newv[d];
-  if (flagged) {
-    if (lane != 0) return;
+  if (flagged) {  // the code points as UTF-8: a wave scan of their sizes places each lane's bytes
     const uint32_t k = ncp[d];
-    if (add_prefix && k > 0 && buf[0] != ' ') *o++ = ' ';
-    for (uint32_t i = 0; i < k; i++) {
-      const uint32_t c = buf[i];
-      if (c < 0x80) { *o++ = (uint8_t)c; }
-      else if (c < 0x800) { *o++ = (uint8_t)(0xC0 | (c >> 6)); *o++ = (uint8_t)(0x80 | (c & 0x3F)); }
-      else if (c < 0x10000) { *o++ = (uint8_t)(0xE0 | (c >> 12)); *o++ = (uint8_t)(0x80 | ((c >> 6) & 0x3F)); *o++ = (uint8_t)(0x80 | (c & 0x3F)); }
-      else { *o++ = (uint8_t)(0xF0 | (c >> 18)); *o++ = (uint8_t)(0x80 | ((c >> 12) & 0x3F)); *o++ = (uint8_t)(0x80 | ((c >> 6) & 0x3F)); *o++ = (uint8_t)(0x80 | (c & 0x3F)); }
+    const uint32_t pre = (add_prefix && k > 0 && buf[0] != ' ') ? 1u : 0u;
+    if (pre && lane == 0) o[0] = ' ';
+    uint64_t pos = pre;
+    for (uint32_t q0 = 0; q0 < k; q0 += 64) {
+      const uint32_t q = q0 + lane;
+      const uint32_t c = q < k ? buf[q] : 0u, sz = q < k ? u8size(c) : 0u;
+      const uint32_t inc = wave_incl_scan(sz);
+      uint8_t* w8 = o + pos + (inc - sz);
+      if (sz == 1) {
+        w8[0] = (uint8_t)c;
+      } else if (sz == 2) {
+        w8[0] = (uint8_t)(0xC0 | (c >> 6)); w8[1] = (uint8_t)(0x80 | (c & 0x3F));
+      } else if (sz == 3) {
+        w8[0] = (uint8_t)(0xE0 | (c >> 12)); w8[1] = (uint8_t)(0x80 | ((c >> 6) & 0x3F)); w8[2] = (uint8_t)(0x80 | (c & 0x3F));
+      } else if (sz == 4) {
+        w8[0] = (uint8_t)(0xF0 | (c >> 18)); w8[1] = (uint8_t)(0x80 | ((c >> 12) & 0x3F));
+        w8[2] = (uint8_t)(0x80 | ((c >> 6) & 0x3F)); w8[3] = (uint8_t)(0x80 | (c & 0x3F));
+      }
+      pos += lane63(inc);
     }
     return;
   }

@@ -129,7 +129,8 @@ typedef struct ctok_stats {
   double ms_h2d, ms_d2h;  /* host-buffer copies (ctok_encode_batch only)               */
   uint64_t bytes_in;      /* raw UTF-8 bytes of the batch                              */
   uint64_t bytes_norm;    /* bytes after normalisation / prefix space                  */
-  uint64_t docs, pieces, long_pieces, tokens, nfc_docs;
+  uint64_t docs, pieces, long_pieces, tokens, nfc_docs;  /* nfc_docs: documents NFC-normalised (a superset
+                                                          of those NFC changes: flagged per 64-byte word) */
   double ms_segment;      /* k_segment alone: piece starts + whole-piece probes/routing */
   double ms_bpe_lo;       /* k_bpe_short: pieces of <= 16 bytes (classes 0 and 1)        */
   double ms_bpe_hi;       /* k_bpe_mid<2>: pieces of 17..32 bytes                        */

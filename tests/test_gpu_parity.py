@@ -349,7 +349,10 @@ def test_nfc_speculation_redo(gpt2):
         got = tok.encode_batch(docs)
         want = rc.encode_batch(docs)
         assert got == want, "batch with tail %r differs" % tail
-        assert tok.last_stats is None or tok.last_stats.get("nfc_docs", 0) == (1 if tail else 0)
+        # (nfc_docs: the docs normalised again; flags are per 64-byte word, so the doc sharing the
+        # tail's first word is re-encoded too -- a superset, with the same ids)
+        n = 0 if tok.last_stats is None else tok.last_stats.get("nfc_docs", 0)
+        assert (1 <= n <= 2) if tail else n == 0
 
 
 @pytest.mark.parametrize("mode", ["splice", "rerun"])
