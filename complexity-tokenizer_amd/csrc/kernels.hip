@@ -2117,7 +2117,8 @@ __device__ uint32_t bpe_wave_seg(const Tables& t, const PairLds& P, const int32_
     bool chain = false;
     if (sites) chain = tok[first] == tok[nxt[first]];
     const bool eager = serial_round(t, r);
-    if (eager && __ballot(chain) != 0) {
+    const bool chain_any = __ballot(chain) != 0;
+    if (eager && chain_any) {
       const uint32_t lm = uni(wave_min_full_u32(first));
       sites = first == lm ? (sites & (~sites + 1)) : 0ull;  // the leftmost site only
     } else if (eager) {
@@ -2180,6 +2181,66 @@ __device__ uint32_t bpe_wave_seg(const Tables& t, const PairLds& P, const int32_
         rest &= rest - 1;
       }
     };
+    // One pass (the common round: every site holds a pair (a, b) with a != b, all of them merge,
+    // and no lane holds more than kB): the new pairs' tokens are read from the state before the
+    // merges -- a site's right pair is (nid, the token after its right neighbour, nid when that
+    // is a site itself), its left pair (the token before it, or nid with the site before that
+    // when that one merges into it) -- so their lookups, global loads included, are in flight
+    // while the merges are written, instead of after a second walk of the list.
+    if (!eager && !chain_any && __ballot(__popcll(sites) > (uint32_t)kB) == 0) {
+      uint32_t p[kB], q[kB], pp[kB], nq[kB], ppp[kB], tpp[kB], rnq[kB], tnq[kB], rppp[kB];
+      uint64_t rest = sites;
+      take(rest, p);
+#pragma unroll
+      for (int i = 0; i < kB; i++) {
+        q[i] = p[i] != kNone ? (uint32_t)nxt[p[i]] : kNoPos;
+        pp[i] = p[i] != kNone ? (uint32_t)prv[p[i]] : kNoPos;
+      }
+#pragma unroll
+      for (int i = 0; i < kB; i++) {
+        nq[i] = q[i] != kNoPos ? (uint32_t)nxt[q[i]] : kNoPos;
+        ppp[i] = pp[i] != kNoPos ? (uint32_t)prv[pp[i]] : kNoPos;
+        tpp[i] = pp[i] != kNoPos ? (uint32_t)tok[pp[i]] : 0u;
+      }
+#pragma unroll
+      for (int i = 0; i < kB; i++) {
+        rnq[i] = nq[i] != kNoPos ? (uint32_t)rk[nq[i]] : kNoRank;
+        tnq[i] = nq[i] != kNoPos ? (uint32_t)tok[nq[i]] : 0u;
+        rppp[i] = ppp[i] != kNoPos ? (uint32_t)rk[ppp[i]] : kNoRank;
+      }
+      Probe<false, HOT> R[kB], L[kB];
+      uint32_t lpos[kB];
+#pragma unroll
+      for (int i = 0; i < kB; i++) {
+        const bool left_site = rppp[i] == r;  // (rank r: a site, which takes pp in)
+        lpos[i] = left_site ? ppp[i] : pp[i];
+        R[i].start(t, P, nid, rnq[i] == r ? nid : tnq[i], p[i] != kNone && nq[i] != kNoPos);
+        L[i].start(t, P, left_site ? nid : tpp[i], nid, p[i] != kNone && pp[i] != kNoPos);
+      }
+#pragma unroll
+      for (int i = 0; i < kB; i++) {
+        if (p[i] == kNone) continue;
+        tok[p[i]] = nid;
+        tok[q[i]] = kDead;
+        rk[q[i]] = kNoRank;
+        nxt[p[i]] = (uint16_t)nq[i];
+        if (nq[i] != kNoPos) prv[nq[i]] = (uint16_t)p[i];
+        dirty[unit(q[i])] = 1;
+      }
+#pragma unroll
+      for (int i = 0; i < kB; i++) {
+        if (p[i] == kNone) continue;
+        const uint32_t rr = R[i].finish(t, err), rl = L[i].finish(t, err);
+        rk[p[i]] = nq[i] != kNoPos ? rr : kNoRank;
+        dirty[unit(p[i])] = 1;
+        if (pp[i] != kNoPos) {
+          rk[lpos[i]] = rl;
+          dirty[unit(lpos[i])] = 1;
+        }
+      }
+      wave_sync_lds();
+      continue;
+    }
     // phase A: every selected site merges with its right neighbour
     for (uint64_t rest = sites; rest;) {
       uint32_t p[kB], q[kB], nq[kB];
