@@ -2250,7 +2250,7 @@ int ctok_encode_batch(const ctok* tc, const uint8_t* utf8_in, const uint64_t* do
     const uint64_t chunk = (uint64_t)(exec && exec->chunk_mb ? exec->chunk_mb : 64u) << 20;
     const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
     const unsigned nthr = exec && exec->host_threads ? exec->host_threads
-                                                     : std::max(1u, std::min(8u, hw / (2u * (unsigned)devs.size())));
+                                                     : std::max(1u, std::min(16u, hw / (unsigned)devs.size()));  // (widening threads: t4 / t8 / t16 = 5.4 / 5.6 / 5.0 ms on C2, profiles/r03/v22_e2e_probe.txt)
     if (stats) *stats = ctok_stats{};
     // shards: contiguous doc ranges balanced by bytes (cut at the first doc start >= k * B / G)
     const size_t G = devs.size();

@@ -19,6 +19,6 @@ for i in 1 2 3; do
 import json
 d=json.loads(open('$OUT/v$k.$i.json').read().strip().splitlines()[-1])
 k=d['roofline']['kernels']; p=d['pipeline']
-print('v$k.$i', '$(basename $lib)', d['value'], ' '.join('%s=%.4f'%(n,v['ms']) for n,v in k.items()), 'dev=%.4f'%p['ms_device'], 'ws=%s' % p.get('workspace_B_per_byte'))" | tee -a "$OUT/ab.txt"
+print('v$k.$i', '$(basename $lib)', d['value'], ' '.join('%s=%.4f'%(n,v['ms']) for n,v in k.items()), 'dev=%.4f'%p['ms_device'], 'ws=%s' % p.get('workspace_B_per_byte'), str(d.get('parity'))[:24])" | tee -a "$OUT/ab.txt"
   done
 done
