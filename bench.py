@@ -190,6 +190,9 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
 
     import torch
+    # torch only holds device buffers here: one intra-op CPU thread, so its spinning pool does not
+    # take the cgroup's CPUs from the CPU baseline's threads (tools/bench_matrix.py, same reason)
+    torch.set_num_threads(1)
     dist = None
     if world > 1:
         import torch.distributed as dist

@@ -252,6 +252,11 @@ def main():
     args = ap.parse_args()
     os.environ.setdefault("RAYON_NUM_THREADS", str(args.threads))
     import torch
+    # torch is here only for device buffers: its intra-op CPU pool (OMP_NUM_THREADS = 16 on the
+    # box) spins after CPU tensor ops and takes the cgroup's CPU share from the host-buffer
+    # pipeline's widening threads and from the Python leg (C2 E2E 20.7 vs 24.3 GB/s, Python
+    # 170 vs 364 MB/s, profiles/r03/v25_matrix_omp.txt); a tokenizer-only process has no such pool
+    torch.set_num_threads(1)
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     # measured HBM stream peak: device-to-device copy of 2 GiB (reads + writes)
@@ -271,6 +276,7 @@ def main():
     torch.cuda.empty_cache()
     rows = []
     meta = {"gpu": torch.cuda.get_device_name(0), "cpu_model": cpu_model(), "cpu_threads_used": args.threads,
+            "torch_intraop_threads": torch.get_num_threads(),
             "d2d_copy_GBps": round(copy_gbps, 1), "hbm_spec_GBps": 8000.0}
     log("[matrix] meta", meta)
     for c in args.configs.split(","):
