@@ -552,7 +552,8 @@ void parse_pre_tokenizer(const ctj::Value* v, std::vector<std::pair<char, bool>>
       if (r && r->kind == ctj::Value::String) pat = r->s;
     }
     if (rust_regex_compiles(pat))
-      throw_err(CTOK_E_UNSUPPORTED, "Split pre-tokenizer with a pattern the Rust regex crate compiles is outside the encode hot path");
+      throw_err(CTOK_E_UNSUPPORTED, "Split pre-tokenizer with a pattern the Rust regex crate compiles is outside the "
+                                    "encode hot path (pattern: " + pat + ")");
     chain.push_back({'S', false});
   } else if (ty == "Sequence" && depth == 0) {
     const ctj::Value* ps = v->get("pretokenizers");
@@ -2250,7 +2251,7 @@ int ctok_encode_batch(const ctok* tc, const uint8_t* utf8_in, const uint64_t* do
     const uint64_t chunk = (uint64_t)(exec && exec->chunk_mb ? exec->chunk_mb : 64u) << 20;
     const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
     const unsigned nthr = exec && exec->host_threads ? exec->host_threads
-                                                     : std::max(1u, std::min(16u, hw / (unsigned)devs.size()));  // (widening threads: t4 / t8 / t16 = 5.4 / 5.6 / 5.0 ms on C2, profiles/r03/v22_e2e_probe.txt)
+                                                     : std::max(1u, std::min(8u, hw / (unsigned)devs.size()));  // (widening threads: 4 / 8 / 16 within run-to-run noise on C2, profiles/r03/v22_e2e_probe.txt, v27_*; 8 + the pipeline threads stay inside a 16-CPU quota)
     if (stats) *stats = ctok_stats{};
     // shards: contiguous doc ranges balanced by bytes (cut at the first doc start >= k * B / G)
     const size_t G = devs.size();

@@ -186,7 +186,7 @@ def test_split_pattern_compilability(pattern, compiles):
         split, {"type": "ByteLevel", "use_regex": False}]})
     assert ref_py.rust_regex_compiles(pattern) == compiles
     if compiles:
-        with pytest.raises(UnsupportedConfigError):
+        with pytest.raises(UnsupportedConfigError, match="pattern: "):  # (the refusal names the pattern)
             Tokenizer.from_str(json.dumps(obj))
     else:
         Tokenizer.from_str(json.dumps(obj))

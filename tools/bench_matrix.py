@@ -28,6 +28,9 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "complexity-tokenizer_amd")]
+# one OpenMP thread for torch / numpy (before they load): their pools spin after CPU work and take
+# the cgroup's CPU share from the host-buffer pipeline's threads (see main)
+os.environ["OMP_NUM_THREADS"] = "1"
 
 import numpy as np  # noqa: E402
 

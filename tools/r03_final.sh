@@ -31,7 +31,7 @@ if [ "$STEP" = all ] || [ "$STEP" = prof ]; then
   cat "$OUT/pmc_traffic.log"
 fi
 if [ "$STEP" = all ] || [ "$STEP" = matrix ]; then
-  timeout -k 10 900 python -u tools/bench_matrix.py --configs c1,c2,c3,c5,c5nfc --out "$OUT/matrix.json" > "$OUT/matrix.log" 2>&1 || { tail -30 "$OUT/matrix.log"; exit 1; }
+  timeout -k 10 900 python -u tools/bench_matrix.py --configs c1,c2,c3,c3tt,c5,c5nfc --out "$OUT/matrix.json" > "$OUT/matrix.log" 2>&1 || { tail -30 "$OUT/matrix.log"; exit 1; }
   grep "\[matrix\]" "$OUT/matrix.log" | grep done
 fi
 echo "r03_final $STEP done"
