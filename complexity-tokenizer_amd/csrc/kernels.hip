@@ -355,7 +355,10 @@ __device__ __forceinline__ uint32_t select_bit(uint64_t x, uint32_t k) {
 //     one whole-piece probe; every other piece is appended to its tile's class list (<= 8 B,
 //     9..16 B, 17..32 B) or to the long list, so that the merge passes run dense, length-uniform
 //     waves.
-__global__ __launch_bounds__(64 * kSegWaves) void k_segment(Work w, Tables t) {
+// (amdgpu_waves_per_eu(7): at most 72 VGPRs, 7 waves per SIMD; without it the compiler takes 72-73
+// and this kernel runs at 6-7; C4 k_segment 2.78 -> 2.67 ms, 8 waves spill: 2.96 ms,
+// profiles/r03/v30_ab_seg_waves_per_eu.txt)
+__global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(7))) void k_segment(Work w, Tables t) {
   __shared__ uint16_t s_pos_all[kSegWaves][64 * kSegUnroll + 8];  // one round's piece starts
   __shared__ uint32_t s_text_all[kSegWaves][(kTileWords + 1) * 16 + 4];  // the tile + look-ahead word
   __shared__ uint64_t s_D_all[kSegWaves][64];  // doc starts per word (piece records carry kRecDoc)
