@@ -168,8 +168,9 @@ class Tokenizer:
 
     def __del__(self):
         h = getattr(self, "_h", None)
-        if h is not None and h.value:
-            _n.lib.ctok_destroy(h)
+        lib = getattr(_n, "lib", None) if _n is not None else None  # (None at interpreter teardown)
+        if h is not None and h.value and lib is not None:
+            lib.ctok_destroy(h)
             self._h = None
 
     # ------------------------------------------------------------------ constructors

@@ -207,7 +207,7 @@ struct DeviceState {
   DevBuf<uint64_t> merge_tab, lds_image, lds16_image, merge16;
   DevBuf<uint32_t> pair0;
   DevBuf<uint32_t> piece_tab;
-  DevBuf<uint32_t> rank_newid, eager;
+  DevBuf<uint32_t> rank_newid, eager, wmeta;
   DevBuf<int32_t> byte2id;
   DevBuf<uint8_t> cls_s1, cls_s2, nfc_s1, alnum, at_bytes, at_flags;
   DevBuf<uint16_t> nfc_s2, decomp_off;
@@ -309,6 +309,8 @@ struct ctok {
   uint32_t piece_mask = 0;
   std::vector<uint32_t> rank_newid;
   std::vector<uint32_t> eager_bits;  // bit v: the merge of table value v is eager (see Tables::eager)
+  std::vector<uint32_t> wmeta;       // window rounds (Tables::wmeta): per id, max left | max right << 16
+  bool window = false;               // window rounds exact for this table (see Tables::window)
   int32_t byte2id[256];
   std::string at_bytes;
   std::vector<uint32_t> at_off{0}, at_id;
@@ -912,6 +914,48 @@ void load_root(ctok* t, const ctj::Value& root) {
   }
 
 
+  // window rounds of the segmented long-piece tier (Tables::window, kernels.hip bpe_wave_seg):
+  // exact when the table is rank-monotone and every token instance spans exactly its string's
+  // length -- each byte's initial token is one char, and every merge that can apply makes the
+  // token its two sides spell (no rank shift from an invalid merge before it, src/bpe.rs:60-69).
+  // Per id: the longest left side of a merge whose right side it is, and the longest right side
+  // of a merge whose left side it is (chars = bytes; 0xFFFF when longer).
+  {
+    auto nchars = [&](uint32_t id, bool& ok) -> uint32_t {
+      auto it = t->id_to_token.find(id);
+      if (it == t->id_to_token.end()) { ok = false; return 0; }
+      uint32_t c = 0;
+      for (unsigned char ch : it->second) c += (ch & 0xC0) != 0x80;
+      return c;
+    };
+    bool ok = t->proper && !getenv("CTOK_NO_WINDOW");
+    for (int b = 0; b < 256 && ok; b++)
+      if (t->byte2id[b] >= 0 && nchars((uint32_t)t->byte2id[b], ok) != 1) ok = false;
+    uint32_t max_id = 0;
+    for (const auto& kv : t->vocab) max_id = std::max(max_id, kv.second);
+    std::vector<uint32_t> ml, mr;
+    if (ok) {
+      ml.assign((size_t)max_id + 1, 0);
+      mr.assign((size_t)max_id + 1, 0);
+    }
+    for (const auto& kv : ranks) {
+      if (!ok) break;
+      const uint32_t r = kv.second;
+      if (r >= valid_new.size()) continue;  // panics when looked up: never merges
+      const uint32_t a = (uint32_t)(kv.first >> 32), b = (uint32_t)kv.first;
+      const uint32_t la = nchars(a, ok), lb = nchars(b, ok), lz = nchars(valid_new[r], ok);
+      if (!ok || lz != la + lb || a > max_id || b > max_id) { ok = false; break; }
+      ml[b] = std::max(ml[b], la);
+      mr[a] = std::max(mr[a], lb);
+    }
+    t->window = ok;
+    if (ok) {
+      t->wmeta.resize((size_t)max_id + 1);
+      for (size_t i = 0; i <= max_id; i++) t->wmeta[i] = std::min(ml[i], 0xFFFFu) | std::min(mr[i], 0xFFFFu) << 16;
+    }
+  }
+  lap("window");
+
   // byte-pair table: the merge-table value of (byte2id[a], byte2id[b]) for every byte pair a, b
   // (the initial pairs of every piece are byte pairs), kNoRank where the pair has no merge
   t->pair0.assign(65536, kNoRank);
@@ -1123,6 +1167,7 @@ DeviceState* device_state(ctok* t, int device) {
   upload(ds->pair0, t->pair0.data(), t->pair0.size(), s);
   upload(ds->rank_newid, t->rank_newid.data(), t->rank_newid.size(), s);
   upload(ds->eager, t->eager_bits.data(), t->eager_bits.size(), s);
+  if (t->window) upload(ds->wmeta, t->wmeta.data(), t->wmeta.size(), s);
   upload(ds->piece_tab, t->piece_tab.data(), t->piece_tab.size(), s);
   upload(ds->byte2id, t->byte2id, 256, s);
   upload(ds->cls_s1, ct_cls_stage1, sizeof(ct_cls_stage1), s);
@@ -1152,6 +1197,8 @@ DeviceState* device_state(ctok* t, int device) {
   tb.piece_mask = t->piece_mask;
   tb.rank_newid = ds->rank_newid.p;
   tb.eager = ds->eager.p;
+  tb.wmeta = ds->wmeta.p;
+  tb.window = t->window ? 1 : 0;
   tb.n_ranks = (uint32_t)t->rank_newid.size();
   tb.byte2id = ds->byte2id.p;
   tb.cls_s1 = ds->cls_s1.p;

@@ -183,6 +183,11 @@ struct Tables {            // device pointers, owned by the host runtime
                             // A round of a non-eager merge applies all its occurrences at once:
                             // every pair the round makes ranks after it, so the sequential loop
                             // also applies them all, left to right, before any other merge.
+  uint32_t window;          // 1: window rounds are exact (proper table, every token spans its string's
+                            // length): the segmented tier also merges, in the same round, any pair
+                            // ranked below every other pair of its window (kernels.hip bpe_wave_seg)
+  const uint32_t* wmeta;    // window: per id, the longest left side of a merge it is the right side of
+                            // (bits 0-15) and the longest right side of one it is the left side of
   uint32_t compact;         // 1: entry values are new ids (strictly increasing in rank), else ranks
   uint32_t narrow;          // 1: every vocab id < 2^16 (the merge passes keep the last tier's tokens as u16 in LDS)
   uint32_t dbg;             // debug mode (CTOK_DBG_MODE), 0 in production

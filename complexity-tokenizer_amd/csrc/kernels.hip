@@ -2003,8 +2003,9 @@ __device__ uint32_t bpe_wave_dense(const Tables& t, const PairLds& P, const int3
 template <int K>
 struct SegSlice {  // per-wave LDS slice for up to 64K positions
   static constexpr uint32_t C = 64 * K;
-  static constexpr uint32_t kBytes = 13 * C + 256;
-  lds_u32* base;  // tok[C] | rk[C] | nxt[C] u16 | prv[C] u16 | sel[C] u8 | dirty[256] u8 (per group)
+  static constexpr uint32_t kBytes = 13 * C + 256 + 1024;
+  lds_u32* base;  // tok[C] | rk[C] | nxt[C] u16 | prv[C] u16 | sel[C] u8 | dirty[256] u8 (per group) |
+                  // gmin[256] u32 (per group: its minimum rank, window rounds)
   __device__ __forceinline__ lds_u32* tok() const { return base; }
   __device__ __forceinline__ lds_u32* rk() const { return base + C; }
   __device__ __forceinline__ __attribute__((address_space(3))) uint16_t* nxt() const {
@@ -2015,6 +2016,7 @@ struct SegSlice {  // per-wave LDS slice for up to 64K positions
     return (__attribute__((address_space(3))) uint8_t*)(prv() + C);
   }
   __device__ __forceinline__ __attribute__((address_space(3))) uint8_t* dirty() const { return sel() + C; }
+  __device__ __forceinline__ lds_u32* gmin() const { return (lds_u32*)(dirty() + 256); }
 };
 
 constexpr uint32_t kNoPos = 0xFFFFu;
@@ -2172,6 +2174,78 @@ __device__ uint32_t bpe_wave_seg(const Tables& t, const PairLds& P, const int32_
       }
       sites = keep;
     }
+    // Window rounds (t.window: a rank-monotone table -- every pair a merge makes ranks after it --
+    // whose token instances span exactly their strings' lengths).  Besides the sites of the
+    // round's rank r, a pair c = (x, y) of rank rc > r merges now when no other pair starting in
+    // its window [c - left(x), end(y) + right(y)) ranks <= rc, left(x) / right(y) being the
+    // longest left / right side of any merge with x on the right / y on the left (Tables::wmeta).
+    // Exact: the sequential loop (src/bpe.rs:88-153) takes merges in non-decreasing rank order,
+    // so before c it can only touch x or y by merging some u into (u, x) or (y, v) at a rank <
+    // rc; u (v) spans at most left(x) (right(y)) positions next to c, and the first merge
+    // building it was a pair of today's tokens inside that span ranked below rc -- which the
+    // window excludes.  So c is the first merge that touches x or y, and applying it now leaves
+    // the rest of the sequence unchanged (every pair it makes ranks above rc).  Checked at group
+    // granularity: c must be its group's only minimum, and every other group the window
+    // overlaps must have a larger minimum (gmin, published here each round); a window over more
+    // than kWinGroups groups is not checked.  Random-letter 4 KiB runs (C3): ~820 rounds -> ~30.
+    uint64_t bsites = 0;
+    if (t.window) {
+      constexpr uint32_t kWinGroups = 16;
+      lds_u32* gmin = S.gmin();
+#pragma unroll
+      for (int g = 0; g < 4; g++) gmin[4 * lane + g] = gm[g];
+      uint32_t cp[4], cb[4];
+#pragma unroll
+      for (int g = 0; g < 4; g++) {
+        cp[g] = kNone;
+        cb[g] = 0;
+        if (gm[g] != kNoRank && gm[g] != r) {
+          uint32_t eq = 0;
+#pragma unroll
+          for (int k = 0; k < (int)R; k++) eq |= (uint32_t)(v[g * R + k] == gm[g]) << k;
+          if (__popc(eq) == 1) {
+            const uint32_t k = (uint32_t)__builtin_ctz(eq);
+            cb[g] = g * R + k;
+            cp[g] = a0 + g * G + k;
+          }
+        }
+      }
+      wave_sync_lds();
+      uint32_t q[4], tc[4], tq[4], nq[4];
+#pragma unroll
+      for (int g = 0; g < 4; g++) {
+        q[g] = cp[g] != kNone ? (uint32_t)nxt[cp[g]] : kNoPos;
+        tc[g] = cp[g] != kNone ? (uint32_t)tok[cp[g]] : 0u;
+      }
+#pragma unroll
+      for (int g = 0; g < 4; g++) {
+        tq[g] = q[g] != kNoPos ? (uint32_t)tok[q[g]] : 0u;
+        nq[g] = q[g] != kNoPos ? (uint32_t)nxt[q[g]] : kNoPos;
+      }
+      uint32_t wl[4], wr[4];
+#pragma unroll
+      for (int g = 0; g < 4; g++) {
+        wl[g] = q[g] != kNoPos ? (t.wmeta[tc[g]] & 0xFFFFu) : 0u;
+        wr[g] = q[g] != kNoPos ? (t.wmeta[tq[g]] >> 16) : 0u;
+      }
+#pragma unroll
+      for (int g = 0; g < 4; g++) {
+        if (q[g] == kNoPos) continue;
+        const uint32_t c = cp[g];
+        const uint32_t lo = c >= wl[g] ? c - wl[g] : 0u;
+        const uint32_t end = min((nq[g] == kNoPos ? m : nq[g]) + wr[g], m);
+        const uint32_t h0 = unit(lo), h1 = unit(end - 1), own = unit(c);
+        if (h1 - h0 >= kWinGroups) continue;
+        bool ok = true;
+        for (uint32_t h = h0; h <= h1; h++)
+          if (h != own && (uint32_t)gmin[h] <= gm[g]) {
+            ok = false;
+            break;
+          }
+        if (ok) bsites |= 1ull << cb[g];
+      }
+      sites |= bsites;
+    }
     // A lane's sites go four at a time, the LDS reads (and in phase B the pair lookups, global
     // loads included) of the four in flight together: no read of a phase depends on a write of
     // the same phase (a site's right neighbour q is never a site; the left neighbour pp of a site
@@ -2190,7 +2264,7 @@ __device__ uint32_t bpe_wave_seg(const Tables& t, const PairLds& P, const int32_
     // is a site itself), its left pair (the token before it, or nid with the site before that
     // when that one merges into it) -- so their lookups, global loads included, are in flight
     // while the merges are written, instead of after a second walk of the list.
-    if (!eager && !chain_any && __ballot(__popcll(sites) > (uint32_t)kB) == 0) {
+    if (!eager && !chain_any && __ballot(__popcll(sites) > (uint32_t)kB || bsites != 0) == 0) {
       uint32_t p[kB], q[kB], pp[kB], nq[kB], ppp[kB], tpp[kB], rnq[kB], tnq[kB], rppp[kB];
       uint64_t rest = sites;
       take(rest, p);
@@ -2244,18 +2318,27 @@ __device__ uint32_t bpe_wave_seg(const Tables& t, const PairLds& P, const int32_
       wave_sync_lds();
       continue;
     }
-    // phase A: every selected site merges with its right neighbour
+    // phase A: every selected site merges with its right neighbour (window rounds: each site
+    // with its own rank's new id; no site is another site's right neighbour, whose rank this
+    // phase overwrites)
     for (uint64_t rest = sites; rest;) {
-      uint32_t p[kB], q[kB], nq[kB];
+      uint32_t p[kB], q[kB], nq[kB], np[kB];
       take(rest, p);
 #pragma unroll
-      for (int i = 0; i < kB; i++) q[i] = p[i] != kNone ? (uint32_t)nxt[p[i]] : kNoPos;
+      for (int i = 0; i < kB; i++) {
+        q[i] = p[i] != kNone ? (uint32_t)nxt[p[i]] : kNoPos;
+        np[i] = nid;
+        if (t.window && p[i] != kNone) np[i] = (uint32_t)rk[p[i]];
+      }
 #pragma unroll
-      for (int i = 0; i < kB; i++) nq[i] = p[i] != kNone ? (uint32_t)nxt[q[i]] : kNoPos;
+      for (int i = 0; i < kB; i++) {
+        nq[i] = p[i] != kNone ? (uint32_t)nxt[q[i]] : kNoPos;
+        if (t.window && p[i] != kNone) np[i] = new_id_of(t, np[i]);
+      }
 #pragma unroll
       for (int i = 0; i < kB; i++) {
         if (p[i] == kNone) continue;
-        tok[p[i]] = nid;
+        tok[p[i]] = np[i];
         tok[q[i]] = kDead;
         rk[q[i]] = kNoRank;
         nxt[p[i]] = (uint16_t)nq[i];
@@ -2267,12 +2350,14 @@ __device__ uint32_t bpe_wave_seg(const Tables& t, const PairLds& P, const int32_
     // phase B: the new pairs' ranks.  When the left neighbour pp is itself a site, its right-pair
     // lookup and this site's left-pair lookup are the same pair (nid, nid) and write the same rank.
     for (uint64_t rest = sites; rest;) {
-      uint32_t p[kB], q[kB], pp[kB], tq[kB], tp[kB];
+      uint32_t p[kB], q[kB], pp[kB], tq[kB], tp[kB], ts[kB];
       take(rest, p);
 #pragma unroll
       for (int i = 0; i < kB; i++) {
         q[i] = p[i] != kNone ? (uint32_t)nxt[p[i]] : kNoPos;
         pp[i] = p[i] != kNone ? (uint32_t)prv[p[i]] : kNoPos;
+        ts[i] = nid;
+        if (t.window && p[i] != kNone) ts[i] = (uint32_t)tok[p[i]];
       }
 #pragma unroll
       for (int i = 0; i < kB; i++) {
@@ -2282,8 +2367,8 @@ __device__ uint32_t bpe_wave_seg(const Tables& t, const PairLds& P, const int32_
       Probe<false, HOT> R[kB], L[kB];
 #pragma unroll
       for (int i = 0; i < kB; i++) {
-        R[i].start(t, P, nid, tq[i], q[i] != kNoPos);
-        L[i].start(t, P, tp[i], nid, pp[i] != kNoPos);
+        R[i].start(t, P, ts[i], tq[i], q[i] != kNoPos);
+        L[i].start(t, P, tp[i], ts[i], pp[i] != kNoPos);
       }
 #pragma unroll
       for (int i = 0; i < kB; i++) {

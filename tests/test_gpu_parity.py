@@ -169,6 +169,43 @@ def test_c3_tiktoken_layout_full_corpus(llama3_tt_path):
     assert tok.last_stats["long_pieces"] >= 1000  # (the 1% of docs with a 1-4 KiB run)
 
 
+@pytest.mark.parametrize("seed", range(6))
+def test_window_rounds_random_proper(seed):
+    """Window rounds of the segmented tiers (kernels.hip bpe_wave_seg, Tables::window) on random
+    rank-monotone tables with tokens up to 8..23 letters (wide windows, model and CPU check in
+    tests/test_window_rule.py): pieces of 2-3 letters at every tier's lengths, against the C
+    oracle; the same table with an invalid merge in front (window rounds off) too."""
+    alpha = b"abc"[: 2 + seed % 2]
+    obj = toys.random_proper(seed, alphabet=alpha.decode(), max_len=8 + 3 * seed)
+    rng = np.random.default_rng(seed)
+    docs = []
+    for n in [40, 200, 257, 300, 700, 1024, 1025, 1500, 2500, 4000, 4096, 5000]:
+        for _ in range(3):
+            docs.append(b"x " + bytes(rng.choice(list(alpha), size=n).astype(np.uint8)) + b" y")
+    text, off = corpus.pack(docs)
+    for o in (obj, toys.with_invalid_merges(obj, seed=seed, n_bad=3)):
+        tok, rc = gpu_tok(o), ref_c.RefC(o)
+        ids, toff = tok.encode_packed(text, off)
+        assert_same(ids, toff, *rc.encode_packed(text, off))
+
+
+def test_c3_full_corpus(llama3_path):
+    """C3 (100k docs, 76 MB, 1% with 1-4 KiB runs of letters, digits, words or one repeated
+    letter) with the rank-monotone Llama-3-shaped fixture, whose long pieces take the window
+    rounds, against the C oracle's digest (tests/golden/digests.json C3)."""
+    import hashlib
+    gold = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "digests.json")))["C3"]
+    tok = Tokenizer.from_file(llama3_path)
+    text, off = corpus.corpus_c3()
+    assert int(off[-1]) == gold["bytes"]
+    ids, toff = tok.encode_packed(text, off, timing=True)
+    h = hashlib.sha256()
+    h.update(np.ascontiguousarray(toff, dtype="<u8").tobytes())
+    h.update(np.ascontiguousarray(ids, dtype="<u4").tobytes())
+    assert len(ids) == gold["tokens"]
+    assert h.hexdigest() == gold["sha256"]
+
+
 def test_eager_cascade_rounds():
     """toys.eager_cascade: after an "a b" merges, ("ab", "a") ranks below ("a", "b"), so a round
     of that merge must stop at its first site whose new pairs rank lower (kernels.hip

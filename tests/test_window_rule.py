@@ -1,0 +1,54 @@
+"""The window rounds of the segmented long-piece tier (kernels.hip bpe_wave_seg) restated in
+Python (tests/window_model.py) against the reference's sequential merge loop (oracle/ref_py.py,
+src/bpe.rs:88-153): random rank-monotone tables with long tokens (wide windows), the Llama-3-shaped
+fixture on C3-like runs, and the round counts that make the rule worth it."""
+import json
+
+import numpy as np
+import pytest
+
+from oracle.ref_py import RefTokenizer
+from tests import toys
+from tests.window_model import window_bpe, window_meta
+
+
+def _ids(tok, data: bytes):
+    be = toys.byte_chars()
+    return [tok.vocab[be[b]] for b in data if be[b] in tok.vocab]
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_window_rounds_random_proper_tables(seed):
+    tok = RefTokenizer(toys.random_proper(seed, alphabet="abc"[: 2 + seed % 2], max_len=8 + 3 * seed))
+    assert window_meta(tok) is not None
+    rng = np.random.default_rng(seed)
+    for n in [2, 5, 17, 64, 130, 300, 700]:
+        for _ in range(3):
+            data = bytes(rng.choice(list(b"abc"[: 2 + seed % 2]), size=n).astype(np.uint8))
+            ids = _ids(tok, data)
+            for k in (16, 64):
+                got, _ = window_bpe(tok, ids, k=k)
+                assert got == tok.bpe("".join(toys.byte_chars()[b] for b in data)), (seed, n, k)
+
+
+def test_window_meta_refuses_shifted_ranks():
+    """An invalid merge before valid ones shifts the new ids (src/bpe.rs:60-69): a merged token
+    need not spell its two sides, so the window bound does not hold and the rule is off."""
+    obj = toys.with_invalid_merges(toys.random_proper(1), seed=3, n_bad=5)
+    assert window_meta(RefTokenizer(obj)) is None
+
+
+def test_window_rounds_llama3_runs(llama3_path):
+    with open(llama3_path) as f:
+        tok = RefTokenizer(json.load(f))
+    rng = np.random.default_rng(3)
+    words = [w for w in (tok.id_to_token_map[i] for i in range(300, 8000)) if w.isalpha()][:3000]
+    runs = [bytes(rng.integers(ord("a"), ord("z") + 1, size=1200).astype(np.uint8)),
+            bytes(rng.integers(ord("0"), ord("9") + 1, size=1200).astype(np.uint8)),
+            "".join(words[int(i)] for i in rng.integers(len(words), size=400)).encode()[:1200],
+            b"q" * 1200]
+    for data in runs:
+        ids = _ids(tok, data)
+        got, rounds = window_bpe(tok, ids, k=64)
+        assert got == tok.bpe("".join(toys.byte_chars()[b] for b in data))
+        assert rounds < 60  # (rank rounds alone: ~300-400 on the first three)

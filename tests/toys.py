@@ -79,3 +79,31 @@ def eager_cascade():
         vocab[t] = len(vocab)
     merges = [("ab", "a"), ("a", "b"), ("b", "a"), ("c", "c"), ("cc", "cc"), ("ab", "ab"), ("ab", "c")]
     return tok_json(vocab, merges)
+
+
+def random_proper(seed, alphabet="abc", n_merges=80, max_len=24):
+    """A random rank-monotone table over a few letters (every merge's token exists before any merge
+    consumes it is ranked, and no token is produced after one consuming it): the tables for which
+    the segmented tier's window rounds apply (kernels.hip bpe_wave_seg, Tables::window).  Long
+    tokens make wide windows; the whole byte alphabet is in the vocab."""
+    rng = random.Random(seed)
+    chars = byte_chars()
+    vocab = {c: i for i, c in enumerate(chars)}
+    toks = [chars[ord(a)] for a in alphabet]
+    merges, seen, consumed = [], set(), set()
+    tries = 0
+    while len(merges) < n_merges and tries < 50 * n_merges:
+        tries += 1
+        # bias towards recent (longer) tokens so that windows get wide
+        x = toks[min(len(toks) - 1, int(rng.expovariate(0.15) if rng.random() < 0.5 else rng.randrange(len(toks))))]
+        y = rng.choice(toks) if rng.random() < 0.7 else toks[-1 - rng.randrange(min(4, len(toks)))]
+        z = x + y
+        if len(z) > max_len or (x, y) in seen or (z in vocab and z in consumed):
+            continue
+        seen.add((x, y))
+        merges.append((x, y))
+        consumed.update((x, y))
+        if z not in vocab:
+            vocab[z] = len(vocab)
+            toks.append(z)
+    return tok_json(vocab, merges)

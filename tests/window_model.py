@@ -1,0 +1,88 @@
+"""Python model of the segmented long-piece tier's window rounds (kernels.hip bpe_wave_seg,
+Tables::window) -- test infrastructure: tests/test_window_rule.py checks it against the
+sequential merge loop of the reference (oracle/ref_py.py RefTokenizer.bpe, src/bpe.rs:88-153).
+
+A round: r = the lowest rank of any pair; every site of r merges ((x, x) runs: the 1st, 3rd, ...
+site), and so does the pair c = (x, y) of rank rc > r when c is the only minimum of its group of
+positions and every other group overlapping its window [pos(c) - left(x), end(y) + right(y))
+has a larger minimum.  Positions are the initial tokens' indices (fixed: a merged token keeps its
+left position), groups are G = SW / 4 consecutive positions (SW = the per-lane segment width)."""
+
+
+def window_meta(tok):
+    """left(id) / right(id): the longest left side of a merge whose right side is id / right side
+    of a merge whose left side is id, in chars (= bytes); None when the table is not eligible."""
+    ranks, new_ids, id2s = tok.merge_ranks, tok.merge_new_ids, tok.id_to_token_map
+    left, right = {}, {}
+    for (a, b), r in ranks.items():
+        if r >= len(new_ids):
+            continue
+        if len(id2s[new_ids[r]]) != len(id2s[a]) + len(id2s[b]):
+            return None
+        left[b] = max(left.get(b, 0), len(id2s[a]))
+        right[a] = max(right.get(a, 0), len(id2s[b]))
+    return left, right
+
+
+def seg_width(m, k):
+    return min(k, (((m + 63) // 64) + 15) & ~15)
+
+
+def window_bpe(tok, ids, k=64, max_groups=16):
+    """The window rounds on one piece's initial ids; returns (ids, rounds)."""
+    INF = 1 << 62
+    left, right = window_meta(tok)
+    ranks, new_ids = tok.merge_ranks, tok.merge_new_ids
+    m = len(ids)
+    g_w = seg_width(m, k) // 4
+    t, pos = list(ids), list(range(m))
+    rounds = 0
+    while True:
+        n = len(t)
+        rk = [ranks.get((t[i], t[i + 1]), INF) for i in range(n - 1)]
+        if not rk or min(rk) == INF:
+            return t, rounds
+        rounds += 1
+        r = min(rk)
+        fire = [False] * (n - 1)
+        i = 0
+        while i < n - 1:
+            if rk[i] == r:
+                j = i
+                while j + 1 < n - 1 and rk[j + 1] == r:
+                    j += 1
+                for q in range(i, j + 1, 2):
+                    fire[q] = True
+                i = j + 1
+            else:
+                i += 1
+        n_groups = (m + g_w - 1) // g_w
+        gmin, gcnt, garg = [INF] * n_groups, [0] * n_groups, [None] * n_groups
+        for i in range(n - 1):
+            g = pos[i] // g_w
+            if rk[i] < gmin[g]:
+                gmin[g], gcnt[g], garg[g] = rk[i], 1, i
+            elif rk[i] == gmin[g]:
+                gcnt[g] += 1
+        for g in range(n_groups):
+            if gmin[g] in (INF, r) or gcnt[g] != 1:
+                continue
+            i = garg[g]
+            lo = max(0, pos[i] - left.get(t[i], 0))
+            end = min((pos[i + 2] if i + 2 < n else m) + right.get(t[i + 1], 0), m)
+            h0, h1 = lo // g_w, (end - 1) // g_w
+            if h1 - h0 >= max_groups:
+                continue
+            if all(gmin[h] > rk[i] for h in range(h0, h1 + 1) if h != g):
+                fire[i] = True
+        nt, npos, i = [], [], 0
+        while i < n:
+            if i < n - 1 and fire[i]:
+                nt.append(new_ids[rk[i]])
+                npos.append(pos[i])
+                i += 2
+            else:
+                nt.append(t[i])
+                npos.append(pos[i])
+                i += 1
+        t, pos = nt, npos
