@@ -1958,9 +1958,30 @@ __device__ uint32_t bpe_wave_dense(const Tables& t, const PairLds& P, const int3
       for (uint32_t p = lane; p < m; p += 64) sel[p] = chg[p];
       wave_sync_lds();
     }
-    // in-place compaction: a site's right neighbour is dropped, the site takes nid.  Position p
-    // moves to q <= p; a step reads its 64 positions before it writes, and later steps read only
-    // positions past every q written so far.
+    // window rounds (t.window, see bpe_wave_seg): a pair p of rank rc > r merges too when every
+    // other pair of its window ranks above rc.  Here the window is taken in token indices: a
+    // token spans >= 1 byte, so pairs starting within left(x) bytes before p / right(y) bytes
+    // after its right token lie within [p - left(x), p + 1 + right(y)] (a superset: exact).
+    // Only local minima are checked (both neighbour pairs lie in every window).
+    if (t.window) {
+      for (uint32_t p = lane; p + 1 < m; p += 64) {
+        const uint32_t rc = rk[p];
+        if (rc == kNoRank || rc == r || (p > 0 && (uint32_t)rk[p - 1] <= rc) || (uint32_t)rk[p + 1] <= rc) continue;
+        const uint32_t wl = t.wmeta[tok[p]] & 0xFFFFu, wr = t.wmeta[tok[p + 1]] >> 16;
+        const uint32_t a = p > wl ? p - wl : 0u, b = min(m - 2, p + 1 + wr);
+        bool fire = true;
+        for (uint32_t j = a; j <= b; j++)
+          if (j != p && (uint32_t)rk[j] <= rc) {
+            fire = false;
+            break;
+          }
+        if (fire) sel[p] = 1;
+      }
+      wave_sync_lds();
+    }
+    // in-place compaction: a site's right neighbour is dropped, the site takes its new id (nid,
+    // or in window rounds its own rank's).  Position p moves to q <= p; a step reads its 64
+    // positions before it writes, and later steps read only positions past every q written so far.
     uint32_t base = 0;
     for (uint32_t p0 = 0; p0 < m; p0 += 64) {
       const uint32_t p = p0 + lane;
@@ -1972,7 +1993,7 @@ __device__ uint32_t bpe_wave_dense(const Tables& t, const PairLds& P, const int3
       const uint64_t bal = __ballot(alive);
       if (alive) {
         const uint32_t q = base + __popcll(bal & lanemask_lt());
-        tok[q] = site ? nid : tv;
+        tok[q] = site ? (t.window ? new_id_of(t, rv) : nid) : tv;
         rk[q] = rv;
         chg[q] = site ? 1 : 0;
       }

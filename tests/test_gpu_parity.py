@@ -179,7 +179,7 @@ def test_window_rounds_random_proper(seed):
     obj = toys.random_proper(seed, alphabet=alpha.decode(), max_len=8 + 3 * seed)
     rng = np.random.default_rng(seed)
     docs = []
-    for n in [40, 200, 257, 300, 700, 1024, 1025, 1500, 2500, 4000, 4096, 5000]:
+    for n in [40, 70, 129, 200, 256, 257, 300, 700, 1024, 1025, 1500, 2500, 4000, 4096, 5000]:
         for _ in range(3):
             docs.append(b"x " + bytes(rng.choice(list(alpha), size=n).astype(np.uint8)) + b" y")
     text, off = corpus.pack(docs)

@@ -1,0 +1,39 @@
+#!/usr/bin/env python3
+"""Device-path probe for one matrix config (profiling helper for rocprofv3, not product code):
+usage probe.py CONFIG [fixture] [reps] -- e.g. probe.py c5 multi_32k 5."""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "complexity-tokenizer_amd")]
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from complexity_tokenizer import Tokenizer  # noqa: E402
+from datagen import corpus  # noqa: E402
+from datagen.build_tokenizers import fixture_path  # noqa: E402
+
+cfg = sys.argv[1].upper() if len(sys.argv) > 1 else "C3"
+fx = sys.argv[2] if len(sys.argv) > 2 else {"C3": "llama3_128k", "C5": "multi_32k", "C5NFC": "multi_32k"}.get(cfg, "gpt2_50k")
+reps = int(sys.argv[3]) if len(sys.argv) > 3 else 5
+tok = Tokenizer.from_file(fixture_path(fx, "/tmp"))
+text, off = corpus.CONFIGS[cfg]()
+nb, nd = int(off[-1]), len(off) - 1
+d_text = torch.zeros(nb + 64, dtype=torch.uint8, device="cuda")
+d_text[:nb] = torch.from_numpy(text).cuda()
+d_off = torch.from_numpy(off.astype(np.int64)).cuda()
+cap = 3 * nb + nd + 16
+d_ids = torch.empty(cap, dtype=torch.int32, device="cuda")
+d_tok = torch.empty(nd + 1, dtype=torch.int64, device="cuda")
+args = (d_text.data_ptr(), d_off.data_ptr(), nd, nb, d_ids.data_ptr(), cap, d_tok.data_ptr())
+tok.encode_packed_device(*args)
+ts = []
+for _ in range(reps):
+    t = time.perf_counter()
+    tok.encode_packed_device(*args, timing=True)
+    ts.append(time.perf_counter() - t)
+st = tok.last_stats
+print("%s %s: %d docs %d B, call %.3f ms (%.0f MB/s), device %.3f ms, long %.3f ms, long pieces %d" % (
+    cfg, fx, nd, nb, min(ts) * 1e3, nb / min(ts) / 1e6, st["ms_device"], st["ms_bpe_long"], st["long_pieces"]), flush=True)
+print({k: v for k, v in st.items() if k.startswith("ms_")}, flush=True)
