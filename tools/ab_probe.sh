@@ -1,0 +1,7 @@
+# usage: bash /tmp/abprobe.sh CFG FIX LIB_A LIB_B  (alternating probes on one box)
+set -e
+for i in 1 2 3; do
+  for L in $3 $4; do
+    CTOK_LIB=$L timeout -k 10 200 python -u tools/probe.py $1 $2 5 2>/dev/null | grep MB/s | sed "s|^|$(basename $L) |"
+  done
+done
