@@ -2054,18 +2054,30 @@ __device__ uint32_t bpe_wave_seg(const Tables& t, const PairLds& P, const int32_
   auto prv = S.prv();
   auto sel = S.sel();
   auto dirty = S.dirty();
-  // initial ids (dropped bytes compacted away); raw bytes parked in sel for the byte-pair ranks
+  // initial ids (dropped bytes compacted away); raw bytes parked in sel for the byte-pair ranks.
+  // The byte loads of 16 rows of 64 (coalesced) are issued together, then the rows are
+  // compacted: one global latency per 1 KiB instead of one per 64 bytes.
   uint32_t m = 0;
-  for (uint32_t i0 = 0; i0 < n; i0 += 64) {
-    const uint32_t i = i0 + lane;
-    const int32_t id = i < n ? s_b2id[bytes[i]] : -1;
-    const uint64_t bal = __ballot(id >= 0);
-    if (id >= 0) {
-      const uint32_t q = m + __popcll(bal & lanemask_lt());
-      tok[q] = (uint32_t)id;
-      sel[q] = bytes[i];
+  for (uint32_t j0 = 0; j0 * 64 < n; j0 += 16) {
+    uint32_t bb[16];
+    int32_t id[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      const uint32_t i = (j0 + j) * 64 + lane;
+      bb[j] = i < n ? (uint32_t)bytes[i] : 0u;
     }
-    m = uni(m + __popcll(bal));
+#pragma unroll
+    for (int j = 0; j < 16; j++) id[j] = ((j0 + j) * 64 + lane < n) ? s_b2id[bb[j]] : -1;
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      const uint64_t bal = __ballot(id[j] >= 0);
+      if (id[j] >= 0) {
+        const uint32_t q = m + __popcll(bal & lanemask_lt());
+        tok[q] = (uint32_t)id[j];
+        sel[q] = (uint8_t)bb[j];
+      }
+      m = uni(m + __popcll(bal));
+    }
   }
   wave_sync_lds();
   if (m == 0) return 0;
@@ -2079,20 +2091,25 @@ __device__ uint32_t bpe_wave_seg(const Tables& t, const PairLds& P, const int32_
   auto unit = [&](uint32_t p) { return __umulhi(p, gmag); };
   const uint32_t a0 = lane * SW;
   auto pos = [&](uint32_t b) { return a0 + (b / R) * G + (b % R); };  // site bit -> position
-  for (uint32_t k = 0; k < SW; k++) {
-    const uint32_t p = a0 + k;
-    uint32_t r = kNoRank;
-    if (p + 1 < m) {
-      r = t.pair0[((uint32_t)sel[p] << 8) | sel[p + 1]];
-      if (r != kNoRank && value_panics(t, r)) {
+  // initial pair ranks, 16 positions at a time (their byte-pair table loads in flight together)
+  for (uint32_t k0 = 0; k0 < SW; k0 += 16) {
+    uint32_t sb[17], r[16];
+#pragma unroll
+    for (int k = 0; k < 17; k++) sb[k] = a0 + k0 + k < m ? (uint32_t)sel[a0 + k0 + k] : 0u;
+#pragma unroll
+    for (int k = 0; k < 16; k++) r[k] = a0 + k0 + k + 1 < m ? t.pair0[(sb[k] << 8) | sb[k + 1]] : kNoRank;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      const uint32_t p = a0 + k0 + k;
+      if (r[k] != kNoRank && value_panics(t, r[k])) {
         atomicOr(err, kErrPanic);
-        r = kNoRank;
+        r[k] = kNoRank;
       }
-    }
-    rk[p] = r;
-    if (p < m) {
-      nxt[p] = p + 1 < m ? (uint16_t)(p + 1) : (uint16_t)kNoPos;
-      prv[p] = p > 0 ? (uint16_t)(p - 1) : (uint16_t)kNoPos;
+      rk[p] = r[k];
+      if (p < m) {
+        nxt[p] = p + 1 < m ? (uint16_t)(p + 1) : (uint16_t)kNoPos;
+        prv[p] = p > 0 ? (uint16_t)(p - 1) : (uint16_t)kNoPos;
+      }
     }
   }
   wave_sync_lds();
@@ -2407,14 +2424,21 @@ __device__ uint32_t bpe_wave_seg(const Tables& t, const PairLds& P, const int32_
     // (no per-round read of the panic flag: a panicking pair ranks as kNoRank, so the loop still
     // ends, and the host discards the batch -- a global load per round would double its latency)
   }
-  // surviving tokens in position order
+  // surviving tokens in position order (rows of 64 positions, 16 rows' LDS reads at a time)
   uint32_t c = 0;
-  for (uint32_t i0 = 0; i0 < m; i0 += 64) {
-    const uint32_t i = i0 + lane;
-    const uint32_t v = i < m ? (uint32_t)tok[i] : kDead;
-    const uint64_t bal = __ballot(v != kDead);
-    if (v != kDead) out[c + __popcll(bal & lanemask_lt())] = v;
-    c = uni(c + __popcll(bal));
+  for (uint32_t i0 = 0; i0 < m; i0 += 16 * 64) {
+    uint32_t tv[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      const uint32_t i = i0 + (uint32_t)j * 64 + lane;
+      tv[j] = i < m ? (uint32_t)tok[i] : kDead;
+    }
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      const uint64_t bal = __ballot(tv[j] != kDead);
+      if (tv[j] != kDead) out[c + __popcll(bal & lanemask_lt())] = tv[j];
+      c = uni(c + __popcll(bal));
+    }
   }
   return c;
 }
