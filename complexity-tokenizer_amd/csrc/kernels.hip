@@ -2633,9 +2633,19 @@ hipError_t launch_bpe_long(const Work& w, const Tables& t, hipStream_t s, uint32
     // The long list holds pieces > kMedMax B and pieces whose end lies past the tile's look-ahead
     // (>= 63 B: they can be shorter than kMedMax), and a tile's class-0 pieces past its list's
     // capacity, so the first tier starts at 1 B.
-    HIPCHK((launch_wave<4, 0, 4, false, false>(w, t, cap((n_long + 3) / 4, 2 * w.n_cus), s)));
+    // <= 256 B: 16 waves per workgroup, one workgroup per CU (75 KiB of LDS).  A round is a chain
+    // of LDS and global round trips, so waves per CU is the lever: C5 31.4 -> 34.5 GB/s against
+    // 4 waves x 2 workgroups per CU (which could share a CU with a wide-vocabulary merge pass;
+    // profiles/r03/v36_ab_dense_waves.txt)
+    if (t.dbg == 12) {  // A/B: the round-2 launch, 4 waves per workgroup, 2 workgroups per CU
+      HIPCHK((launch_wave<4, 0, 4, false, false>(w, t, cap((n_long + 3) / 4, 2 * w.n_cus), s)));
+    } else {
+      HIPCHK((launch_wave<4, 0, 16, false, false>(w, t, cap((n_long + 15) / 16, w.n_cus), s)));
+    }
     if (t.dbg == 10) {  // A/B: 257..1024 B four waves per CU
       HIPCHK((launch_wave<16, 256, 4, true, true>(w, t, cap((n_long + 3) / 4, w.n_cus), s)));
+    } else if (t.dbg == 15) {  // A/B: 257..1024 B, 8 waves per CU with the Bloom filter only
+      HIPCHK((launch_wave<16, 256, 8, false, true>(w, t, cap((n_long + 7) / 8, w.n_cus), s)));
     } else {
       HIPCHK((launch_wave<16, 256, 2, true, true>(w, t, cap((n_long + 1) / 2, w.n_cus), s)));
     }
