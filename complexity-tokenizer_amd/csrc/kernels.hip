@@ -954,6 +954,7 @@ typedef __attribute__((address_space(3))) uint64_t lds_u64;
 struct PairLds {
   const lds_u64* hot;  // bucket c = hot[2c], hot[2c + 1]
   const lds_u32* bloom;
+  bool no_bloom = false;  // (HOT = false) no filter in LDS: every lookup goes to the global table
 };
 
 // Rank lookup, LDS stage: the pair's value from the hot table, else kNoRank; `global` is set
@@ -962,6 +963,12 @@ struct PairLds {
 template <bool HOT>
 __device__ __forceinline__ uint32_t rank_lds(const PairLds& P, uint32_t a, uint32_t b, uint32_t h1, uint32_t h2,
                                              bool& global) {
+  if constexpr (!HOT) {
+    if (P.no_bloom) {
+      global = true;
+      return kNoRank;
+    }
+  }
   const uint32_t b1 = (h1 >> 12) & (kBloomBits - 1), b2 = (h2 >> 12) & (kBloomBits - 1);
   const uint32_t f = (P.bloom[b1 >> 5] >> (b1 & 31)) & (P.bloom[b2 >> 5] >> (b2 & 31)) & 1u;
   if constexpr (!HOT) {
@@ -2024,19 +2031,18 @@ __device__ uint32_t bpe_wave_dense(const Tables& t, const PairLds& P, const int3
 template <int K>
 struct SegSlice {  // per-wave LDS slice for up to 64K positions
   static constexpr uint32_t C = 64 * K;
-  static constexpr uint32_t kBytes = 13 * C + 256 + 1024;
-  lds_u32* base;  // tok[C] | rk[C] | nxt[C] u16 | prv[C] u16 | sel[C] u8 | dirty[256] u8 (per group) |
-                  // gmin[256] u32 (per group: its minimum rank, window rounds)
+  static constexpr uint32_t kBytes = 12 * C + 256 + 1024;
+  lds_u32* base;  // tok[C] | rk[C] | nxt[C] u16 | prv[C] u16 (the raw bytes until the list is built) |
+                  // dirty[256] u8 (per group) | gmin[256] u32 (per group: its minimum rank, window rounds)
   __device__ __forceinline__ lds_u32* tok() const { return base; }
   __device__ __forceinline__ lds_u32* rk() const { return base + C; }
   __device__ __forceinline__ __attribute__((address_space(3))) uint16_t* nxt() const {
     return (__attribute__((address_space(3))) uint16_t*)(base + 2 * C);
   }
   __device__ __forceinline__ __attribute__((address_space(3))) uint16_t* prv() const { return nxt() + C; }
-  __device__ __forceinline__ __attribute__((address_space(3))) uint8_t* sel() const {
+  __device__ __forceinline__ __attribute__((address_space(3))) uint8_t* dirty() const {
     return (__attribute__((address_space(3))) uint8_t*)(prv() + C);
   }
-  __device__ __forceinline__ __attribute__((address_space(3))) uint8_t* dirty() const { return sel() + C; }
   __device__ __forceinline__ lds_u32* gmin() const { return (lds_u32*)(dirty() + 256); }
 };
 
@@ -2052,9 +2058,9 @@ __device__ uint32_t bpe_wave_seg(const Tables& t, const PairLds& P, const int32_
   lds_u32* rk = S.rk();
   auto nxt = S.nxt();
   auto prv = S.prv();
-  auto sel = S.sel();
+  auto raw = S.prv();  // (the raw bytes, for the byte-pair ranks, until prv is built)
   auto dirty = S.dirty();
-  // initial ids (dropped bytes compacted away); raw bytes parked in sel for the byte-pair ranks.
+  // initial ids (dropped bytes compacted away); raw bytes parked in prv for the byte-pair ranks.
   // The byte loads of 16 rows of 64 (coalesced) are issued together, then the rows are
   // compacted: one global latency per 1 KiB instead of one per 64 bytes.
   uint32_t m = 0;
@@ -2074,7 +2080,7 @@ __device__ uint32_t bpe_wave_seg(const Tables& t, const PairLds& P, const int32_
       if (id[j] >= 0) {
         const uint32_t q = m + __popcll(bal & lanemask_lt());
         tok[q] = (uint32_t)id[j];
-        sel[q] = (uint8_t)bb[j];
+        raw[q] = (uint16_t)bb[j];
       }
       m = uni(m + __popcll(bal));
     }
@@ -2095,7 +2101,7 @@ __device__ uint32_t bpe_wave_seg(const Tables& t, const PairLds& P, const int32_
   for (uint32_t k0 = 0; k0 < SW; k0 += 16) {
     uint32_t sb[17], r[16];
 #pragma unroll
-    for (int k = 0; k < 17; k++) sb[k] = a0 + k0 + k < m ? (uint32_t)sel[a0 + k0 + k] : 0u;
+    for (int k = 0; k < 17; k++) sb[k] = a0 + k0 + k < m ? (uint32_t)raw[a0 + k0 + k] : 0u;
 #pragma unroll
     for (int k = 0; k < 16; k++) r[k] = a0 + k0 + k + 1 < m ? t.pair0[(sb[k] << 8) | sb[k + 1]] : kNoRank;
 #pragma unroll
@@ -2106,11 +2112,13 @@ __device__ uint32_t bpe_wave_seg(const Tables& t, const PairLds& P, const int32_
         r[k] = kNoRank;
       }
       rk[p] = r[k];
-      if (p < m) {
-        nxt[p] = p + 1 < m ? (uint16_t)(p + 1) : (uint16_t)kNoPos;
-        prv[p] = p > 0 ? (uint16_t)(p - 1) : (uint16_t)kNoPos;
-      }
+      if (p < m) nxt[p] = p + 1 < m ? (uint16_t)(p + 1) : (uint16_t)kNoPos;
     }
+  }
+  wave_sync_lds();  // (every raw byte read before prv overwrites them)
+  for (uint32_t k = 0; k < SW; k++) {
+    const uint32_t p = a0 + k;
+    if (p < m) prv[p] = p > 0 ? (uint16_t)(p - 1) : (uint16_t)kNoPos;
   }
   wave_sync_lds();
   lds_u32* dirty32 = (lds_u32*)dirty;
@@ -2513,14 +2521,14 @@ __global__ __launch_bounds__(256) void k_long_order(Work w) {
 // One wavefront per piece of (LO, 64K] bytes; NW waves per workgroup, each taking the tier's
 // pieces (a range of long_ord, longest first) from a counter.  LDS: the merge-table image (HOT:
 // hot table + Bloom filter, 96 KiB; else the Bloom filter, 32 KiB) and one slice per wave.
-template <int K, uint32_t LO, int NW, bool HOT, bool SEG>
+template <int K, uint32_t LO, int NW, bool HOT, bool SEG, bool NOB = false>
 __global__ __launch_bounds__(64 * NW) void k_bpe_wave(Work w, Tables t) {
   constexpr uint32_t kSlice = SEG ? SegSlice<K>::kBytes : WaveSlice<K>::kBytes;
   constexpr uint32_t HI = 64u * K;
   static_assert(HI <= 4096 && LO % 64 == 0 && LO < HI, "tier bounds: multiples of the 64 B buckets");
   extern __shared__ __attribute__((aligned(16))) uint4 s_dyn[];
   __shared__ int32_t s_b2id[256];
-  constexpr uint32_t kImg = HOT ? kLdsImageBytes / 16 : kBloomWords / 4;  // uint4 units
+  constexpr uint32_t kImg = NOB ? 0u : HOT ? kLdsImageBytes / 16 : kBloomWords / 4;  // uint4 units
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   const uint32_t wid = uni(tid >> 6);
   static_assert(SEG ? LO >= kDenseMax : HI <= kDenseMax, "ordered tiers: > kDenseMax B; dense tier: <= kDenseMax B");
@@ -2550,7 +2558,7 @@ __global__ __launch_bounds__(64 * NW) void k_bpe_wave(Work w, Tables t) {
   for (uint32_t i = tid; i < 256; i += 64 * NW) s_b2id[i] = t.byte2id[i];
   __syncthreads();
   const PairLds P = HOT ? PairLds{(const lds_u64*)s_dyn, (const lds_u32*)(s_dyn + kHotBuckets)}
-                        : PairLds{nullptr, (const lds_u32*)s_dyn};
+                        : PairLds{nullptr, (const lds_u32*)s_dyn, NOB};
   lds_u32* slice = (lds_u32*)((__attribute__((address_space(3))) uint8_t*)(s_dyn + kImg) + (size_t)wid * kSlice);
   uint32_t* err = &w.counters[2];
   for (uint32_t step = uni(blockIdx.x * NW + wid);; step += gridDim.x * NW) {
@@ -2585,13 +2593,13 @@ __global__ __launch_bounds__(64 * NW) void k_bpe_wave(Work w, Tables t) {
   }
 }
 
-template <int K, uint32_t LO, int NW, bool HOT, bool SEG>
+template <int K, uint32_t LO, int NW, bool HOT, bool SEG, bool NOB = false>
 static hipError_t launch_wave(const Work& w, const Tables& t, uint32_t grid, hipStream_t s) {
   static LdsAttr attr;
   const size_t slice = SEG ? SegSlice<K>::kBytes : WaveSlice<K>::kBytes;
-  const size_t lds = (HOT ? kLdsImageBytes : kBloomWords * 4) + (size_t)NW * slice;
-  HIPCHK(lds_attr_once(attr, (const void*)k_bpe_wave<K, LO, NW, HOT, SEG>, lds));
-  k_bpe_wave<K, LO, NW, HOT, SEG><<<grid, 64 * NW, lds, s>>>(w, t);
+  const size_t lds = (NOB ? 0 : HOT ? kLdsImageBytes : kBloomWords * 4) + (size_t)NW * slice;
+  HIPCHK(lds_attr_once(attr, (const void*)k_bpe_wave<K, LO, NW, HOT, SEG, NOB>, lds));
+  k_bpe_wave<K, LO, NW, HOT, SEG, NOB><<<grid, 64 * NW, lds, s>>>(w, t);
   return hipGetLastError();
 }
 
@@ -2653,6 +2661,8 @@ hipError_t launch_bpe_long(const Work& w, const Tables& t, hipStream_t s, uint32
     // with the hot table (96 + 53 KiB): C3 10.3 -> 5.25 ms (profiles/r02/v14_ab_long_tiers.txt)
     if (t.dbg == 9) {  // A/B: the hot-table variant
       HIPCHK((launch_wave<64, 1024, 1, true, true>(w, t, cap(n_long, w.n_cus), s)));
+    } else if (t.dbg == 16) {  // A/B: three waves per CU, no Bloom filter (3 x 49 KiB)
+      HIPCHK((launch_wave<64, 1024, 3, false, true, true>(w, t, cap((n_long + 2) / 3, w.n_cus), s)));
     } else {
       HIPCHK((launch_wave<64, 1024, 2, false, true>(w, t, cap((n_long + 1) / 2, w.n_cus), s)));
     }
