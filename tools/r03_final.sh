@@ -4,7 +4,7 @@
 # and the config matrix.  Every GPU step has its own time limit; the first failure ends the script.
 set -e
 export TMPDIR=/tmp
-OUT=$(pwd)/gpurun_out/r03_final
+OUT=$(pwd)/gpurun_out/${TAG:-r03_final}
 mkdir -p "$OUT"
 ROOT=$(pwd)
 STEP=${1:-all}
