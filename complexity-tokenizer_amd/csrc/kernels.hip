@@ -1843,8 +1843,8 @@ __global__ __launch_bounds__(256) void k_bpe_long(Work w, Tables t) {
 template <int K>
 struct WaveSlice {  // per-wave LDS slice: 64K positions (compacted in place every round)
   static constexpr uint32_t C = 64 * K;
-  static constexpr uint32_t kBytes = 8 * C + 2 * (C + 64);
-  lds_u32* base;  // tok | rk | chg | sel
+  static constexpr uint32_t kBytes = 8 * C + 2 * (C + 64) + 2 * C;
+  lds_u32* base;  // tok | rk | chg | sel | pos (u16: the token's first initial position, window rounds)
   __device__ __forceinline__ lds_u32* tok() const { return base; }
   __device__ __forceinline__ lds_u32* rk() const { return base + C; }
   __device__ __forceinline__ __attribute__((address_space(3))) uint8_t* chg() const {
@@ -1852,6 +1852,9 @@ struct WaveSlice {  // per-wave LDS slice: 64K positions (compacted in place eve
   }
   __device__ __forceinline__ __attribute__((address_space(3))) uint8_t* sel() const {
     return (__attribute__((address_space(3))) uint8_t*)(base + 2 * C) + C + 64;
+  }
+  __device__ __forceinline__ __attribute__((address_space(3))) uint16_t* pos() const {
+    return (__attribute__((address_space(3))) uint16_t*)(sel() + C + 64);
   }
 };
 
@@ -1882,6 +1885,7 @@ __device__ uint32_t bpe_wave_dense(const Tables& t, const PairLds& P, const int3
   lds_u32* rk = S.rk();
   auto chg = S.chg();
   auto sel = S.sel();
+  auto pos = S.pos();
   // initial ids (bytes whose char is not in the vocab are dropped: order-preserving compaction);
   // the raw bytes go to chg for the initial pair ranks
   uint32_t m = 0;
@@ -1911,7 +1915,9 @@ __device__ uint32_t bpe_wave_dense(const Tables& t, const PairLds& P, const int3
       }
     }
     rk[p] = r;
+    pos[p] = (uint16_t)p;
   }
+  const uint32_t m0 = m;  // initial positions (window rounds: token spans are in these units)
   wave_sync_lds();
   for (;;) {
     uint32_t lmin = kNoRank;
@@ -1966,22 +1972,28 @@ __device__ uint32_t bpe_wave_dense(const Tables& t, const PairLds& P, const int3
       wave_sync_lds();
     }
     // window rounds (t.window, see bpe_wave_seg): a pair p of rank rc > r merges too when every
-    // other pair of its window ranks above rc.  Here the window is taken in token indices: a
-    // token spans >= 1 byte, so pairs starting within left(x) bytes before p / right(y) bytes
-    // after its right token lie within [p - left(x), p + 1 + right(y)] (a superset: exact).
-    // Only local minima are checked (both neighbour pairs lie in every window).
+    // other pair starting in its window [pos(x) - left(x), end(y) + right(y)) ranks above rc
+    // (pos: each token's first initial position, carried through the compaction; end(y) = the
+    // next token's pos).  Only local minima are checked (both neighbour pairs lie in every
+    // window); the scans walk out from p and stop at the window's ends or the first lower pair.
     if (t.window) {
       for (uint32_t p = lane; p + 1 < m; p += 64) {
         const uint32_t rc = rk[p];
         if (rc == kNoRank || rc == r || (p > 0 && (uint32_t)rk[p - 1] <= rc) || (uint32_t)rk[p + 1] <= rc) continue;
         const uint32_t wl = t.wmeta[tok[p]] & 0xFFFFu, wr = t.wmeta[tok[p + 1]] >> 16;
-        const uint32_t a = p > wl ? p - wl : 0u, b = min(m - 2, p + 1 + wr);
+        const uint32_t p0 = pos[p];
+        const uint32_t lo = p0 > wl ? p0 - wl : 0u;
+        const uint32_t hi = (p + 2 < m ? (uint32_t)pos[p + 2] : m0) + wr;
         bool fire = true;
-        for (uint32_t j = a; j <= b; j++)
-          if (j != p && (uint32_t)rk[j] <= rc) {
-            fire = false;
-            break;
-          }
+        for (uint32_t j = p; fire && j > 0;) {
+          --j;
+          if ((uint32_t)pos[j] < lo) break;
+          fire = (uint32_t)rk[j] > rc;
+        }
+        for (uint32_t j = p + 1; fire && j + 1 < m; j++) {
+          if ((uint32_t)pos[j] >= hi) break;
+          fire = (uint32_t)rk[j] > rc;
+        }
         if (fire) sel[p] = 1;
       }
       wave_sync_lds();
@@ -1997,11 +2009,13 @@ __device__ uint32_t bpe_wave_dense(const Tables& t, const PairLds& P, const int3
       const bool dead = in && p > 0 && sel[p - 1];
       const bool alive = in && !dead;
       const uint32_t tv = in ? (uint32_t)tok[p] : 0u, rv = in ? (uint32_t)rk[p] : 0u;
+      const uint32_t pv = in ? (uint32_t)pos[p] : 0u;
       const uint64_t bal = __ballot(alive);
       if (alive) {
         const uint32_t q = base + __popcll(bal & lanemask_lt());
         tok[q] = site ? (t.window ? new_id_of(t, rv) : nid) : tv;
         rk[q] = rv;
+        pos[q] = (uint16_t)pv;
         chg[q] = site ? 1 : 0;
       }
       base = uni(base + __popcll(bal));

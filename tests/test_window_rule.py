@@ -9,7 +9,7 @@ import pytest
 
 from oracle.ref_py import RefTokenizer
 from tests import toys
-from tests.window_model import window_bpe, window_meta
+from tests.window_model import window_bpe, window_bpe_dense, window_meta
 
 
 def _ids(tok, data: bytes):
@@ -26,9 +26,11 @@ def test_window_rounds_random_proper_tables(seed):
         for _ in range(3):
             data = bytes(rng.choice(list(b"abc"[: 2 + seed % 2]), size=n).astype(np.uint8))
             ids = _ids(tok, data)
+            want = tok.bpe("".join(toys.byte_chars()[b] for b in data))
             for k in (16, 64):
                 got, _ = window_bpe(tok, ids, k=k)
-                assert got == tok.bpe("".join(toys.byte_chars()[b] for b in data)), (seed, n, k)
+                assert got == want, (seed, n, k)
+            assert window_bpe_dense(tok, ids)[0] == want, (seed, n, "dense")
 
 
 def test_window_meta_refuses_shifted_ranks():

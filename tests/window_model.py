@@ -86,3 +86,64 @@ def window_bpe(tok, ids, k=64, max_groups=16):
                 npos.append(pos[i])
                 i += 1
         t, pos = nt, npos
+
+
+def window_bpe_dense(tok, ids):
+    """The dense (<= 256 B) tier's window rounds: local minima only, the window scanned outward
+    from the pair over the tokens' first initial positions (kernels.hip bpe_wave_dense)."""
+    INF = 1 << 62
+    left, right = window_meta(tok)
+    ranks, new_ids = tok.merge_ranks, tok.merge_new_ids
+    m0 = len(ids)
+    t, pos = list(ids), list(range(m0))
+    rounds = 0
+    while True:
+        n = len(t)
+        rk = [ranks.get((t[i], t[i + 1]), INF) for i in range(n - 1)] + [INF]
+        r = min(rk)
+        if r == INF:
+            return t, rounds
+        rounds += 1
+        fire = [False] * n
+        i = 0
+        while i < n - 1:
+            if rk[i] == r:
+                j = i
+                while j + 1 < n - 1 and rk[j + 1] == r:
+                    j += 1
+                for q in range(i, j + 1, 2):
+                    fire[q] = True
+                i = j + 1
+            else:
+                i += 1
+        for p in range(n - 1):
+            rc = rk[p]
+            if rc in (INF, r) or (p > 0 and rk[p - 1] <= rc) or rk[p + 1] <= rc:
+                continue
+            lo = max(0, pos[p] - left.get(t[p], 0))
+            hi = (pos[p + 2] if p + 2 < n else m0) + right.get(t[p + 1], 0)
+            ok = True
+            j = p
+            while ok and j > 0:
+                j -= 1
+                if pos[j] < lo:
+                    break
+                ok = rk[j] > rc
+            j = p + 1
+            while ok and j + 1 < n:
+                if pos[j] >= hi:
+                    break
+                ok = rk[j] > rc
+                j += 1
+            fire[p] = fire[p] or ok
+        nt, npos, i = [], [], 0
+        while i < n:
+            if i < n - 1 and fire[i]:
+                nt.append(new_ids[rk[i]])
+                npos.append(pos[i])
+                i += 2
+            else:
+                nt.append(t[i])
+                npos.append(pos[i])
+                i += 1
+        t, pos = nt, npos
