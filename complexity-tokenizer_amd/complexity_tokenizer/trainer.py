@@ -20,18 +20,20 @@ def _raise(code):
 
 
 def _rust_lines(data: bytes, path: str):
-    """BufRead::lines (src/trainer.rs:272): split on '\\n', one trailing '\\r' dropped, UTF-8 or an
-    InvalidData io::Error (-> IOError)."""
+    """BufRead::lines (src/trainer.rs:272): split on '\\n', the '\\r' of a "\\r\\n" ending dropped (a
+    last line without '\\n' keeps its '\\r'), UTF-8 or an InvalidData io::Error (-> IOError)."""
     if not data:
         return []
     parts = data.split(b"\n")
-    if parts[-1] == b"":
-        parts.pop()
-    return [_line(p, path) for p in parts]
+    last = parts.pop()  # b"" after a trailing newline, else the unterminated last line
+    out = [_line(p, path) for p in parts]
+    if last:
+        out.append(_line(last, path, False))
+    return out
 
 
-def _line(p: bytes, path: str) -> str:
-    if p.endswith(b"\r"):
+def _line(p: bytes, path: str, newline: bool = True) -> str:
+    if newline and p.endswith(b"\r"):
         p = p[:-1]
     try:
         return p.decode("utf-8")
@@ -52,8 +54,8 @@ def _file_line_blocks(path: str, block: int):
             carry = parts.pop()  # the unfinished last line (b"" after a trailing newline)
             if parts:
                 yield [_line(p, path) for p in parts]
-        if carry:
-            yield [_line(carry, path)]
+        if carry:  # a last line without '\n' keeps a trailing '\r'
+            yield [_line(carry, path, False)]
 
 
 class Trainer:

@@ -1271,7 +1271,7 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
 // Returns the token count; *n_flagged = the flagged documents.
 uint64_t nfc_splice(ctok* t, DeviceState* ds, const uint8_t* d_text, const uint64_t* d_off, uint64_t n_docs,
                     uint64_t n_bytes, uint32_t* d_ids, uint64_t ids_cap, uint64_t* d_tok_off, uint64_t ntok_main,
-                    hipStream_t s, uint64_t* n_flagged) {
+                    hipStream_t s, uint64_t* n_flagged, bool split_added) {
   (void)n_bytes;
   ds->doc_flag.ensure(n_docs + 1);
   HIPTRY(launch_flag_docs(d_off, n_docs, ds->nfc_bits.p, ds->doc_flag.p, s));
@@ -1300,11 +1300,13 @@ uint64_t nfc_splice(ctok* t, DeviceState* ds, const uint8_t* d_text, const uint6
   ds->spl_toff.ensure(n_docs + 1);
   if (ntok_main) HIPTRY(hipMemcpyAsync(ds->spl_ids.p, d_ids, ntok_main * 4, hipMemcpyDeviceToDevice, s));
   HIPTRY(hipMemcpyAsync(ds->spl_toff.p, d_tok_off, (n_docs + 1) * 8, hipMemcpyDeviceToDevice, s));
-  // the sub-batch: NFC check + normalise + encode (no speculation: every doc in it is flagged)
+  // the sub-batch: NFC check + normalise + encode (no speculation: every doc in it is flagged),
+  // with the outer call's added-token rule (encode_to_encoding's words skip the split,
+  // src/huggingface/mod.rs:395-420)
   ds->sub_ids.ensure(ctok_ids_bound(t, SB, F));
   ds->sub_toff.ensure(F + 1);
   encode_device(t, ds, ds->sub_text.p, ds->sub_off.p, F, SB, ds->sub_ids.p, ds->sub_ids.cap, ds->sub_toff.p, s, false,
-                nullptr, true, false, false, true);  // (all_nfc: every doc of the sub-batch is normalised)
+                nullptr, split_added, false, false, true);  // (all_nfc: every doc of the sub-batch is normalised)
   ds->scan_tmp.ensure(scan_tmp_elems(n_docs + 1) + 64);
   HIPTRY(launch_splice(ds->spl_rank.p, ds->spl_toff.p, ds->spl_ids.p, ds->sub_toff.p, ds->sub_ids.p, n_docs, d_ids,
                        ids_cap, d_tok_off, ds->scan_tmp.p, ds->scan_tmp.cap, s));
@@ -1550,11 +1552,14 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
     continue;
   }
   if (w.nfc_watch == 2 && cnt[12]) {
-    if (ntok > ids_cap) {  // the pass's ids did not all fit the output: run again normalised
+    // the pass's ids did not all fit the output, or its panic flag may come from a flagged doc's
+    // raw (unnormalised) pairs, which the reference never sees (it normalises first): run again
+    // normalised
+    if (ntok > ids_cap || (cnt[2] & kErrPanic)) {
       speculate = false;
       continue;
     }
-    ntok = nfc_splice(t, ds, d_text, d_off, n_docs, n_bytes, d_ids, ids_cap, d_tok_off, ntok, s, &nfc_docs);
+    ntok = nfc_splice(t, ds, d_text, d_off, n_docs, n_bytes, d_ids, ids_cap, d_tok_off, ntok, s, &nfc_docs, split_added);
     if (timing) {
       HIPTRY(hipEventRecord(ds->ev[11], s));
       HIPTRY(hipEventSynchronize(ds->ev[11]));

@@ -362,9 +362,10 @@ _NFC_SNIPPETS = [s.encode() for s in [
     "o\u0308\u0304 ", "\u212b \u2126 ", "n\u0303o\u0303 ", "\u05e9\u05c1\u05b8 ", "\u0e01\u0e48\u0e32 "]]
 
 
-def corpus_c5nfc(n_docs: int = 1_000_000, seed: int = 5, frac: float = 0.03):
-    """C5's docs with one NFC-active snippet spliced (at a char boundary) into `frac` of them."""
-    text, off = corpus_c5(n_docs, seed)
+def corpus_c5nfc(n_docs: int = 1_000_000, seed: int = 5, frac: float = 0.03, base=None):
+    """C5's docs with one NFC-active snippet spliced (at a char boundary) into `frac` of them.
+    `base`: corpus_c5(n_docs, seed) when the caller already has it."""
+    text, off = base if base is not None else corpus_c5(n_docs, seed)
     docs = unpack(text, off)
     rng = np.random.default_rng([seed, 0x4E4643])
     pick = rng.choice(n_docs, size=max(1, int(n_docs * frac)), replace=False)

@@ -33,17 +33,19 @@ DEFAULT_SPECIALS = ["</s>", "<pad>", "<s>", "<unk>"]
 
 
 def rust_lines(data: bytes):
-    """BufRead::lines: split on b'\\n', drop one trailing b'\\r' per line, UTF-8 or error."""
+    """BufRead::lines (Rust std): split on b'\\n'; a line that ended in b'\\n' also drops one b'\\r'
+    before it, an unterminated last line keeps its b'\\r'; UTF-8 or error."""
     if not data:
         return []
     parts = data.split(b"\n")
-    if parts[-1] == b"":
-        parts.pop()
+    last = parts.pop()
     out = []
     for p in parts:
         if p.endswith(b"\r"):
             p = p[:-1]
         out.append(p.decode("utf-8"))  # UnicodeDecodeError ~ io::ErrorKind::InvalidData
+    if last:
+        out.append(last.decode("utf-8"))
     return out
 
 

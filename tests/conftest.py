@@ -19,6 +19,19 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device) -- parity tests of the HIP path")
 
 
+def pytest_collection_finish(session):
+    """A GPU session that will run the full-size digest tests (tests/test_gpu_z_full_configs.py)
+    starts building their 1M-doc corpora in background processes now, before any test touches the
+    GPU, so that they are ready when those tests (collected last) run."""
+    names = {getattr(it, "callspec", None) and it.callspec.params.get("cfg") for it in session.items
+             if it.module.__name__.endswith("test_gpu_z_full_configs")}
+    names.discard(None)
+    if names:
+        from datagen import cache
+        groups = [[n for n in ("C5", "C5NFC") if n in names or (n == "C5" and "C5NFC" in names)], ["C2"] if "C2" in names else []]
+        cache.start_background(cache.default_dir(), [g for g in groups if g])
+
+
 @pytest.fixture(scope="session")
 def fixture_dir(tmp_path_factory):
     return str(tmp_path_factory.mktemp("tokjson"))

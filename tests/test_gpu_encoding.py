@@ -279,3 +279,26 @@ def test_encode_padded_concurrent_threads(base):
     for t in th:
         t.join()
     assert not errs, errs[0]
+
+
+def test_padded_nfc_splice_keeps_no_added_split(base):
+    """encode_to_encoding's words skip the added-token split (src/huggingface/mod.rs:395-420); the
+    NFC splice re-encodes flagged docs as a sub-batch, which must keep that rule.
+    Docs hold an added token's text inside a piece beside a decomposed accent (NFC-flagged), among
+    unflagged docs; the padded rows and the plain encode (which does split) against the oracle."""
+    obj = encoding_cases.with_post_processor(base, "template")
+    nid = max(max(obj["model"]["vocab"].values()), max(a["id"] for a in obj["added_tokens"])) + 1
+    for k, content in enumerate(["hello", "ing"]):
+        obj["added_tokens"].append({"id": nid + k, "content": content, "single_word": False, "lstrip": False,
+                                    "rstrip": False, "normalized": False, "special": False})
+    tok, ref = pair_of(obj)
+    ts = ["helloé singing", "plain hello text", "xhello café thing", "", "nothing flagged here",
+          "abc éabc hellohello"] + ["filler doc %d with words" % i for i in range(50)]
+    r = tok.encode_padded(ts, padding="longest")
+    want = [ref.encode_to_encoding(t) for t in ts]
+    for i, e in enumerate(want):
+        L = int(r["row_len"][i])
+        assert r["input_ids"][i, :L].tolist() == e.ids, repr(ts[i])
+    got = tok.encode_batch_to_encoding(ts)
+    assert [g.ids for g in got] == [e.ids for e in want]
+    assert tok.encode_batch(ts) == [ref.encode(t) for t in ts]

@@ -187,6 +187,32 @@ def test_window_rounds_random_proper(seed):
         tok, rc = gpu_tok(o), ref_c.RefC(o)
         ids, toff = tok.encode_packed(text, off)
         assert_same(ids, toff, *rc.encode_packed(text, off))
+    assert len(ids) < 0.8 * len(text)  # (the table merges these runs: toys.byte_map, round 4)
+
+
+@pytest.mark.parametrize("alpha", ["日本語", "かなカ", "한국어", "日a本", "\U0001F600\U0001F601", "éßø", "中文字符"])
+def test_window_rounds_random_proper_multibyte(alpha):
+    """Window rounds on random rank-monotone tables over the UTF-8 bytes of multi-byte chars
+    (the C5 path of the dense tier's position windows, kernels.hip bpe_wave_dense): runs of 1..1500
+    random chars of the alphabet (3- and 4-byte chars: pieces at every tier, most in the <= 256 B
+    dense tier), against the C oracle; the same table with an invalid merge in front (rules off)."""
+    seed = sum(map(ord, alpha)) % 1000
+    rng = np.random.default_rng(seed)
+    chars = list(alpha)
+    obj = toys.random_proper_from_text(seed, "".join(rng.choice(chars, size=3000)).encode(), n_merges=150,
+                                       max_len=12 + seed % 9)
+    docs = []
+    for n in [1, 2, 5, 10, 15, 21, 22, 30, 40, 60, 63, 64, 70, 85, 86, 100, 200, 341, 500, 1000, 1400]:
+        for _ in range(4):
+            docs.append(b"x " + "".join(rng.choice(chars, size=n)).encode() + b" y")
+    rng.shuffle(docs)
+    text, off = corpus.pack(docs)
+    for o in (obj, toys.with_invalid_merges(obj, seed=seed, n_bad=3)):
+        tok, rc = gpu_tok(o), ref_c.RefC(o)
+        ids, toff = tok.encode_packed(text, off)
+        assert_same(ids, toff, *rc.encode_packed(text, off))
+    # the table really merges these runs (the pieces do not stay bytes)
+    assert len(ids) < 0.4 * len(text)
 
 
 def test_c3_full_corpus(llama3_path):
@@ -349,6 +375,35 @@ def test_panic_toy():
         tok.encode("ab")
     with pytest.raises(ref_py.PanicException):
         ref_py.RefTokenizer(obj).encode("ab")
+
+
+def test_nfd_only_panic_pair_does_not_panic(gpt2):
+    """A merge ranked past the valid merges (src/bpe.rs:60-69, :141 panics on it) whose pair exists
+    only in decomposed text: the reference normalises first (NFC, src/normalizers.rs:45-47) and
+    never sees it.  The speculative pass over the raw bytes does; its panic flag must not survive
+    into the result."""
+    obj, _, _ = gpt2
+    pair = (toys.byte_char(0xCC), toys.byte_char(0x81))  # the bytes of U+0301, byte-mapped: one piece of their own
+    obj = json.loads(json.dumps(obj))
+    assert "%s %s" % pair not in obj["model"]["merges"]
+    obj["model"]["vocab"][pair[0] + pair[1]] = max(obj["model"]["vocab"].values()) + 1
+    ms = list(obj["model"]["merges"]) + ["zzq%d qqz%d" % (k, k) for k in range(3)] + ["%s %s" % pair]
+    obj["model"]["merges"] = ms
+    tok, rc = gpu_tok(obj), ref_c.RefC(obj)
+    text, off = corpus.corpus_c2(2_000, seed=79)
+    docs = [d.decode() for d in corpus.unpack(text, off)]
+    docs[5] = "cafe\u0301 and re\u0301sume\u0301"
+    docs[1500] = "e\u0301" * 30
+    want = rc.encode_batch(docs)
+    assert tok.encode_batch(docs) == want
+    ids, toff = tok.encode_packed(*corpus.pack([d.encode() for d in docs]))
+    assert_same(ids, toff, *rc.encode_packed(*corpus.pack([d.encode() for d in docs])))
+    # U+0301 after a char it does not compose with survives NFC: both panic
+    for d in (docs[:10] + ["q\u0301"], ["x q\u0301 y"]):
+        with pytest.raises(ref_py.PanicException):
+            rc.encode_batch(d)
+        with pytest.raises(PanicException):
+            tok.encode_batch(d)
 
 
 def test_wide_table_mode(gpt2, monkeypatch):

@@ -72,6 +72,9 @@ def test_rust_lines():
     assert trainer_ref.rust_lines(b"a\r\nb\n\nc") == ["a", "b", "", "c"]
     assert trainer_ref.rust_lines(b"") == []
     assert trainer_ref.rust_lines(b"x\n") == ["x"]
+    # BufRead::lines drops '\r' only as part of "\r\n": an unterminated last line keeps it
+    assert trainer_ref.rust_lines(b"a\r\nb\r") == ["a", "b\r"]
+    assert trainer_ref.rust_lines(b"\r") == ["\r"]
     with pytest.raises(UnicodeDecodeError):
         trainer_ref.rust_lines(b"\xff\n")
 
@@ -120,7 +123,8 @@ def test_file_lines_streamed_in_blocks(tmp_path, block):
     """train(files) reads files in blocks: the lines must be BufRead::lines' for any block size
     (src/trainer.rs:272), including CRLF pairs and multi-byte chars cut by a block edge."""
     from complexity_tokenizer.trainer import _file_line_blocks
-    for data in (b"", b"\n", b"a\r\nb\n\nc", b"x\n", "héllo wörld\r\n日本語\n\nend".encode(), b"\r\n\r\n", b"last"):
+    for data in (b"", b"\n", b"a\r\nb\n\nc", b"x\n", "héllo wörld\r\n日本語\n\nend".encode(), b"\r\n\r\n", b"last",
+                 b"end\r", b"a\r\nb\r", b"\r"):
         p = tmp_path / "f.txt"
         p.write_bytes(data)
         got = [ln for blk in _file_line_blocks(str(p), block) for ln in blk]

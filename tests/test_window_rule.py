@@ -13,7 +13,7 @@ from tests.window_model import window_bpe, window_bpe_dense, window_meta
 
 
 def _ids(tok, data: bytes):
-    be = toys.byte_chars()
+    be = toys.byte_map()
     return [tok.vocab[be[b]] for b in data if be[b] in tok.vocab]
 
 
@@ -26,10 +26,32 @@ def test_window_rounds_random_proper_tables(seed):
         for _ in range(3):
             data = bytes(rng.choice(list(b"abc"[: 2 + seed % 2]), size=n).astype(np.uint8))
             ids = _ids(tok, data)
-            want = tok.bpe("".join(toys.byte_chars()[b] for b in data))
+            want = tok.bpe("".join(toys.byte_map()[b] for b in data))
             for k in (16, 64):
                 got, _ = window_bpe(tok, ids, k=k)
                 assert got == want, (seed, n, k)
+            assert window_bpe_dense(tok, ids)[0] == want, (seed, n, "dense")
+
+
+MULTI = ["日本語", "かなカ", "한국어", "日a本", "\U0001F600\U0001F601", "éßø"]
+
+
+@pytest.mark.parametrize("seed", range(len(MULTI)))
+def test_window_rounds_multibyte_tables(seed):
+    """The same on tables over the UTF-8 bytes of multi-byte chars (CJK / kana / Hangul / emoji /
+    Latin-1 runs: the dense tier's C5 workload), pieces of random chars."""
+    alpha = MULTI[seed]
+    rng = np.random.default_rng(seed)
+    sample = "".join(rng.choice(list(alpha), size=2000)).encode()
+    tok = RefTokenizer(toys.random_proper_from_text(seed, sample, n_merges=120, max_len=9 + 2 * seed))
+    assert window_meta(tok) is not None
+    for n in [1, 3, 9, 22, 40, 85]:
+        for _ in range(3):
+            data = "".join(rng.choice(list(alpha), size=n)).encode()
+            ids = _ids(tok, data)
+            want = tok.bpe("".join(toys.byte_map()[b] for b in data))
+            for k in (16, 64):
+                assert window_bpe(tok, ids, k=k)[0] == want, (seed, n, k)
             assert window_bpe_dense(tok, ids)[0] == want, (seed, n, "dense")
 
 
@@ -52,5 +74,5 @@ def test_window_rounds_llama3_runs(llama3_path):
     for data in runs:
         ids = _ids(tok, data)
         got, rounds = window_bpe(tok, ids, k=64)
-        assert got == tok.bpe("".join(toys.byte_chars()[b] for b in data))
+        assert got == tok.bpe("".join(toys.byte_map()[b] for b in data))
         assert rounds < 60  # (rank rounds alone: ~300-400 on the first three)

@@ -15,6 +15,18 @@ def byte_chars():
     return [chr(c) for c in cs]
 
 
+def byte_map():
+    """The GPT-2 char of every byte, indexed by byte (src/pretokenizers.rs:130-153); byte_chars()
+    lists the same chars in the table's own order (printable bytes first)."""
+    bs = list(range(0x21, 0x7F)) + list(range(0xA1, 0xAD)) + list(range(0xAE, 0x100))
+    m = dict(zip(bs + [x for x in range(256) if x not in bs], byte_chars()))
+    return [m[b] for b in range(256)]
+
+
+def byte_char(b):
+    return byte_map()[b]
+
+
 def tok_json(vocab, merges, added=(), normalizer=None, pre_tokenizer=None, merges_as_arrays=False):
     obj = {"version": "1.0", "added_tokens": list(added), "normalizer": normalizer,
            "pre_tokenizer": pre_tokenizer if pre_tokenizer is not None else
@@ -82,14 +94,16 @@ def eager_cascade():
 
 
 def random_proper(seed, alphabet="abc", n_merges=80, max_len=24):
-    """A random rank-monotone table over a few letters (every merge's token exists before any merge
+    """A random rank-monotone table over the bytes of a few letters (multi-byte chars: their UTF-8
+    bytes, merged in any grouping) (every merge's token exists before any merge
     consumes it is ranked, and no token is produced after one consuming it): the tables for which
     the segmented tier's window rounds apply (kernels.hip bpe_wave_seg, Tables::window).  Long
     tokens make wide windows; the whole byte alphabet is in the vocab."""
     rng = random.Random(seed)
     chars = byte_chars()
     vocab = {c: i for i, c in enumerate(chars)}
-    toks = [chars[ord(a)] for a in alphabet]
+    bm = byte_map()
+    toks = [bm[b] for b in dict.fromkeys(alphabet.encode())]  # the chars of the alphabet's bytes
     merges, seen, consumed = [], set(), set()
     tries = 0
     while len(merges) < n_merges and tries < 50 * n_merges:
@@ -106,4 +120,39 @@ def random_proper(seed, alphabet="abc", n_merges=80, max_len=24):
         if z not in vocab:
             vocab[z] = len(vocab)
             toks.append(z)
+    return tok_json(vocab, merges)
+
+
+def random_proper_from_text(seed, sample: bytes, n_merges=150, max_len=24):
+    """A random rank-monotone table whose merges join pairs that occur in `sample` (bytes): like a
+    BPE training run that picks a random adjacent pair of the current tokenisation instead of the
+    most frequent one.  For multi-byte alphabets, where random byte pairs rarely occur in text."""
+    rng = random.Random(seed)
+    chars = byte_chars()
+    vocab = {c: i for i, c in enumerate(chars)}
+    bm = byte_map()
+    seq = [bm[b] for b in sample]
+    merges, seen, consumed = [], set(), set()
+    tries = 0
+    while len(merges) < n_merges and tries < 50 * n_merges and len(seq) > 1:
+        tries += 1
+        i = rng.randrange(len(seq) - 1)
+        x, y = seq[i], seq[i + 1]
+        z = x + y
+        if len(z) > max_len or (x, y) in seen or z in consumed:
+            continue
+        seen.add((x, y))
+        merges.append((x, y))
+        consumed.update((x, y))
+        if z not in vocab:
+            vocab[z] = len(vocab)
+        out, j = [], 0
+        while j < len(seq):
+            if j + 1 < len(seq) and seq[j] == x and seq[j + 1] == y:
+                out.append(z)
+                j += 2
+            else:
+                out.append(seq[j])
+                j += 1
+        seq = out
     return tok_json(vocab, merges)
