@@ -111,6 +111,57 @@ def cpu_baseline(tok_path, text, off, seconds):
                       "rayon-like doc threads)" % (nn, int(off[nn]) / 1e6, dt, threads, n1)}
 
 
+def user_facing(tok, text, off, ids_dev, toff_dev, reps, py_docs):
+    """The user-facing rates of SURVEY.md 8(d), outside the headline `value`, on this rank's shard:
+    `e2e` -- ctok_encode_batch from host buffers (text up, ids and offsets down through the chunked
+    pipeline, include/ctok.h) into a reused output buffer, its result checked against the
+    device-resident run's (itself checked against the golden digest); `python` --
+    Tokenizer.encode_batch(list[str]) -> list[list[int]] (the reference's API,
+    src/bindings/tokenizer.rs:207-210) on the shard's first `py_docs` docs, checked the same way."""
+    import ctypes
+    from complexity_tokenizer import _native as _n
+    n_docs, n_bytes = len(off) - 1, int(off[-1])
+    T = int(toff_dev[-1])
+    ids = np.empty(T + 16, dtype=np.uint32)
+    toff = np.empty(n_docs + 1, dtype=np.uint64)
+    text = np.ascontiguousarray(text)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+
+    def call():
+        ex = tok._host_exec(False)
+        t = time.perf_counter()
+        rc = _n.lib.ctok_encode_batch(tok._h, text.ctypes.data, off.ctypes.data, n_docs, ids.ctypes.data, T + 16,
+                                      toff.ctypes.data, ctypes.byref(ex), None)
+        dt = time.perf_counter() - t
+        if rc != _n.CTOK_OK:
+            raise RuntimeError("ctok_encode_batch: %d %s" % (rc, _n.last_error()))
+        return dt
+
+    call()  # (first touch of the output pages)
+    ts = sorted(call() for _ in range(reps))
+    e2e_ok = np.array_equal(toff, toff_dev) and np.array_equal(ids[:T], ids_dev)
+    m = min(py_docs, n_docs)
+    docs = [bytes(text[int(off[i]):int(off[i + 1])]).decode() for i in range(m)]
+    tp = []
+    for _ in range(3):
+        t = time.perf_counter()
+        got = tok.encode_batch(docs)
+        tp.append(time.perf_counter() - t)
+    py_ok = all(got[i] == ids_dev[int(toff_dev[i]):int(toff_dev[i + 1])].tolist() for i in range(m))
+    tp.sort()
+    mb = int(off[m]) / 1e6
+    return {
+        "e2e": {"value": round(n_bytes / ts[len(ts) // 2] / 1e6, 1), "unit": "MB/s", "ms_per_call": round(ts[len(ts) // 2] * 1e3, 3),
+                "calls": reps, "parity": "identical to the digest-checked device run" if e2e_ok else "MISMATCH",
+                "what": "ctok_encode_batch on the rank's whole shard from host buffers (pageable numpy; text up, "
+                        "ids + offsets down over PCIe, chunked pipeline), reused output buffer, median call"},
+        "python": {"value": round(mb / tp[1], 1), "unit": "MB/s", "ms_per_call": round(tp[1] * 1e3, 2), "docs": m,
+                   "parity": "identical to the digest-checked device run" if py_ok else "MISMATCH",
+                   "what": "Tokenizer.encode_batch(list[str]) -> list[list[int]] on the shard's first %d docs "
+                           "(%.1f MB), median of 3" % (m, mb)},
+    }
+
+
 def free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -177,6 +228,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--corpus-workers", type=int, default=0, help="1: build the corpus without a process pool")
+    ap.add_argument("--no-user-facing", action="store_true", help="skip the e2e / python rates (rank 0, after timing)")
+    ap.add_argument("--py-docs", type=int, default=100_000)
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -307,6 +360,16 @@ def main():
     b_alg = B + 4 * T + 16 * (D + 1)
     ms_dev = avg("ms_device")
 
+    uf = None
+    if rank == 0 and not args.no_user_facing:
+        ids_dev = d_ids[:ntok].cpu().numpy().view(np.uint32)
+        toff_dev = d_tok_off.cpu().numpy().view(np.uint64)
+        del d_ids
+        torch.cuda.empty_cache()
+        uf = user_facing(tok, text, off, ids_dev, toff_dev, 5, args.py_docs)
+        log("[bench] e2e %.1f MB/s, python %.1f MB/s" % (uf["e2e"]["value"], uf["python"]["value"]))
+        del ids_dev, toff_dev
+
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
@@ -350,6 +413,7 @@ def main():
                          "kernel_MBps": round(n_bytes / (ms_dev * 1e-3) / 1e6, 1),
                          "workspace_bytes": int(st["workspace_bytes"]),
                          "workspace_B_per_byte": round(st["workspace_bytes"] / max(1, n_bytes), 2)},
+            "user_facing": uf,
             "cpu_baseline": cpu,
             "parity": parity,
         }

@@ -914,10 +914,11 @@ void load_root(ctok* t, const ctj::Value& root) {
   }
 
 
-  // window rounds of the segmented long-piece tier (Tables::window, kernels.hip bpe_wave_seg):
-  // exact when the table is rank-monotone and every token instance spans exactly its string's
-  // length -- each byte's initial token is one char, and every merge that can apply makes the
-  // token its two sides spell (no rank shift from an invalid merge before it, src/bpe.rs:60-69).
+  // window rounds of the long-piece tiers (Tables::window, kernels.hip bpe_wave_seg): exact when
+  // every token instance spans exactly its string's length -- each byte's initial token is one
+  // char, and every merge that can apply makes the token its two sides spell (no rank shift from
+  // an invalid merge before it, src/bpe.rs:60-69); on a table that is not rank-monotone the
+  // kernels add a check for candidates whose merge is eager.
   // Per id: the longest left side of a merge whose right side it is, and the longest right side
   // of a merge whose left side it is (chars = bytes; 0xFFFF when longer).
   {
@@ -928,7 +929,8 @@ void load_root(ctok* t, const ctj::Value& root) {
       for (unsigned char ch : it->second) c += (ch & 0xC0) != 0x80;
       return c;
     };
-    bool ok = t->proper && !getenv("CTOK_NO_WINDOW");
+    // (not rank-monotone: the kernels check each candidate whose merge is eager, bpe_wave_seg)
+    bool ok = !getenv("CTOK_NO_WINDOW");
     for (int b = 0; b < 256 && ok; b++)
       if (t->byte2id[b] >= 0 && nchars((uint32_t)t->byte2id[b], ok) != 1) ok = false;
     uint32_t max_id = 0;

@@ -183,9 +183,10 @@ struct Tables {            // device pointers, owned by the host runtime
                             // A round of a non-eager merge applies all its occurrences at once:
                             // every pair the round makes ranks after it, so the sequential loop
                             // also applies them all, left to right, before any other merge.
-  uint32_t window;          // 1: window rounds are exact (proper table, every token spans its string's
-                            // length): the segmented tier also merges, in the same round, any pair
-                            // ranked below every other pair of its window (kernels.hip bpe_wave_seg)
+  uint32_t window;          // 1: window rounds are exact (every token spans its string's length; a
+                            // table that is not rank-monotone also has each eager candidate checked):
+                            // the long-piece tiers also merge, in the same round, any pair ranked
+                            // below every other pair of its window (kernels.hip bpe_wave_seg)
   const uint32_t* wmeta;    // window: per id, the longest left side of a merge it is the right side of
                             // (bits 0-15) and the longest right side of one it is the left side of
   uint32_t compact;         // 1: entry values are new ids (strictly increasing in rank), else ranks

@@ -1982,8 +1982,21 @@ __device__ uint32_t bpe_wave_dense(const Tables& t, const PairLds& P, const int3
         if (rc == kNoRank || rc == r || (p > 0 && (uint32_t)rk[p - 1] <= rc) || (uint32_t)rk[p + 1] <= rc) continue;
         const uint32_t wl = t.wmeta[tok[p]] & 0xFFFFu, wr = t.wmeta[tok[p + 1]] >> 16;
         const uint32_t p0 = pos[p];
-        const uint32_t lo = p0 > wl ? p0 - wl : 0u;
-        const uint32_t hi = (p + 2 < m ? (uint32_t)pos[p + 2] : m0) + wr;
+        uint32_t lo = p0 > wl ? p0 - wl : 0u;
+        uint32_t hi = (p + 2 < m ? (uint32_t)pos[p + 2] : m0) + wr;
+        if (serial_round(t, rc)) {
+          // eager candidate (not rank-monotone; see bpe_wave_seg): its new pairs with today's
+          // neighbours rank above it, and the window covers the neighbours' own windows
+          const uint32_t nn = new_id_of(t, rc);
+          const uint32_t rl = p > 0 ? rank_pair<HOT>(t, P, tok[p - 1], nn, sink) : kNoRank;
+          const uint32_t rr = p + 2 < m ? rank_pair<HOT>(t, P, nn, tok[p + 2], sink) : kNoRank;
+          if (rl <= rc || rr <= rc) continue;
+          if (p > 0) {
+            const uint32_t wlu = t.wmeta[tok[p - 1]] & 0xFFFFu, pu = pos[p - 1];
+            lo = min(lo, pu > wlu ? pu - wlu : 0u);
+          }
+          if (p + 2 < m) hi = max(hi, (p + 3 < m ? (uint32_t)pos[p + 3] : m0) + (t.wmeta[tok[p + 2]] >> 16));
+        }
         bool fire = true;
         for (uint32_t j = p; fire && j > 0;) {
           --j;
@@ -2234,8 +2247,9 @@ __device__ uint32_t bpe_wave_seg(const Tables& t, const PairLds& P, const int32_
       }
       sites = keep;
     }
-    // Window rounds (t.window: a rank-monotone table -- every pair a merge makes ranks after it --
-    // whose token instances span exactly their strings' lengths).  Besides the sites of the
+    // Window rounds (t.window: token instances span exactly their strings' lengths; the argument
+    // below is for a rank-monotone table -- every pair a merge makes ranks after it -- and holds for
+    // any candidate whose merge is not eager; eager ones get the extra check further down).  Besides the sites of the
     // round's rank r, a pair c = (x, y) of rank rc > r merges now when no other pair starting in
     // its window [c - left(x), end(y) + right(y)) ranks <= rc, left(x) / right(y) being the
     // longest left / right side of any merge with x on the right / y on the left (Tables::wmeta).
@@ -2288,12 +2302,63 @@ __device__ uint32_t bpe_wave_seg(const Tables& t, const PairLds& P, const int32_
         wl[g] = q[g] != kNoPos ? (t.wmeta[tc[g]] & 0xFFFFu) : 0u;
         wr[g] = q[g] != kNoPos ? (t.wmeta[tq[g]] >> 16) : 0u;
       }
+      uint32_t lo_x[4], end_x[4];  // window bounds widened for eager candidates (below)
+#pragma unroll
+      for (int g = 0; g < 4; g++) {
+        lo_x[g] = kNone;
+        end_x[g] = 0;
+      }
+      if (!t.proper) {
+        // Not rank-monotone (tiktoken-style lists): a candidate whose merge is eager -- some merge
+        // consuming its token n ranks below it -- also needs its new pairs with today's
+        // neighbours, (u, n) and (n, v), to rank above it, and its window widened to u's and v's
+        // own windows ([u - left(u), end(v) + right(v))), so that neither neighbour can change
+        // before the sequential loop reaches it; then nothing it makes is taken earlier than the
+        // sequential loop would take it.  A non-eager candidate needs neither: every pair its
+        // token n makes, with any neighbour, ranks above it (the monotone argument).  Model and
+        // random non-monotone tables: tests/window_model.py, tests/test_window_rule.py.
+        bool eg[4];
+        uint32_t pu[4], tu[4], tv[4], nv[4], nn[4];
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+          eg[g] = q[g] != kNoPos && serial_round(t, gm[g]);
+          pu[g] = eg[g] ? (uint32_t)prv[cp[g]] : kNoPos;
+          nn[g] = eg[g] ? new_id_of(t, gm[g]) : 0u;
+        }
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+          tu[g] = pu[g] != kNoPos ? (uint32_t)tok[pu[g]] : 0u;
+          tv[g] = eg[g] && nq[g] != kNoPos ? (uint32_t)tok[nq[g]] : 0u;
+          nv[g] = eg[g] && nq[g] != kNoPos ? (uint32_t)nxt[nq[g]] : kNoPos;
+        }
+        Probe<false, HOT> PL[4], PR[4];
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+          PL[g].start(t, P, tu[g], nn[g], pu[g] != kNoPos);
+          PR[g].start(t, P, nn[g], tv[g], eg[g] && nq[g] != kNoPos);
+        }
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+          if (!eg[g]) continue;
+          const uint32_t rl = pu[g] != kNoPos ? PL[g].finish(t, sink) : kNoRank;
+          const uint32_t rr = nq[g] != kNoPos ? PR[g].finish(t, sink) : kNoRank;
+          if (rl <= gm[g] || rr <= gm[g]) {
+            q[g] = kNoPos;  // (not a candidate this round)
+            continue;
+          }
+          if (pu[g] != kNoPos) {
+            const uint32_t wlu = t.wmeta[tu[g]] & 0xFFFFu;
+            lo_x[g] = pu[g] >= wlu ? pu[g] - wlu : 0u;
+          }
+          if (nq[g] != kNoPos) end_x[g] = (nv[g] == kNoPos ? m : nv[g]) + (t.wmeta[tv[g]] >> 16);
+        }
+      }
 #pragma unroll
       for (int g = 0; g < 4; g++) {
         if (q[g] == kNoPos) continue;
         const uint32_t c = cp[g];
-        const uint32_t lo = c >= wl[g] ? c - wl[g] : 0u;
-        const uint32_t end = min((nq[g] == kNoPos ? m : nq[g]) + wr[g], m);
+        const uint32_t lo = min(c >= wl[g] ? c - wl[g] : 0u, lo_x[g]);
+        const uint32_t end = min(max((nq[g] == kNoPos ? m : nq[g]) + wr[g], end_x[g]), m);
         const uint32_t h0 = unit(lo), h1 = unit(end - 1), own = unit(c);
         if (h1 - h0 >= kWinGroups) continue;
         bool ok = true;

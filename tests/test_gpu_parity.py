@@ -215,6 +215,27 @@ def test_window_rounds_random_proper_multibyte(alpha):
     assert len(ids) < 0.4 * len(text)
 
 
+@pytest.mark.parametrize("seed", range(8))
+def test_window_rounds_non_monotone(seed):
+    """Window rounds on tables that are not rank-monotone (round 4: eager candidates checked
+    against their neighbours, kernels.hip bpe_wave_seg / bpe_wave_dense): a random proper table's
+    merges shuffled, and re-laid out tiktoken-style (tests/test_window_rule.py _non_monotone), with
+    runs at every long-piece tier's lengths, against the C oracle."""
+    from tests.test_window_rule import _non_monotone
+    alpha, rng, objs = _non_monotone(seed)
+    chars = list(alpha)
+    docs = []
+    for n in [5, 20, 40, 63, 64, 65, 86, 100, 200, 256, 257, 400, 700, 1024, 1025, 1400, 3000, 4096, 5000]:
+        for _ in range(3):
+            docs.append(b"x " + "".join(rng.choice(chars, size=max(1, n // len(chars[0].encode())))).encode() + b" y")
+    rng.shuffle(docs)
+    text, off = corpus.pack(docs)
+    for o in objs:
+        tok, rc = gpu_tok(o), ref_c.RefC(o)
+        ids, toff = tok.encode_packed(text, off)
+        assert_same(ids, toff, *rc.encode_packed(text, off))
+
+
 def test_c3_full_corpus(llama3_path):
     """C3 (100k docs, 76 MB, 1% with 1-4 KiB runs of letters, digits, words or one repeated
     letter) with the rank-monotone Llama-3-shaped fixture, whose long pieces take the window

@@ -9,7 +9,7 @@ import pytest
 
 from oracle.ref_py import RefTokenizer
 from tests import toys
-from tests.window_model import window_bpe, window_bpe_dense, window_meta
+from tests.window_model import eager_set, window_bpe, window_bpe_dense, window_meta
 
 
 def _ids(tok, data: bytes):
@@ -53,6 +53,56 @@ def test_window_rounds_multibyte_tables(seed):
             for k in (16, 64):
                 assert window_bpe(tok, ids, k=k)[0] == want, (seed, n, k)
             assert window_bpe_dense(tok, ids)[0] == want, (seed, n, "dense")
+
+
+def _non_monotone(seed):
+    """Two tables that are not rank-monotone, from one random proper table: its merges shuffled,
+    and re-laid out as the tiktoken conversion does (every split of every token, by the token's id:
+    datagen/build_tokenizers.py tiktoken_style_merges)."""
+    from datagen.build_tokenizers import tiktoken_style_merges
+    alpha = ["abc", "ab", "abcd", "日本", "xyz"][seed % 5]
+    rng = np.random.default_rng(seed)
+    base = toys.random_proper_from_text(seed, "".join(rng.choice(list(alpha), size=2000)).encode(),
+                                        n_merges=60 + seed % 80, max_len=6 + seed % 12)
+    tt = json.loads(json.dumps(base))
+    tt["model"]["merges"] = ["%s %s" % m for m in tiktoken_style_merges(tt["model"]["vocab"])]
+    return alpha, rng, [toys.shuffled_merges(base, seed), tt]
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_window_rounds_non_monotone_tables(seed):
+    """Window rounds on tables that are not rank-monotone (round 4): a candidate whose merge is
+    eager also needs its new pairs with today's neighbours to rank above it and a window that covers
+    the neighbours' windows (kernels.hip bpe_wave_seg / bpe_wave_dense).  Against the reference loop."""
+    alpha, rng, objs = _non_monotone(seed)
+    for o in objs:
+        tok = RefTokenizer(o)
+        assert window_meta(tok) is not None
+        eg = eager_set(tok)
+        assert eg  # (the table really is not rank-monotone)
+        for n in [3, 10, 40, 100, 300]:
+            data = "".join(rng.choice(list(alpha), size=n)).encode()
+            ids = _ids(tok, data)
+            want = tok.bpe("".join(toys.byte_map()[b] for b in data))
+            for k in (16, 64):
+                assert window_bpe(tok, ids, k=k, eager=eg)[0] == want, (seed, n, k)
+            assert window_bpe_dense(tok, ids, eager=eg)[0] == want, (seed, n, "dense")
+
+
+def test_window_rounds_tiktoken_layout_llama3(llama3_tt_path):
+    """The 304k-merge tiktoken-layout Llama-3 fixture (C3TT): exact, and the eager-candidate rule
+    cuts the rounds of C3-like runs several-fold (rank rounds alone: ~350-1200)."""
+    with open(llama3_tt_path) as f:
+        tok = RefTokenizer(json.load(f))
+    eg = eager_set(tok)
+    rng = np.random.default_rng(3)
+    words = [w for w in (tok.id_to_token_map[i] for i in range(300, 8000)) if w.isalpha()][:3000]
+    runs = [bytes(rng.integers(ord("a"), ord("z") + 1, size=1200).astype(np.uint8)),
+            "".join(words[int(i)] for i in rng.integers(len(words), size=400)).encode()[:1200], b"q" * 1200]
+    for data in runs:
+        got, rounds = window_bpe(tok, _ids(tok, data), k=64, eager=eg)
+        assert got == tok.bpe("".join(toys.byte_map()[b] for b in data))
+        assert rounds < 60
 
 
 def test_window_meta_refuses_shifted_ranks():
