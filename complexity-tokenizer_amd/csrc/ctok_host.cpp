@@ -1135,6 +1135,22 @@ void upload(DevBuf<T>& b, const T* src, size_t n, hipStream_t s) {
   if (n) HIPTRY(hipMemcpyAsync(b.p, src, n * sizeof(T), hipMemcpyHostToDevice, s));
 }
 
+// Tables::cp_fast: every code point of cp_range_class's ranges has the class it gives and no NFC
+// flag in the generated tables (gen/unicode_data.h), so k_segment may skip their lookups.
+bool cp_fast_ok() {
+  static const bool ok = [] {
+    if (getenv("CTOK_NO_CP_RANGES")) return false;
+    for (uint32_t cp = 0x3000; cp < 0x1F700; cp++) {
+      const int rc = cp_range_class(cp);
+      if (rc < 0) continue;
+      const int cl = (ct_cls_stage2[ct_cls_stage1[cp >> 8] * 64 + ((cp & 255) >> 2)] >> ((cp & 3) * 2)) & 3;
+      if (cl != rc || ct_nfc_stage2[ct_nfc_stage1[cp >> 8] * 256 + (cp & 255)] != 0) return false;
+    }
+    return true;
+  }();
+  return ok;
+}
+
 DeviceState* device_state(ctok* t, int device) {
   std::lock_guard<std::mutex> lk(t->dev_mu);
   auto it = t->devs.find(device);
@@ -1207,6 +1223,7 @@ DeviceState* device_state(ctok* t, int device) {
   tb.cls_s2 = ds->cls_s2.p;
   tb.nfc_s1 = ds->nfc_s1.p;
   tb.nfc_s2 = ds->nfc_s2.p;
+  tb.cp_fast = cp_fast_ok() ? 1u : 0u;
   tb.decomp_cp = ds->decomp_cp.p;
   tb.decomp_off = ds->decomp_off.p;
   tb.decomp_data = ds->decomp_data.p;

@@ -145,6 +145,19 @@ __host__ __device__ inline uint32_t piece_hash(uint32_t lo, uint32_t hi, uint32_
   return h ^ (h >> 16);
 }
 
+// Common non-ASCII blocks classified by range tests instead of the two-level tables (C5: CJK,
+// kana, Hangul, emoji): the class (1 = L, 3 = other) when cp lies in one, else -1.  Every code
+// point of these ranges has that class and no NFC flag in the generated tables; the host checks
+// this once (cp_fast_ok, ctok_host.cpp) and clears Tables::cp_fast otherwise.
+__host__ __device__ __forceinline__ int cp_range_class(uint32_t cp) {
+  if (cp - 0x4E00u < 0x5200u) return 1;    // CJK Unified Ideographs U+4E00..U+9FFF (Lo)
+  if (cp - 0xAC00u < 0x2BA4u) return 1;    // Hangul Syllables U+AC00..U+D7A3 (Lo)
+  if (cp - 0x3041u < 0x56u) return 1;      // Hiragana U+3041..U+3096 (Lo)
+  if (cp - 0x30A1u < 0x5Au) return 1;      // Katakana U+30A1..U+30FA (Lo)
+  if (cp - 0x1F300u < 0x350u) return 3;    // Misc. Symbols and Pictographs, Emoticons U+1F300..U+1F64F (So / Sk)
+  return -1;
+}
+
 struct Tables {            // device pointers, owned by the host runtime
   const uint64_t* merge_tab;
   uint32_t merge_mask;     // capacity - 1 (power of two)
@@ -163,6 +176,8 @@ struct Tables {            // device pointers, owned by the host runtime
   const uint8_t* cls_s2;
   const uint8_t* nfc_s1;
   const uint16_t* nfc_s2;
+  uint32_t cp_fast;        // 1: the code point ranges of cp_range_class (kernels.hip) hold the class
+                           // it gives and no NFC flag in these tables (checked at upload)
   const uint32_t* decomp_cp;
   const uint16_t* decomp_off;
   const uint32_t* decomp_data;

@@ -360,7 +360,7 @@ __device__ __forceinline__ uint32_t select_bit(uint64_t x, uint32_t k) {
 // profiles/r03/v30_ab_seg_waves_per_eu.txt)
 __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(7))) void k_segment(Work w, Tables t) {
   __shared__ uint16_t s_pos_all[kSegWaves][64 * kSegUnroll + 8];  // one round's piece starts
-  __shared__ uint32_t s_text_all[kSegWaves][(kTileWords + 1) * 16 + 4];  // the tile + look-ahead word
+  __shared__ uint32_t s_text_all[kSegWaves][(kTileWords + 2) * 16 + 4];  // context word + tile + look-ahead word
   __shared__ uint64_t s_D_all[kSegWaves][64];  // doc starts per word (piece records carry kRecDoc)
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wid = uni(threadIdx.x >> 6);
@@ -405,14 +405,17 @@ __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(
   }
   seg::Masks m = seg::ascii_masks(x);
   s_D_all[wid][lane] = D;
-  uint32_t* s_text = s_text_all[wid];
-  if (!first) {  // the tile's bytes (and the look-ahead word) for the whole-piece probes
+  // every lane's word in LDS: the tile's bytes (and the look-ahead word) for the whole-piece
+  // probes (s_text: the tile's first byte), the context word too for the code point decoding below
+  uint32_t* s_all = s_text_all[wid];
+  uint32_t* s_text = s_all + 16;
 #pragma unroll
-    for (int k = 0; k < 4; k++)
-      *reinterpret_cast<uint4*>(s_text + (lane - 1) * 16 + 4 * k) = make_uint4(x[4 * k], x[4 * k + 1], x[4 * k + 2], x[4 * k + 3]);
-  } else {
-    s_text[(kTileWords + 1) * 16] = 0;
-  }
+  for (int k = 0; k < 4; k++)
+    *reinterpret_cast<uint4*>(s_all + lane * 16 + 4 * k) = make_uint4(x[4 * k], x[4 * k + 1], x[4 * k + 2], x[4 * k + 3]);
+  if (last) s_all[64 * 16] = 0;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   if (m.NA) {  // non-ASCII code points: classes and NFC flags from the two-level tables
     constexpr int kSegCp = 4;
     const uint32_t x0 = (uint32_t)(g * 64);
@@ -449,20 +452,23 @@ __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(
       }
 #pragma unroll
       for (int k = 0; k < kSegCp; k++) {
-        const uint32_t a = x0 + min(pos[k], 63u);
-        const uint32_t b0 = w.text[min(a, B - 1)];
-        const uint32_t b1 = w.text[min(a + 1, B - 1)] & 0x3Fu, b2 = w.text[min(a + 2, B - 1)] & 0x3Fu;
-        const uint32_t b3 = w.text[min(a + 3, B - 1)] & 0x3Fu;
+        // the code point's bytes from LDS (this lane's word and the next: s_all is contiguous;
+        // valid UTF-8 never runs past the text, whose bytes past B read as zero)
+        const uint32_t a = lane * 64 + min(pos[k], 63u);
+        const uint32_t v = __builtin_amdgcn_alignbyte(s_all[(a >> 2) + 1], s_all[a >> 2], a & 3);
+        const uint32_t b0 = v & 255u, b1 = (v >> 8) & 0x3Fu, b2 = (v >> 16) & 0x3Fu, b3 = (v >> 24) & 0x3Fu;
         const int l = u8len((uint8_t)b0);
         len[k] = (uint32_t)l;
         cp[k] = l == 2 ? ((b0 & 0x1Fu) << 6) | b1
               : l == 3 ? ((b0 & 0x0Fu) << 12) | (b1 << 6) | b2
               : l == 4 ? ((b0 & 0x07u) << 18) | (b1 << 12) | (b2 << 6) | b3 : b0;
       }
+      int rc[kSegCp];  // range-test class, -1: look it up
       uint32_t s1[kSegCp], n1[kSegCp];
 #pragma unroll
       for (int k = 0; k < kSegCp; k++) {
-        const bool in = pos[k] < 64 && cp[k] < 0x110000;
+        rc[k] = t.cp_fast ? cp_range_class(cp[k]) : -1;
+        const bool in = pos[k] < 64 && cp[k] < 0x110000 && rc[k] < 0;
         s1[k] = in ? t.cls_s1[cp[k] >> 8] : 0u;
         n1[k] = in ? t.nfc_s1[cp[k] >> 8] : 0u;
       }
@@ -472,7 +478,9 @@ __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(
         const uint32_t c = cp[k];
         int cl = 3;
         bool nf = false;
-        if (c < 0x80) {
+        if (rc[k] >= 0) {
+          cl = rc[k];
+        } else if (c < 0x80) {
           cl = cls_ascii(c);
         } else if (c < 0x110000) {
           cl = (t.cls_s2[s1[k] * 64 + ((c & 255) >> 2)] >> ((c & 3) * 2)) & 3;

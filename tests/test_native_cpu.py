@@ -229,3 +229,30 @@ def test_create_from_tables_rejects_tokens_with_spaces():
     # tokens without spaces still load, and a vocab entry with a space that no merge joins is fine
     t = Tokenizer.from_tables(vocab, [(vocab["a"], vocab["b"])])
     assert t.token_to_id("a b") == n
+
+
+def _c_array(src, name):
+    import re
+    m = re.search(r"%s\[\d+\] = \{(.*?)\};" % name, src, re.S)
+    return [int(x, 0) for x in m.group(1).replace("\n", " ").split(",") if x.strip()]
+
+
+def test_cp_range_classes_match_tables():
+    """k_segment classifies CJK / Hangul / kana / emoji code points by range tests (ctok_internal.h
+    cp_range_class, round 4) instead of the two-level tables: every code point of those ranges must
+    have that class and no NFC flag in gen/unicode_data.h (the host re-checks this at upload,
+    cp_fast_ok), and the classes must be the regex module's (\\p{L} / other)."""
+    import regex
+    src = open(os.path.join(ROOT, "complexity-tokenizer_amd", "csrc", "gen", "unicode_data.h")).read()
+    c1, c2 = _c_array(src, "ct_cls_stage1"), _c_array(src, "ct_cls_stage2")
+    n1, n2 = _c_array(src, "ct_nfc_stage1"), _c_array(src, "ct_nfc_stage2")
+    ranges = [(0x4E00, 0x9FFF, 1), (0xAC00, 0xD7A3, 1), (0x3041, 0x3096, 1), (0x30A1, 0x30FA, 1),
+              (0x1F300, 0x1F64F, 3)]
+    rl, rn, rs = regex.compile(r"\p{L}"), regex.compile(r"\p{N}"), regex.compile(r"\s")
+    for lo, hi, want in ranges:
+        for cp in range(lo, hi + 1):
+            cl = (c2[c1[cp >> 8] * 64 + ((cp & 255) >> 2)] >> ((cp & 3) * 2)) & 3
+            assert cl == want, hex(cp)
+            assert n2[n1[cp >> 8] * 256 + (cp & 255)] == 0, hex(cp)
+            ch = chr(cp)
+            assert (1 if rl.match(ch) else 0 if rs.match(ch) else 2 if rn.match(ch) else 3) == want, hex(cp)

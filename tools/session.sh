@@ -1,0 +1,54 @@
+#!/bin/bash
+# One GPU-box session (run through gpurun from the repo root).  Steps, chained so that the first
+# failure ends the session, each under its own time limit:
+#   tests   pytest -m gpu (whole suite)          bench   bench.py default line (C4, CPU baseline)
+#   prof    rocprofv3 kernel trace of bench.py   pmc     FETCH_SIZE / WRITE_SIZE passes -> traffic
+#   ab:CFG:FIX:LIB_A:LIB_B   alternating kernel-only probes (tools/probe.py) of two libraries
+#   matrix  tools/bench_matrix.py (every config)  probe:CFG:FIX  one probe of the working tree
+#   usage: TAG=name bash tools/session.sh STEP [STEP ...]
+set -e
+TAG=${TAG:-run}
+ROOT=$(pwd)
+OUT=$ROOT/gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+for step in "$@"; do
+  case "$step" in
+    tests)
+      timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 900 --timeout-method thread \
+        > "$OUT/gpu_tests.log" 2>&1 || { tail -40 "$OUT/gpu_tests.log"; exit 1; }
+      tail -3 "$OUT/gpu_tests.log" ;;
+    bench)
+      timeout -k 10 500 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.log" || { tail -20 "$OUT/bench.log"; exit 1; }
+      cat "$OUT/bench.json" ;;
+    prof)
+      (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
+        python3 "$ROOT/bench.py" --steps 10 --no-cpu-baseline --no-user-facing > "$OUT/prof_bench.json" 2> "$OUT/prof_bench.log") \
+        || { tail -20 "$OUT/prof_bench.log"; exit 1; }
+      cat "$OUT/prof_bench.json" ;;
+    pmc)
+      (cd /tmp && timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- \
+        python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-parity --no-user-facing --corpus-workers 1 \
+        > "$OUT/pmc_fetch.log" 2>&1) || { tail -20 "$OUT/pmc_fetch.log"; exit 1; }
+      (cd /tmp && timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
+        python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-parity --no-user-facing --corpus-workers 1 \
+        > "$OUT/pmc_write.log" 2>&1) || { tail -20 "$OUT/pmc_write.log"; exit 1; }
+      python3 "$ROOT/tools/pmc_traffic.py" "$OUT/pmc_fetch" "$OUT/pmc_write" "$OUT/pmc_traffic.json" c4/10000000 ;;
+    ab:*)
+      IFS=: read -r _ cfg fx la lb <<< "$step"
+      for i in 1 2 3; do
+        for L in "$la" "$lb"; do
+          CTOK_LIB=$L timeout -k 10 300 python -u tools/probe.py "$cfg" "$fx" 5 2>/dev/null | grep MB/s | sed "s|^|$(basename "$L") |" \
+            | tee -a "$OUT/ab_${cfg}_${fx}.txt"
+        done
+      done ;;
+    probe:*)
+      IFS=: read -r _ cfg fx <<< "$step"
+      timeout -k 10 300 python -u tools/probe.py "$cfg" "$fx" 5 2>&1 | tee -a "$OUT/probe_${cfg}_${fx}.txt" ;;
+    matrix)
+      timeout -k 10 900 python -u tools/bench_matrix.py > "$OUT/matrix.json" 2> "$OUT/matrix.log" || { tail -20 "$OUT/matrix.log"; exit 1; }
+      tail -5 "$OUT/matrix.log" ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "session $TAG done"
