@@ -1357,7 +1357,8 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
           for (int k = 0; k < N; k++)
             if ((uint32_t)k < m) out[k] = tk[k];
         }
-        w.tcnt[(size_t)tile * kTileSlots + j] = rec_short(m, pos) | ((e & kEntDoc) ? kRecDoc : 0u);
+        if (t.dbg != 30)  // (A/B measurement only: 30 drops the record stores, ids wrong)
+          w.tcnt[(size_t)tile * kTileSlots + j] = rec_short(m, pos) | ((e & kEntDoc) ? kRecDoc : 0u);
         st_bytes += n;
         st_ids += m;
     };

@@ -200,3 +200,28 @@ def test_trainer_oracle_merge_order_pinned_without_ties():
     ref = trainer_ref.RefTrainer(vocab_size=target, min_frequency=1, inl_gate=0.0)
     ref.train_from_word_freqs(dict(wf))
     assert ref.merges == want
+
+
+@pytest.mark.parametrize("threads", [1, 4])
+def test_trainer_c_restatement_matches_oracle(threads):
+    """oracle/trainer_ref.c (the CPU timing baseline of the trainer, tools/trainer_timing.py) applies
+    a training run's merges with the reference's bookkeeping: its final words and live pair count
+    must equal oracle/trainer_ref.py's after the same training."""
+    import copy
+    from oracle import trainer_c
+    from datagen import corpus
+    text, off = corpus.corpus_c1()
+    texts = [d.decode() for d in corpus.unpack(text, off)][:400]
+    ref = trainer_ref.RefTrainer(vocab_size=350, min_frequency=1)
+    wf = {}
+    ref._count_into(wf, texts)
+    words = ref.init_vocab_bytelevel(wf)
+    start = copy.deepcopy(words)
+    tf0 = dict(ref.token_freqs)
+    ref.compute_initial_pairs(words)
+    ref.learn_merges_heap(words)
+    merges = [(ref.vocab[a], ref.vocab[b], ref.vocab[a + b]) for a, b in ref.merges]
+    assert len(merges) > 30
+    got, _, _, live = trainer_c.run([(t, f) for t, f in start], merges, tf0, len(ref.vocab) + 1, threads)
+    assert got == [t for t, _ in words]
+    assert live == len(ref.pair_freqs)

@@ -9,7 +9,7 @@ for i in 1 2 3; do
   for v in A B; do
     spec=$A; [ $v = B ] && spec=$B
     lib=${spec%%,*}; envs=""; [ "$spec" != "$lib" ] && envs=${spec#*,}
-    env CTOK_LIB=$lib $envs timeout -k 10 120 python -u bench.py --no-cpu-baseline --steps 30 "$@" \
+    env CTOK_LIB=$lib $envs timeout -k 10 180 python -u bench.py --no-cpu-baseline --no-user-facing --steps 30 "$@" \
       > gpurun_out/ab/$v$i.json 2> gpurun_out/ab/$v$i.log
     python3 -c "
 import json,sys

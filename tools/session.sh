@@ -5,6 +5,7 @@
 #   prof    rocprofv3 kernel trace of bench.py   pmc     FETCH_SIZE / WRITE_SIZE passes -> traffic
 #   ab:CFG:FIX:LIB_A:LIB_B   alternating kernel-only probes (tools/probe.py) of two libraries
 #   matrix  tools/bench_matrix.py (every config)  probe:CFG:FIX  one probe of the working tree
+#   abenv:VAR=VAL   bench.py A/B (tools/ab.sh) without / with VAR=VAL     ablib:LIB_A:LIB_B   the same for two libraries
 #   usage: TAG=name bash tools/session.sh STEP [STEP ...]
 set -e
 TAG=${TAG:-run}
@@ -42,6 +43,12 @@ for step in "$@"; do
             | tee -a "$OUT/ab_${cfg}_${fx}.txt"
         done
       done ;;
+    abenv:*)  # bench.py A/B of the working tree's library without / with an environment setting
+      L=complexity-tokenizer_amd/complexity_tokenizer/libctok.so
+      bash tools/ab.sh "$L" "$L,${step#abenv:}" 2>&1 | tee -a "$OUT/abenv.txt" ;;
+    ablib:*)  # bench.py A/B of two libraries
+      IFS=: read -r _ la lb <<< "$step"
+      bash tools/ab.sh "$la" "$lb" 2>&1 | tee -a "$OUT/ablib.txt" ;;
     probe:*)
       IFS=: read -r _ cfg fx <<< "$step"
       timeout -k 10 300 python -u tools/probe.py "$cfg" "$fx" 5 2>&1 | tee -a "$OUT/probe_${cfg}_${fx}.txt" ;;
