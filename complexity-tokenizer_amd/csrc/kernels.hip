@@ -609,7 +609,7 @@ __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(
     }
     // all first probes in flight together (unrolled by hand: a loop over u around the probing
     // loop would not unroll, and the arrays would go to scratch)
-    uint32_t hitv[U];
+    uint32_t hitv[U], rec[U];
 #define CTOK_PROBE_LOAD(u) const uint4 e##u = t.piece_tab[h[u]];
 #define CTOK_PROBE_USE(u) hitv[u] = piece_probe(t, e##u, h[u], plo[u], phi[u], n[u]);
     static_assert(U == 4 || U == 8, "kSegUnroll: 4 or 8");
@@ -623,17 +623,15 @@ __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(
 #undef CTOK_PROBE_USE
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      const uint32_t j = j0 + 64 * u + lane;
-      uint32_t rec = 0;  // placeholder, rewritten by the pass that merges the piece
+      rec[u] = 0;  // placeholder, rewritten by the pass that merges the piece
       // (written as flag arithmetic: an if / else-if chain assigning cls[u] in each arm was
       // miscompiled by this hipcc in the unrolled loop)
       if (cls[u] == 5) {
         const bool hit = hitv[u] != kNone;
-        rec = hit ? kRecHit | hitv[u] | (doc[u] ? kRecDoc : 0u) : 0u;
+        rec[u] = hit ? kRecHit | hitv[u] | (doc[u] ? kRecDoc : 0u) : 0u;
         hits += hit ? 1u : 0u;
         cls[u] = hit ? 4u : 0u;
       }
-      if (j < np) tcnt[j] = rec;  // every piece's slot: whole coalesced lines
     }
     {  // the tile's class-0 list is full: the rest of its class-0 pieces go to the long list (one
        // uniform test per round; the per-piece fix-up only in the rare round that crosses w.k0)
@@ -659,10 +657,20 @@ __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(
         const uint64_t m1 = __ballot(cls[u] == 1), m2 = __ballot(cls[u] == 2);
         const uint64_t m3 = __ballot(cls[u] == 6);
         const uint64_t below = lanemask_lt();
-        if (cls[u] == 0) w.list0[(size_t)tile * w.k0 + n0 + __popcll(m0 & below)] = e;
-        if (cls[u] == 1) w.list1[(size_t)tile * kCap1 + n1 + __popcll(m1 & below)] = e;
-        if (cls[u] == 2) w.list2[(size_t)tile * kCap2 + n2 + __popcll(m2 & below)] = e;
-        if (cls[u] == 6) w.list3[(size_t)tile * kCap3 + n3 + __popcll(m3 & below)] = e;
+        const uint32_t q0 = n0 + __popcll(m0 & below), q1 = n1 + __popcll(m1 & below);
+        const uint32_t q2 = n2 + __popcll(m2 & below), q3 = n3 + __popcll(m3 & below);
+        if (cls[u] == 0) w.list0[(size_t)tile * w.k0 + q0] = e;
+        if (cls[u] == 1) w.list1[(size_t)tile * kCap1 + q1] = e;
+        if (cls[u] == 2) w.list2[(size_t)tile * kCap2 + q2] = e;
+        if (cls[u] == 6) w.list3[(size_t)tile * kCap3 + q3] = e;
+        // the piece's record (every piece's slot: whole coalesced lines): a class-list piece
+        // points at its list slot, where its merge pass leaves count | pos (Work::lrec)
+        if (w.lrec && !generic) {
+          const uint32_t dr = doc[u] ? kRecDoc : 0u;
+          rec[u] = cls[u] == 0 ? rec_list(0, q0) | dr : cls[u] == 1 ? rec_list(1, q1) | dr
+                 : cls[u] == 2 ? rec_list(2, q2) | dr : cls[u] == 6 ? rec_list(3, q3) | dr : rec[u];
+        }
+        if (j < np) tcnt[j] = rec[u];
         by0 += cls[u] == 0 ? n[u] : 0u;
         by1 += cls[u] == 1 ? n[u] : 0u;
         by2 += cls[u] == 2 ? n[u] : 0u;
@@ -1285,14 +1293,15 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
       }
       __syncthreads();
     }
-    auto entry = [&](uint32_t i, uint32_t& kt) {
+    auto entry = [&](uint32_t i, uint32_t& kt, uint32_t& qi) {
       const uint32_t q = sorted ? (uint32_t)S.perm[i] : i;
       kt = tile_of<K>(S.pre, q);
-      return list[(size_t)(c0 + kt) * cap + (q - S.pre[kt])];
+      qi = q - S.pre[kt];  // (index in the tile's list: where the record goes, Work::lrec)
+      return list[(size_t)(c0 + kt) * cap + qi];
     };
     auto start_of = [&](uint32_t e, uint32_t kt) { return (c0 + kt) * kTile + (e & 0xFFFu); };
     // one piece: list entry e of chunk tile kt, its first N bytes in wv
-    auto body = [&](uint32_t e, uint32_t kt, const uint32_t* wv) {
+    auto body = [&](uint32_t e, uint32_t kt, uint32_t qi, const uint32_t* wv) {
         const uint32_t tile = c0 + kt;
         const uint32_t s = tile * kTile + (e & 0xFFFu);
         const uint32_t j = ent_j(e);
@@ -1357,19 +1366,23 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
           for (int k = 0; k < N; k++)
             if ((uint32_t)k < m) out[k] = tk[k];
         }
-        if (t.dbg != 30)  // (A/B measurement only: 30 drops the record stores, ids wrong)
-          w.tcnt[(size_t)tile * kTileSlots + j] = rec_short(m, pos) | ((e & kEntDoc) ? kRecDoc : 0u);
+        if (t.dbg != 30) {  // (A/B measurement only: 30 drops the record stores, ids wrong)
+          if (w.lrec)  // the list slot the piece came from (k_segment's record points at it)
+            const_cast<uint32_t*>(list)[(size_t)tile * cap + qi] = rec_short(m, pos);
+          else
+            w.tcnt[(size_t)tile * kTileSlots + j] = rec_short(m, pos) | ((e & kEntDoc) ? kRecDoc : 0u);
+        }
         st_bytes += n;
         st_ids += m;
     };
     if constexpr (N > 32) {
       // 64 slots: no registers to spare for a pipeline; a static stride over the chunk
       for (uint32_t i = tid; i < E; i += NT) {
-        uint32_t kt;
-        const uint32_t e = entry(i, kt);
+        uint32_t kt, qi;
+        const uint32_t e = entry(i, kt, qi);
         uint32_t wv[N / 4];
         load_words<N / 4>(w.text, start_of(e, kt), w.n_bytes, wv);
-        body(e, kt, wv);
+        body(e, kt, qi, wv);
       }
     } else {
       // Each wavefront takes blocks of 64 entries from S.next (one LDS atomic per block): a wave
@@ -1385,29 +1398,30 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
         return uni((uint32_t)__shfl((int)b, 0, 64));
       };
       constexpr int kPw = N / 4;
-      uint32_t e0 = 0, kt0 = 0, e1 = 0, kt1 = 0;
+      uint32_t e0 = 0, kt0 = 0, q0 = 0, e1 = 0, kt1 = 0, q1 = 0;
       uint32_t wv0[kPw];
       uint32_t b0 = take();
       uint32_t b1 = b0 < E ? take() : E;
       if (b0 + lane < E) {
-        e0 = entry(b0 + lane, kt0);
+        e0 = entry(b0 + lane, kt0, q0);
         load_words<kPw>(w.text, start_of(e0, kt0), w.n_bytes, wv0);
       }
-      if (b1 + lane < E) e1 = entry(b1 + lane, kt1);
+      if (b1 + lane < E) e1 = entry(b1 + lane, kt1, q1);
       while (b0 < E) {  // wave-uniform
         const uint32_t i = b0 + lane;
         const uint32_t b2 = b1 < E ? take() : E;
-        const uint32_t e = e0, kt = kt0;
+        const uint32_t e = e0, kt = kt0, qi = q0;
         uint32_t wv[N / 4];
 #pragma unroll
         for (int k = 0; k < N / 4; k++) wv[k] = wv0[k];
         e0 = e1;
         kt0 = kt1;
+        q0 = q1;
         if (b1 + lane < E) load_words<kPw>(w.text, start_of(e0, kt0), w.n_bytes, wv0);
-        if (b2 + lane < E) e1 = entry(b2 + lane, kt1);
+        if (b2 + lane < E) e1 = entry(b2 + lane, kt1, q1);
         b0 = b1;
         b1 = b2;
-        if (i < E) body(e, kt, wv);
+        if (i < E) body(e, kt, qi, wv);
       }
     }
     tile_share_flush<K>(w, c0, tb1, S.tsum, S.tbase, LC::cls);
@@ -2781,6 +2795,15 @@ constexpr uint32_t kEmitStage = 1024;  // ids of one round staged in LDS (4 KiB 
 __device__ __forceinline__ uint32_t rec_count(const Work& w, uint32_t v) {
   return (v & kRecHit) ? 1u : (v & kRecLong) ? w.long_cnt[v & kRecLongMask] : (v & 0xFFFFu);
 }
+// A kRecList record's merged form (count | pos << 16) from its list slot, with the flags kept;
+// every other record as it is.
+__device__ __forceinline__ uint32_t rec_resolve(const Work& w, uint32_t tile, uint32_t v) {
+  if ((v & (kRecHit | kRecLong | kRecList)) != kRecList) return v;
+  const uint32_t c = (v >> 12) & 3u, q = v & 0xFFFu;
+  const uint32_t* l = c == 0 ? w.list0 + (size_t)tile * w.k0 : c == 1 ? w.list1 + (size_t)tile * kCap1
+                    : c == 2 ? w.list2 + (size_t)tile * kCap2 : w.list3 + (size_t)tile * kCap3;
+  return l[q] | (v & kRecDoc);
+}
 
 __global__ __launch_bounds__(64 * kEmitWaves) void k_emit(Work w, uint32_t* __restrict__ ids, uint64_t ids_cap,
                                                          uint64_t* __restrict__ tok_off) {
@@ -2806,8 +2829,10 @@ __global__ __launch_bounds__(64 * kEmitWaves) void k_emit(Work w, uint32_t* __re
   uint4 nx = load(4 * lane);
   for (uint32_t r0 = 0; r0 < np; r0 += 256) {
     const uint32_t j0 = r0 + 4 * lane;
-    const uint32_t rec[4] = {nx.x, nx.y, nx.z, nx.w};
+    uint32_t rec[4] = {nx.x, nx.y, nx.z, nx.w};
     if (r0 + 256 < np) nx = load(j0 + 256);
+#pragma unroll
+    for (int k = 0; k < 4; k++) rec[k] = j0 + k < np ? rec_resolve(w, tile, rec[k]) : rec[k];
     uint32_t c[4], sum = 0;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
