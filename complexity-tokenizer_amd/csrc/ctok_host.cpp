@@ -501,15 +501,20 @@ void parse_post_processor(ctok* t, const ctj::Value* v) {
   }
 }
 
-bool rust_regex_compiles(const std::string& p) {
-  // Rust's regex crate has no look-around, atomic groups or backreferences.  Scanned token by
-  // token: an escaped character or anything inside a character class ([...], nested classes
-  // allowed) is a literal, so "[(?=]" or "\\(?=" do not count as look-ahead.
-  int cls = 0;  // character-class nesting depth
+// Does the Rust regex crate compile pattern p?  It has no look-around, atomic groups or
+// backreferences, and rejects unbalanced groups and classes; the reference then drops the Split
+// (src/pretokenizers.rs:298-302).  Returns "" when none of these is found (taken as compiling),
+// else the construct that makes it fail.  Scanned token by token: an escaped character or anything
+// inside a character class ([...], nested classes allowed) is a literal, so "[(?=]" or "\\(?="
+// do not count as look-ahead.  (Other reasons the crate may reject a pattern -- an unknown \p{..}
+// name, a bad repetition -- are not detected: such a Split is refused loudly, never applied.)
+std::string rust_regex_rejects(const std::string& p) {
+  int cls = 0;    // character-class nesting depth
+  int group = 0;  // open groups
   for (size_t i = 0; i < p.size(); i++) {
     const char c = p[i];
     if (c == '\\') {
-      if (i + 1 < p.size() && p[i + 1] >= '1' && p[i + 1] <= '9') return false;  // backreference
+      if (i + 1 < p.size() && p[i + 1] >= '1' && p[i + 1] <= '9') return "backreference \\" + std::string(1, p[i + 1]);
       i++;
       continue;
     }
@@ -524,13 +529,23 @@ bool rust_regex_compiles(const std::string& p) {
       if (i + 1 < p.size() && p[i + 1] == ']') i++;  // a leading ']' is a literal
       continue;
     }
-    if (c == '(' && i + 2 < p.size() && p[i + 1] == '?') {
-      const char d = p[i + 2];
-      if (d == '=' || d == '!' || d == '>') return false;                                      // (?= (?! (?>
-      if (d == '<' && i + 3 < p.size() && (p[i + 3] == '=' || p[i + 3] == '!')) return false;  // (?<= (?<!
+    if (c == '(') {
+      group++;
+      if (i + 2 < p.size() && p[i + 1] == '?') {
+        const char d = p[i + 2];
+        if (d == '=') return "look-ahead (?=";
+        if (d == '!') return "negative look-ahead (?!";
+        if (d == '>') return "atomic group (?>";
+        if (d == '<' && i + 3 < p.size() && p[i + 3] == '=') return "look-behind (?<=";
+        if (d == '<' && i + 3 < p.size() && p[i + 3] == '!') return "negative look-behind (?<!";
+      }
+    } else if (c == ')') {
+      if (--group < 0) return "unbalanced ')'";
     }
   }
-  return true;
+  if (cls) return "unclosed character class";
+  if (group) return "unclosed group";
+  return "";
 }
 
 // flattens parse_pre_tokenizer (src/huggingface/parsing.rs:92-190) into the supported chain:
@@ -553,9 +568,10 @@ void parse_pre_tokenizer(const ctj::Value* v, std::vector<std::pair<char, bool>>
       const ctj::Value* r = p->get("Regex");
       if (r && r->kind == ctj::Value::String) pat = r->s;
     }
-    if (rust_regex_compiles(pat))
+    if (rust_regex_rejects(pat).empty())
       throw_err(CTOK_E_UNSUPPORTED, "Split pre-tokenizer with a pattern the Rust regex crate compiles is outside the "
-                                    "encode hot path (pattern: " + pat + ")");
+                                    "encode hot path: no look-around, atomic group, backreference or unbalanced "
+                                    "group / class found, so the pattern is taken as compiling (pattern: " + pat + ")");
     chain.push_back({'S', false});
   } else if (ty == "Sequence" && depth == 0) {
     const ctj::Value* ps = v->get("pretokenizers");

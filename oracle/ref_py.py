@@ -66,8 +66,9 @@ def deserialize_merges(items):
 
 def rust_regex_compiles(pattern: str) -> bool:
     """Whether Rust `regex::Regex::new` accepts `pattern` (no look-around / backrefs / atomic
-    groups).  Token scan: escaped characters and character-class contents are literals."""
-    p, i, cls = pattern, 0, 0
+    groups, balanced groups and classes).  Token scan: escaped characters and character-class
+    contents are literals."""
+    p, i, cls, group = pattern, 0, 0, 0
     while i < len(p):
         c = p[i]
         if c == "\\":
@@ -87,12 +88,18 @@ def rust_regex_compiles(pattern: str) -> bool:
                 i += 1
             i += 1
             continue
-        if c == "(" and p[i + 1:i + 2] == "?":
-            d = p[i + 2:i + 3]
-            if d in ("=", "!", ">") or (d == "<" and p[i + 3:i + 4] in ("=", "!")):
+        if c == "(":
+            group += 1
+            if p[i + 1:i + 2] == "?":
+                d = p[i + 2:i + 3]
+                if d in ("=", "!", ">") or (d == "<" and p[i + 3:i + 4] in ("=", "!")):
+                    return False
+        elif c == ")":
+            group -= 1
+            if group < 0:
                 return False
         i += 1
-    return True
+    return cls == 0 and group == 0
 
 
 def parse_normalizer(value):

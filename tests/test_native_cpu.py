@@ -175,6 +175,7 @@ def test_shard_bounds_cover_and_balance():
     ("[(?=]x", True),                 # '(?=' inside a character class is literal
     ("\\(?=x", True),                 # escaped '(' : a literal paren, then an optional '='
     ("[^]](?=x)", False), ("(?<name>a)b", True), ("\\s+", True),
+    ("(ab", False), ("ab)", False), ("[ab", False), ("(a[)]b)", True),  # unbalanced: rejected
 ])
 def test_split_pattern_compilability(pattern, compiles):
     """A Split whose pattern Rust's regex compiles would split (unsupported here: loud error); one it
@@ -186,7 +187,7 @@ def test_split_pattern_compilability(pattern, compiles):
         split, {"type": "ByteLevel", "use_regex": False}]})
     assert ref_py.rust_regex_compiles(pattern) == compiles
     if compiles:
-        with pytest.raises(UnsupportedConfigError, match="pattern: "):  # (the refusal names the pattern)
+        with pytest.raises(UnsupportedConfigError, match="taken as compiling.*pattern: "):  # (names the pattern)
             Tokenizer.from_str(json.dumps(obj))
     else:
         Tokenizer.from_str(json.dumps(obj))

@@ -1,4 +1,6 @@
-# usage: bash /tmp/abprobe.sh CFG FIX LIB_A LIB_B  (alternating probes on one box)
+#!/bin/bash
+# Alternating kernel-only probes (tools/probe.py) of two libraries on one box.
+#   usage: bash tools/ab_probe.sh CFG FIX LIB_A LIB_B
 set -e
 for i in 1 2 3; do
   for L in $3 $4; do
