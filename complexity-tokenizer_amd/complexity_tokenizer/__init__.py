@@ -129,6 +129,10 @@ def pack_ids(batch) -> tuple[np.ndarray, np.ndarray]:
 _ID_CACHE: list = []
 
 
+# threads filling the rows of _split_lists (the CPUs this process may use, at most 16)
+_SPLIT_THREADS = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)))
+
+
 def _split_lists(flat: np.ndarray, off: np.ndarray) -> list:
     """(flat uint32 ids, uint64 offsets[D+1]) -> D Python lists, built in C (csrc/pyfast.c) from a
     shared cache of the int objects 0 .. 2^17 - 1 (ids past it are created per use).  The cyclic
@@ -142,7 +146,7 @@ def _split_lists(flat: np.ndarray, off: np.ndarray) -> list:
     was = gc.isenabled()
     gc.disable()
     try:
-        return _fast.split(flat.ctypes.data, off.ctypes.data, len(off) - 1, _ID_CACHE)
+        return _fast.split(flat.ctypes.data, off.ctypes.data, len(off) - 1, _ID_CACHE, _SPLIT_THREADS)
     finally:
         if was:
             gc.enable()
