@@ -594,7 +594,7 @@ __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(
           cls[u] = 3;
         } else {
           n[u] = el - sl[u];
-          cls[u] = generic ? 0 : n[u] > 32 ? 6 : n[u] > 16 ? 2 : n[u] > 8 ? 1 : 5;
+          cls[u] = generic ? 0 : n[u] > 32 ? (t.dbg == 31 ? 3 : 6) : n[u] > 16 ? 2 : n[u] > 8 ? 1 : 5;  // (dbg 31, A/B: 33..64 B to the wave tiers)
         }
       }
       // whole-piece probe key: the piece's raw bytes (from LDS), zero-padded to 8

@@ -49,6 +49,16 @@ for step in "$@"; do
     ablib:*)  # bench.py A/B of two libraries
       IFS=: read -r _ la lb <<< "$step"
       bash tools/ab.sh "$la" "$lb" 2>&1 | tee -a "$OUT/ablib.txt" ;;
+    abpenv:*)  # kernel-only probe A/B of the working tree's library without / with VAR=VAL: abpenv:CFG:FIX:VAR=VAL
+      IFS=: read -r _ cfg fx ev <<< "$step"
+      L=complexity-tokenizer_amd/complexity_tokenizer/libctok.so
+      for i in 1 2 3; do
+        for arm in A B; do
+          envs=""; [ $arm = B ] && envs=$ev
+          env CTOK_LIB=$L $envs timeout -k 10 300 python -u tools/probe.py "$cfg" "$fx" 5 2>/dev/null | grep MB/s \
+            | sed "s|^|$arm${envs:+ $envs} |" | tee -a "$OUT/abpenv_${cfg}.txt"
+        done
+      done ;;
     probe:*)
       IFS=: read -r _ cfg fx <<< "$step"
       timeout -k 10 300 python -u tools/probe.py "$cfg" "$fx" 5 2>&1 | tee -a "$OUT/probe_${cfg}_${fx}.txt" ;;
