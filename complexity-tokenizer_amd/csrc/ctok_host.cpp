@@ -1545,6 +1545,7 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   }
   if (!(w.nfc_watch == 1 && seg_cnt[12])) {  // (a failed NFC speculation discards this pass: nothing to launch)
     const uint32_t n_long = std::min<uint32_t>((uint32_t)seg_cnt[0], w.long_cap);
+    bool any_gmem = false;  // a long piece for the global-memory tier (its state words reserved)
     if (n_long) {
       // lengths, order and places of the long pieces, then lids / lw sized from their totals
       ds->long_pos.ensure(n_long + 8);
@@ -1559,12 +1560,13 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
       HIPTRY(hipMemcpyAsync((void*)tot, ds->long_pos.p + n_long, 4, hipMemcpyDeviceToHost, ds->side));
       HIPTRY(hipMemcpyAsync((void*)(tot + 1), ds->lw_pos.p + n_long, 4, hipMemcpyDeviceToHost, ds->side));
       spin_sync(ds, ds->side);
+      any_gmem = tot[1] != 0;
       ds->lids.ensure((uint64_t)tot[0] + 64);
       ds->lw.ensure(4 * (uint64_t)tot[1] + 64);
       w.lids = ds->lids.p;
       w.lw = ds->lw.p;
     }
-    STEP("bpe_long", launch_bpe_long(w, tb, ds->side, n_long, seg_cnt[kCtrAnyC3] != 0));
+    STEP("bpe_long", launch_bpe_long(w, tb, ds->side, n_long, seg_cnt[kCtrAnyC3] != 0, any_gmem));
   }
   HIPTRY(hipEventRecord(ds->ev_join, ds->side));
   HIPTRY(hipStreamWaitEvent(s, ds->ev_join, 0));

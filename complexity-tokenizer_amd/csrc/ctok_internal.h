@@ -59,9 +59,12 @@ constexpr uint32_t kEntDoc = 1u << 31;
 __host__ __device__ inline uint32_t list_entry(uint32_t sl, uint32_t j, uint32_t n) { return sl | (j << 12) | (n << 24); }
 __host__ __device__ inline uint32_t ent_len(uint32_t e) { return (e >> 24) & 127u; }
 __host__ __device__ inline uint32_t ent_j(uint32_t e) { return (e >> 12) & 0xFFFu; }
-// long_list entry (u64): start byte | j << 32 | kLongDoc; mid_list entry: start | j << 32 |
-// kMidDoc | n << 48.
+// long_list entry (u64): start byte | j << 32 | n << 44 | kLongDoc (n: the piece's length when
+// k_segment knows it -- its end lies within the tile's look-ahead --, else 0); mid_list entry:
+// start | j << 32 | kMidDoc | n << 48.
 constexpr uint64_t kLongDoc = 1ull << 63, kMidDoc = 1ull << 44;
+__host__ __device__ inline uint32_t long_j(uint64_t e) { return (uint32_t)(e >> 32) & 0xFFFu; }
+__host__ __device__ inline uint32_t long_len(uint64_t e) { return (uint32_t)(e >> 44) & 0x7FFFFu; }
 
 // Piece record (tcnt[tile][j], u32), written by whichever pass finishes piece j:
 //   kRecHit | id            one id, the whole-piece probe's (no scratch entry)
@@ -357,7 +360,7 @@ hipError_t launch_long_prep(const Work& w, const Tables& t, hipStream_t s, uint3
                             uint32_t* tmp, uint64_t tmp_cap);
 // long-piece tiers (side stream): n_long = k_segment's long-list length, any_c3 = a class-3
 // piece exists (the side instance of the 33..64 B pass); grids sized for them, nothing when empty
-hipError_t launch_bpe_long(const Work& w, const Tables& t, hipStream_t s, uint32_t n_long, bool any_c3);
+hipError_t launch_bpe_long(const Work& w, const Tables& t, hipStream_t s, uint32_t n_long, bool any_c3, bool any_gmem);
 hipError_t launch_emit(const Work& w, uint32_t* ids, uint64_t ids_cap, uint64_t* tok_off, hipStream_t s);
 // exclusive scan of n u32 (n read from *n_dev when non-null, else n_max); out[n] = total
 hipError_t scan_u32(const uint32_t* in, uint32_t* out, uint64_t n_max, const uint32_t* n_dev,

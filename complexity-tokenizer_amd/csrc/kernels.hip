@@ -686,8 +686,12 @@ __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(
         if (lane == leader) b = atomicAdd(&w.counters[0], (uint32_t)__popcll(lm));
         b = __builtin_amdgcn_readlane(b, leader);
         const uint32_t li = b + __popcll(lm & lanemask_lt());
-        if (cls[u] == 3 && li < w.long_cap)
-          w.long_list[li] = (uint64_t)(t0 + sl[u]) | ((uint64_t)j << 32) | (doc[u] ? kLongDoc : 0ull);
+        if (cls[u] == 3 && li < w.long_cap) {
+          // the length when the piece ends within the look-ahead (0: k_long_len finds its end)
+          const uint32_t el = s_pos[64 * u + lane + 1];
+          const uint32_t ln = el == 0xFFFFu ? 0u : min(el - sl[u], 0x7FFFFu);
+          w.long_list[li] = (uint64_t)(t0 + sl[u]) | ((uint64_t)j << 32) | ((uint64_t)ln << 44) | (doc[u] ? kLongDoc : 0ull);
+        }
         if (lane == leader && b + __popcll(lm) > w.long_cap) atomicOr(&w.counters[kCtrOverflow], 1u);
       }
     }
@@ -1824,7 +1828,7 @@ __global__ __launch_bounds__(256) void k_bpe_long(Work w, Tables t) {
   for (uint32_t li = uni(blockIdx.x * (blockDim.x >> 6) + wid); li < n_long; li += n_waves) {
     const uint64_t e = w.long_list[li];
     const uint32_t s = uni((uint32_t)e);
-    const uint32_t j = uni((uint32_t)(e >> 32) & 0xFFFFu);
+    const uint32_t j = uni(long_j(e));
     const uint32_t doc = (e & kLongDoc) ? kRecDoc : 0u;
     const uint32_t n = uni(piece_end(w, s) - s);
     // tiers: LDS up to kLdsPos positions, global memory beyond (only beyond the dense wave tiers
@@ -2576,8 +2580,10 @@ __global__ __launch_bounds__(256) void k_long_len(Work w, uint32_t* lwn, uint32_
   if (threadIdx.x < (uint32_t)kLhBuckets) s_hist[threadIdx.x] = 0;
   __syncthreads();
   for (uint32_t li = uni(blockIdx.x * 4 + (threadIdx.x >> 6)); li < n_long; li += n_waves) {
-    const uint32_t s = uni((uint32_t)w.long_list[li]);
-    const uint32_t n = uni(piece_end(w, s) - s);
+    const uint64_t e = w.long_list[li];
+    const uint32_t s = uni((uint32_t)e);
+    const uint32_t kn = uni(long_len(e));  // (k_segment's, when the piece ended within its look-ahead)
+    const uint32_t n = kn ? kn : uni(piece_end(w, s) - s);
     if (lane == 0) {
       w.long_cnt[li] = n;
       lwn[li] = n > gmin ? n : 0u;
@@ -2679,7 +2685,7 @@ __global__ __launch_bounds__(64 * NW) void k_bpe_wave(Work w, Tables t) {
     if (!SEG && n > HI) continue;
     const uint64_t e = w.long_list[li];
     const uint32_t s = uni((uint32_t)e);
-    const uint32_t j = uni((uint32_t)(e >> 32) & 0xFFFFu);
+    const uint32_t j = uni(long_j(e));
     const uint32_t doc = (e & kLongDoc) ? kRecDoc : 0u;
     uint32_t cnt;
     uint32_t* sink = &w.counters[kCtrSink];
@@ -2722,7 +2728,10 @@ hipError_t launch_long_prep(const Work& w, const Tables& t, hipStream_t s, uint3
   return scan_u32(lwn, w.lw_pos, n_long, nullptr, tmp, tmp_cap, s);
 }
 
-hipError_t launch_bpe_long(const Work& w, const Tables& t, hipStream_t s, uint32_t n_long, bool any_c3) {
+// any_gmem: some long piece is longer than the LDS tiers take (launch_long_prep's global-memory
+// state total is non-zero); without one the global-memory tier is not launched (it would still
+// find every long piece's end to skip it: 0.33 ms on C5)
+hipError_t launch_bpe_long(const Work& w, const Tables& t, hipStream_t s, uint32_t n_long, bool any_c3, bool any_gmem) {
   auto cap = [](uint32_t want, uint32_t most) { return std::max(1u, std::min(want, most)); };
   if (t.n_at != 0 || t.dbg == 7) {
     // added tokens can match inside pieces: the linked-list kernel with the added-token split.
@@ -2731,7 +2740,7 @@ hipError_t launch_bpe_long(const Work& w, const Tables& t, hipStream_t s, uint32
     if (n_long == 0) return hipSuccess;
     const size_t lds = 4 * kLdsPos * sizeof(uint32_t);
     k_bpe_long<false><<<cap(n_long, 512), 64, lds, s>>>(w, t);
-    k_bpe_long<true><<<cap((n_long + 3) / 4, 128), 256, 0, s>>>(w, t);
+    if (any_gmem) k_bpe_long<true><<<cap((n_long + 3) / 4, 128), 256, 0, s>>>(w, t);
     return hipGetLastError();
   }
   if (n_long) {
@@ -2768,7 +2777,7 @@ hipError_t launch_bpe_long(const Work& w, const Tables& t, hipStream_t s, uint32
     } else {
       HIPCHK((launch_wave<64, 1024, 2, false, true>(w, t, cap((n_long + 1) / 2, w.n_cus), s)));
     }
-    k_bpe_long<true><<<cap((n_long + 3) / 4, 128), 256, 0, s>>>(w, t);
+    if (any_gmem) k_bpe_long<true><<<cap((n_long + 3) / 4, 128), 256, 0, s>>>(w, t);
     HIPCHK(hipGetLastError());
   }
   // 33..64 B register pass, side-stream instance (see k_bpe_mid): it shares class 3 with the main
