@@ -297,8 +297,9 @@ def test_padded_nfc_splice_keeps_no_added_split(base):
     r = tok.encode_padded(ts, padding="longest")
     want = [ref.encode_to_encoding(t) for t in ts]
     for i, e in enumerate(want):
-        L = int(r["row_len"][i])
-        assert r["input_ids"][i, :L].tolist() == e.ids, repr(ts[i])
+        n = len(e.ids)  # (the row's content; padding follows)
+        assert r["input_ids"][i, :n].tolist() == e.ids, repr(ts[i])
+        assert int(r["attention_mask"][i].sum()) == n, repr(ts[i])
     got = tok.encode_batch_to_encoding(ts)
     assert [g.ids for g in got] == [e.ids for e in want]
     assert tok.encode_batch(ts) == [ref.encode(t) for t in ts]
