@@ -2835,13 +2835,28 @@ __global__ __launch_bounds__(64 * kEmitWaves) void k_emit(Work w, uint32_t* __re
   uint32_t r_first = 0;  // the current round's first id within the tile (wave-uniform)
   __shared__ uint32_t s_stage[kEmitWaves][kEmitStage];
   lds_u32* stage = (lds_u32*)s_stage[threadIdx.x >> 6];
+  // records two rounds deep: round r's are resolved (kRecList: their list slots loaded) while
+  // round r - 1 runs, and loaded while round r - 2 runs -- the extra load of a list record is off
+  // the round's critical path
   uint4 nx = load(4 * lane);
+  uint32_t cur[4];
+  {
+    const uint32_t v[4] = {nx.x, nx.y, nx.z, nx.w};
+#pragma unroll
+    for (int k = 0; k < 4; k++) cur[k] = 4 * lane + k < np ? rec_resolve(w, tile, v[k]) : v[k];
+  }
+  if (256 < np) nx = load(4 * lane + 256);
   for (uint32_t r0 = 0; r0 < np; r0 += 256) {
     const uint32_t j0 = r0 + 4 * lane;
-    uint32_t rec[4] = {nx.x, nx.y, nx.z, nx.w};
-    if (r0 + 256 < np) nx = load(j0 + 256);
+    uint32_t rec[4];
 #pragma unroll
-    for (int k = 0; k < 4; k++) rec[k] = j0 + k < np ? rec_resolve(w, tile, rec[k]) : rec[k];
+    for (int k = 0; k < 4; k++) rec[k] = cur[k];
+    if (r0 + 256 < np) {  // the next round's records, resolved now; the round after next's loaded
+      const uint32_t v[4] = {nx.x, nx.y, nx.z, nx.w};
+#pragma unroll
+      for (int k = 0; k < 4; k++) cur[k] = j0 + 256 + k < np ? rec_resolve(w, tile, v[k]) : v[k];
+      if (r0 + 512 < np) nx = load(j0 + 512);
+    }
     uint32_t c[4], sum = 0;
 #pragma unroll
     for (int k = 0; k < 4; k++) {

@@ -66,6 +66,15 @@ def shuffled_merges(base_obj, seed):
     return derived(base_obj, m)
 
 
+def with_invalid_merge_in_front(base_obj):
+    """One merge whose parts are not in the vocab, in front: every valid merge's rank shifts by one
+    (src/bpe.rs:60-69), so a merge's new id is the previous merge's and the last valid merge panics
+    when used (src/bpe.rs:141); tokens then need not spell their strings (window rounds off)."""
+    def m(o):
+        o["model"]["merges"] = ["zzq0 qqz0"] + list(o["model"]["merges"])
+    return derived(base_obj, m)
+
+
 def with_invalid_merges(base_obj, seed, n_bad=50, tail_only=False):
     """Insert merges whose parts are not in the vocab: shifts BpeTokenizer.merges indices
     (reference src/bpe.rs:60-69 quirk); ranks past the valid list make lookups panic."""

@@ -42,7 +42,7 @@ for step in "$@"; do
       IFS=: read -r _ cfg fx la lb <<< "$step"
       for i in 1 2 3; do
         for L in "$la" "$lb"; do
-          CTOK_LIB=$L timeout -k 10 300 python -u tools/probe.py "$cfg" "$fx" 5 2>/dev/null | grep MB/s | sed "s|^|$(basename "$L") |" \
+          CTOK_LIB=$L timeout -k 10 300 python -u tools/probe.py "$cfg" "$fx" 5 2>/dev/null | grep -E "MB/s|ms_" | sed "s|^|$(basename "$L") |" \
             | tee -a "$OUT/ab_${cfg}_${fx}.txt"
         done
       done ;;
