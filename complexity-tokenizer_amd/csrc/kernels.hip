@@ -663,12 +663,11 @@ __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(
         if (cls[u] == 1) w.list1[(size_t)tile * kCap1 + q1] = e;
         if (cls[u] == 2) w.list2[(size_t)tile * kCap2 + q2] = e;
         if (cls[u] == 6) w.list3[(size_t)tile * kCap3 + q3] = e;
-        // the piece's record (every piece's slot: whole coalesced lines): a class-list piece
-        // points at its list slot, where its merge pass leaves count | pos (Work::lrec)
+        // the piece's record (every piece's slot: whole coalesced lines): a class-0/1 piece
+        // points at its list slot, where k_bpe_short leaves count | pos (Work::lrec)
         if (w.lrec && !generic) {
           const uint32_t dr = doc[u] ? kRecDoc : 0u;
-          rec[u] = cls[u] == 0 ? rec_list(0, q0) | dr : cls[u] == 1 ? rec_list(1, q1) | dr
-                 : cls[u] == 2 ? rec_list(2, q2) | dr : cls[u] == 6 ? rec_list(3, q3) | dr : rec[u];
+          rec[u] = cls[u] == 0 ? rec_list(0, q0) | dr : cls[u] == 1 ? rec_list(1, q1) | dr : rec[u];
         }
         if (j < np) tcnt[j] = rec[u];
         by0 += cls[u] == 0 ? n[u] : 0u;
@@ -1297,15 +1296,16 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
       }
       __syncthreads();
     }
-    auto entry = [&](uint32_t i, uint32_t& kt, uint32_t& qi) {
+    auto entry = [&](uint32_t i, uint32_t& kt) {
       const uint32_t q = sorted ? (uint32_t)S.perm[i] : i;
       kt = tile_of<K>(S.pre, q);
-      qi = q - S.pre[kt];  // (index in the tile's list: where the record goes, Work::lrec)
-      return list[(size_t)(c0 + kt) * cap + qi];
+      return list[(size_t)(c0 + kt) * cap + (q - S.pre[kt])];
     };
     auto start_of = [&](uint32_t e, uint32_t kt) { return (c0 + kt) * kTile + (e & 0xFFFu); };
     // one piece: list entry e of chunk tile kt, its first N bytes in wv
-    auto body = [&](uint32_t e, uint32_t kt, uint32_t qi, const uint32_t* wv) {
+    // (i: the piece's entry in the chunk; its list slot is found again from LDS when the record is
+    // stored, so that no register holds it through the merges)
+    auto body = [&](uint32_t e, uint32_t kt, uint32_t i, const uint32_t* wv) {
         const uint32_t tile = c0 + kt;
         const uint32_t s = tile * kTile + (e & 0xFFFu);
         const uint32_t j = ent_j(e);
@@ -1371,8 +1371,11 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
             if ((uint32_t)k < m) out[k] = tk[k];
         }
         if (t.dbg != 30) {  // (A/B measurement only: 30 drops the record stores, ids wrong)
-          if (w.lrec)  // the list slot the piece came from (k_segment's record points at it)
+          if (N <= 16 && w.lrec) {  // the list slot the piece came from (k_segment's record points at it;
+                                    // classes 0 and 1 only: the sparse classes keep tcnt records)
+            const uint32_t qi = (sorted ? (uint32_t)S.perm[i] : i) - S.pre[kt];
             const_cast<uint32_t*>(list)[(size_t)tile * cap + qi] = rec_short(m, pos);
+          }
           else
             w.tcnt[(size_t)tile * kTileSlots + j] = rec_short(m, pos) | ((e & kEntDoc) ? kRecDoc : 0u);
         }
@@ -1382,11 +1385,11 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
     if constexpr (N > 32) {
       // 64 slots: no registers to spare for a pipeline; a static stride over the chunk
       for (uint32_t i = tid; i < E; i += NT) {
-        uint32_t kt, qi;
-        const uint32_t e = entry(i, kt, qi);
+        uint32_t kt;
+        const uint32_t e = entry(i, kt);
         uint32_t wv[N / 4];
         load_words<N / 4>(w.text, start_of(e, kt), w.n_bytes, wv);
-        body(e, kt, qi, wv);
+        body(e, kt, i, wv);
       }
     } else {
       // Each wavefront takes blocks of 64 entries from S.next (one LDS atomic per block): a wave
@@ -1402,30 +1405,29 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
         return uni((uint32_t)__shfl((int)b, 0, 64));
       };
       constexpr int kPw = N / 4;
-      uint32_t e0 = 0, kt0 = 0, q0 = 0, e1 = 0, kt1 = 0, q1 = 0;
+      uint32_t e0 = 0, kt0 = 0, e1 = 0, kt1 = 0;
       uint32_t wv0[kPw];
       uint32_t b0 = take();
       uint32_t b1 = b0 < E ? take() : E;
       if (b0 + lane < E) {
-        e0 = entry(b0 + lane, kt0, q0);
+        e0 = entry(b0 + lane, kt0);
         load_words<kPw>(w.text, start_of(e0, kt0), w.n_bytes, wv0);
       }
-      if (b1 + lane < E) e1 = entry(b1 + lane, kt1, q1);
+      if (b1 + lane < E) e1 = entry(b1 + lane, kt1);
       while (b0 < E) {  // wave-uniform
         const uint32_t i = b0 + lane;
         const uint32_t b2 = b1 < E ? take() : E;
-        const uint32_t e = e0, kt = kt0, qi = q0;
+        const uint32_t e = e0, kt = kt0;
         uint32_t wv[N / 4];
 #pragma unroll
         for (int k = 0; k < N / 4; k++) wv[k] = wv0[k];
         e0 = e1;
         kt0 = kt1;
-        q0 = q1;
         if (b1 + lane < E) load_words<kPw>(w.text, start_of(e0, kt0), w.n_bytes, wv0);
-        if (b2 + lane < E) e1 = entry(b2 + lane, kt1, q1);
+        if (b2 + lane < E) e1 = entry(b2 + lane, kt1);
         b0 = b1;
         b1 = b2;
-        if (i < E) body(e, kt, qi, wv);
+        if (i < E) body(e, kt, i, wv);
       }
     }
     tile_share_flush<K>(w, c0, tb1, S.tsum, S.tbase, LC::cls);

@@ -65,6 +65,10 @@ for step in "$@"; do
     probe:*)
       IFS=: read -r _ cfg fx <<< "$step"
       timeout -k 10 300 python -u tools/probe.py "$cfg" "$fx" 5 2>&1 | tee -a "$OUT/probe_${cfg}_${fx}.txt" ;;
+    trainer)  # GPU trainer vs the C restatement of the reference's per-merge work
+      timeout -k 10 600 python -u tools/trainer_timing.py > "$OUT/trainer_timing.json" 2> "$OUT/trainer_timing.log" \
+        || { tail -20 "$OUT/trainer_timing.log"; exit 1; }
+      cat "$OUT/trainer_timing.json" ;;
     matrix)
       timeout -k 10 900 python -u tools/bench_matrix.py > "$OUT/matrix.json" 2> "$OUT/matrix.log" || { tail -20 "$OUT/matrix.log"; exit 1; }
       tail -5 "$OUT/matrix.log" ;;
