@@ -1147,6 +1147,46 @@ __device__ __forceinline__ bool merge_slots(const Tables& t, const PairLds& P, u
   }
 }
 
+// merge_slots for compact tables over a narrow vocabulary (every id and every merge value < 0xFFFF):
+// a slot holds its token and the rank of the pair it starts in one register, rank << 16 | token
+// (0xFFFF: none), so N slots take N registers instead of 2N and a shift moves one value.  Same
+// semantics: the lowest (rank, position) pair merges (src/bpe.rs:118-149).  (The 33..64 B pass
+// spilled at 2N registers per thread.)
+template <int N, bool HOT>
+__device__ __forceinline__ bool merge_packed(const Tables& t, const PairLds& P, uint32_t* pk, uint32_t& m,
+                                             uint32_t stop, uint32_t* err) {
+  for (;;) {
+    if (m <= stop) return true;
+    uint32_t key = ~0u;  // rank << 16 | position
+#pragma unroll
+    for (int k = 0; k < N - 1; k++) key = min(key, (pk[k] & 0xFFFF0000u) | (uint32_t)k);
+    if (key >= 0xFFFF0000u) return false;
+    const uint32_t nid = key >> 16, bi = key & 63u;  // (compact: the value is the new id)
+    uint32_t L = 0, R = 0;
+#pragma unroll
+    for (int k = 0; k < N; k++) {
+      L = ((uint32_t)k + 1 == bi) ? pk[k] : L;
+      R = ((uint32_t)k == bi + 2) ? pk[k] : R;
+    }
+    const bool has_l = bi > 0, has_r = bi + 2 < m;
+    Probe<true, HOT> pl, pr;
+    pl.start(t, P, L & 0xFFFFu, nid, has_l);
+    pr.start(t, P, nid, R & 0xFFFFu, has_r);
+#pragma unroll
+    for (int k = 0; k < N; k++) {  // ascending: pk[k+1] is read before it is overwritten
+      const uint32_t nxt = k + 1 < N ? pk[k + 1] : ~0u;
+      pk[k] = (uint32_t)k > bi ? nxt : ((uint32_t)k == bi ? nid : pk[k]);
+    }
+    m--;
+    const uint32_t rl = has_l ? pl.finish(t, err) : kNoRank;
+    const uint32_t rr = has_r ? pr.finish(t, err) : kNoRank;
+    const uint32_t hl = (rl >= 0xFFFFu ? 0xFFFFu : rl) << 16, hr = (rr >= 0xFFFFu ? 0xFFFFu : rr) << 16;
+#pragma unroll
+    for (int k = 0; k < N - 1; k++)
+      pk[k] = ((uint32_t)k + 1 == bi) ? ((pk[k] & 0xFFFFu) | hl) : ((uint32_t)k == bi ? ((pk[k] & 0xFFFFu) | hr) : pk[k]);
+  }
+}
+
 // The last tier (<= 8 tokens) with the working state in LDS instead of registers: positions stay
 // fixed, a live mask says which slots still hold a token, and slot s keeps the key
 // rank << 3 | s of the pair its token starts (~0 when the slot is dead or last).  A merge then
@@ -1310,6 +1350,77 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
         const uint32_t s = tile * kTile + (e & 0xFFFu);
         const uint32_t j = ent_j(e);
         const uint32_t n = ent_len(e);
+        // ids go to the next free slots of the tile's region for this class (dense: a wave's
+        // stores fill whole lines), the record points at them
+        uint32_t pos = 0;
+        auto out_of = [&](uint32_t mm) {
+          pos = atomicAdd(&S.tsum[kt], mm);
+          return w.scratch + (size_t)tile * kTileSlots + pos;
+        };
+        auto store_rec = [&](uint32_t mm) {
+          if (t.dbg == 30) return;  // (A/B measurement only: 30 drops the record stores, ids wrong)
+          if (N <= 16 && w.lrec) {  // the list slot the piece came from (k_segment's record points at it;
+                                    // classes 0 and 1 only: the sparse classes keep tcnt records)
+            const uint32_t qi = (sorted ? (uint32_t)S.perm[i] : i) - S.pre[kt];
+            const_cast<uint32_t*>(list)[(size_t)tile * cap + qi] = rec_short(mm, pos);
+          } else {
+            w.tcnt[(size_t)tile * kTileSlots + j] = rec_short(mm, pos) | ((e & kEntDoc) ? kRecDoc : 0u);
+          }
+        };
+        auto to_mid = [&]() {  // a byte char absent from the vocab is dropped: generic path
+          const uint32_t mi = atomicAdd(&w.counters[4], 1u);
+          if (mi < w.mid_cap)
+            w.mid_list[mi] = (uint64_t)s | ((uint64_t)j << 32) | ((uint64_t)n << 48) | ((e & kEntDoc) ? kMidDoc : 0ull);
+          else
+            atomicOr(&w.counters[kCtrOverflow], 1u);
+        };
+        if constexpr (COMPACT && L8 && N >= 32) {
+          // packed slots (merge_packed): the 17..64 B passes of narrow vocabularies
+          uint32_t pk[N];
+          bool missing = false;
+#pragma unroll
+          for (int k = 0; k < N; k++) {
+            const int32_t id = s_b2id[byte_of(wv[k >> 2], k)];
+            missing |= ((uint32_t)k < n) & (id < 0);
+            pk[k] = (uint32_t)k < n ? ((uint32_t)id & 0xFFFFu) : 0xFFFFu;
+          }
+          if (missing) {
+            to_mid();
+            return;
+          }
+#pragma unroll
+          for (int k = 0; k < N - 1; k++) {
+            const uint32_t r = t.pair0[(byte_of(wv[k >> 2], k) << 8) | byte_of(wv[(k + 1) >> 2], k + 1)];
+            const bool live = (uint32_t)k + 1 < n;
+            if (live && r != kNoRank && value_panics(t, r)) atomicOr(err, kErrPanic);
+            const uint32_t h = (live && r < 0xFFFFu) ? r : 0xFFFFu;  // (a panicking value is not < 0xFFFF)
+            pk[k] |= h << 16;
+          }
+          pk[N - 1] |= 0xFFFF0000u;
+          uint32_t m = n;
+          bool more = true;
+          if constexpr (N >= 64) more = merge_packed<64, HOT>(t, P, pk, m, 32, err);
+          if (more) more = merge_packed<32, HOT>(t, P, pk, m, 16, err);
+          if (more) more = merge_packed<16, HOT>(t, P, pk, m, 8, err);
+          if (more) {
+            uint32_t tk8[8], rk8[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+              tk8[k] = pk[k] & 0xFFFFu;
+              rk8[k] = (pk[k] >> 16) == 0xFFFFu ? kNoRank : (pk[k] >> 16);
+            }
+            m = merge_lds8<COMPACT, HOT, NT>(t, P, tk8, rk8, m, s_key, s_tok, err, out_of);
+          } else {
+            uint32_t* out = out_of(m);
+#pragma unroll
+            for (int k = 0; k < N; k++)
+              if ((uint32_t)k < m) out[k] = pk[k] & 0xFFFFu;
+          }
+          store_rec(m);
+          st_bytes += n;
+          st_ids += m;
+          return;
+        }
         uint32_t tk[N], rk[N];
         bool missing = false;
         {
@@ -1320,12 +1431,8 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
             tk[k] = (uint32_t)id;
           }
         }
-        if (missing) {  // a byte char absent from the vocab is dropped: generic path
-          const uint32_t mi = atomicAdd(&w.counters[4], 1u);
-          if (mi < w.mid_cap)
-            w.mid_list[mi] = (uint64_t)s | ((uint64_t)j << 32) | ((uint64_t)n << 48) | ((e & kEntDoc) ? kMidDoc : 0ull);
-          else
-            atomicOr(&w.counters[kCtrOverflow], 1u);
+        if (missing) {
+          to_mid();
           return;
         }
         // initial pair ranks: every initial pair is a byte pair, one load each from the 256 x 256
@@ -1354,13 +1461,6 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
         if constexpr (N >= 16) {
           if (more) more = merge_slots<16, COMPACT, HOT, L8>(t, P, tk, rk, m, 8, err);
         }
-        // ids go to the next free slots of the tile's region for this class (dense: a wave's
-        // stores fill whole lines), the record points at them
-        uint32_t pos = 0;
-        auto out_of = [&](uint32_t mm) {
-          pos = atomicAdd(&S.tsum[kt], mm);
-          return w.scratch + (size_t)tile * kTileSlots + pos;
-        };
         if (L8 && more) {
           m = merge_lds8<COMPACT, HOT, NT>(t, P, tk, rk, m, s_key, s_tok, err, out_of);
         } else {
@@ -1370,15 +1470,7 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
           for (int k = 0; k < N; k++)
             if ((uint32_t)k < m) out[k] = tk[k];
         }
-        if (t.dbg != 30) {  // (A/B measurement only: 30 drops the record stores, ids wrong)
-          if (N <= 16 && w.lrec) {  // the list slot the piece came from (k_segment's record points at it;
-                                    // classes 0 and 1 only: the sparse classes keep tcnt records)
-            const uint32_t qi = (sorted ? (uint32_t)S.perm[i] : i) - S.pre[kt];
-            const_cast<uint32_t*>(list)[(size_t)tile * cap + qi] = rec_short(m, pos);
-          }
-          else
-            w.tcnt[(size_t)tile * kTileSlots + j] = rec_short(m, pos) | ((e & kEntDoc) ? kRecDoc : 0u);
-        }
+        store_rec(m);
         st_bytes += n;
         st_ids += m;
     };
@@ -1499,17 +1591,25 @@ __global__ __launch_bounds__(1024) void k_bpe_short(Work w, Tables t) {
 // stream's passes, and a large class 3 (multilingual text) is shared by both as CUs free up.
 // Most tiles per chunk of the 17..32 B / 33..64 B passes: these classes can be sparse (C4: ~5
 // class-2 pieces per tile), where 64 tiles left most of a 512-thread workgroup idle per chunk.
-template <int CLS> struct MidCfg { static constexpr int KT = 256; };
+// Threads per workgroup: 512 (two waves per SIMD at <= 256 VGPRs); the packed 32-slot pass of
+// narrow compact tables (merge_packed, ~126 VGPRs) runs 768 (three waves per SIMD; its LDS: the
+// image, 36 KiB of merge_lds8 state and the pass scratch, ~153 KiB)
+template <int CLS, bool COMPACT, bool NARROW> struct MidCfg {
+  static constexpr int KT = 256;
+  static constexpr uint32_t NT = (CLS == 2 && COMPACT && NARROW) ? 768 : 512;
+};
 
 template <bool COMPACT, int CLS, bool NARROW>
-__global__ __launch_bounds__(512) void k_bpe_mid(Work w, Tables t) {
+__global__ __launch_bounds__((MidCfg<CLS, COMPACT, NARROW>::NT)) void k_bpe_mid(Work w, Tables t) {
   if (spec_failed(w)) return;
-  constexpr int KT = MidCfg<CLS>::KT;
+  using Cfg = MidCfg<CLS, COMPACT, NARROW>;
+  constexpr int KT = Cfg::KT;
+  constexpr uint32_t NT = Cfg::NT;
   extern __shared__ __attribute__((aligned(16))) uint4 s_img[];
   __shared__ int32_t s_b2id[256];
   __shared__ PassLds<kSortCap, KT> S;
-  __shared__ uint32_t s_key[NARROW ? 8 * 512 : 1];
-  __shared__ uint16_t s_tok[NARROW ? 8 * 512 : 1];
+  __shared__ uint32_t s_key[NARROW ? 8 * NT : 1];
+  __shared__ uint16_t s_tok[NARROW ? 8 * NT : 1];
   // (the image is loaded up front: a lazy load pushes the 64-slot pass into scratch; the kernel
   // returns at once when k_segment found no piece of its class)
   if (w.counters[CLS == 2 ? kCtrAnyMid : kCtrAnyC3] == 0) return;
@@ -1522,12 +1622,12 @@ __global__ __launch_bounds__(512) void k_bpe_mid(Work w, Tables t) {
   if (!s_left) return;
   const uint32_t tid = threadIdx.x;
   const uint4* img = NARROW ? t.lds16_image : t.lds_image;
-  for (uint32_t i = tid; i < kLdsImageBytes / 16; i += 512) s_img[i] = img[i];
-  for (uint32_t i = tid; i < 256; i += 512) s_b2id[i] = t.byte2id[i];
+  for (uint32_t i = tid; i < kLdsImageBytes / 16; i += NT) s_img[i] = img[i];
+  for (uint32_t i = tid; i < 256; i += NT) s_b2id[i] = t.byte2id[i];
   bool loaded = true;
   const PairLds P{(const lds_u64*)s_img, (const lds_u32*)(s_img + kHotBuckets)};
-  class_pass<CLS == 2 ? 32 : 64, COMPACT, true, 512, kSortCap, NARROW, KT>(w, t, P, s_b2id, S, loaded, [] {},
-                                                                         (lds_u32*)s_key, (lds_u16*)s_tok);
+  class_pass<CLS == 2 ? 32 : 64, COMPACT, true, NT, kSortCap, NARROW, KT>(w, t, P, s_b2id, S, loaded, [] {},
+                                                                        (lds_u32*)s_key, (lds_u16*)s_tok);
 }
 
 // hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device): the attribute is set
@@ -1553,7 +1653,7 @@ static hipError_t launch_mid_t(const Work& w, const Tables& t, hipStream_t s) {
   static LdsAttr attr;
   HIPCHK(lds_attr_once(attr, (const void*)k_bpe_mid<C, CLS, NW>, kLdsImageBytes));
   if (!w.n_tiles) return hipSuccess;
-  k_bpe_mid<C, CLS, NW><<<min((w.n_tiles + w.unit - 1) / w.unit, w.n_cus), 512, kLdsImageBytes, s>>>(w, t);
+  k_bpe_mid<C, CLS, NW><<<min((w.n_tiles + w.unit - 1) / w.unit, w.n_cus), MidCfg<CLS, C, NW>::NT, kLdsImageBytes, s>>>(w, t);
   return hipGetLastError();
 }
 template <bool C, int CLS>
