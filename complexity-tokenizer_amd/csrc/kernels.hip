@@ -1152,6 +1152,11 @@ __device__ __forceinline__ bool merge_slots(const Tables& t, const PairLds& P, u
 // (0xFFFF: none), so N slots take N registers instead of 2N and a shift moves one value.  Same
 // semantics: the lowest (rank, position) pair merges (src/bpe.rs:118-149).  (The 33..64 B pass
 // spilled at 2N registers per thread.)
+#ifndef CTOK_PACK_MIN
+#define CTOK_PACK_MIN 32
+#endif
+constexpr int kPackMin = CTOK_PACK_MIN;  // slot counts >= this use merge_packed (narrow compact tables)
+
 template <int N, bool HOT>
 __device__ __forceinline__ bool merge_packed(const Tables& t, const PairLds& P, uint32_t* pk, uint32_t& m,
                                              uint32_t stop, uint32_t* err) {
@@ -1374,7 +1379,7 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
           else
             atomicOr(&w.counters[kCtrOverflow], 1u);
         };
-        if constexpr (COMPACT && L8 && N >= 32) {
+        if constexpr (COMPACT && L8 && N >= kPackMin) {
           // packed slots (merge_packed): the 17..64 B passes of narrow vocabularies
           uint32_t pk[N];
           bool missing = false;
@@ -1400,7 +1405,9 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
           uint32_t m = n;
           bool more = true;
           if constexpr (N >= 64) more = merge_packed<64, HOT>(t, P, pk, m, 32, err);
-          if (more) more = merge_packed<32, HOT>(t, P, pk, m, 16, err);
+          if constexpr (N >= 32) {
+            if (more) more = merge_packed<32, HOT>(t, P, pk, m, 16, err);
+          }
           if (more) more = merge_packed<16, HOT>(t, P, pk, m, 8, err);
           if (more) {
             uint32_t tk8[8], rk8[8];
