@@ -1440,10 +1440,6 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
     w.nfc_bits = ds->nfc_bits.p;
   }
   w.keep_first = keep_first ? 1u : 0u;
-  // records of class-list pieces in their list slots (Work::lrec): CTOK_LIST_REC=1 (A/B; off by
-  // default until it measures faster end to end)
-  static const bool lrec = getenv("CTOK_LIST_REC") != nullptr && getenv("CTOK_NO_LIST_REC") == nullptr;
-  w.lrec = (lrec && tb.dbg != 30) ? 1u : 0u;  // (dbg 30 drops the tcnt record stores: placeholders stay 0)
   const size_t nt = w.n_tiles;
   ds->docbits.ensure(w.n_words + 8);
   ds->pbits.ensure(w.n_words + 8);

@@ -74,10 +74,7 @@ __host__ __device__ inline uint32_t long_len(uint64_t e) { return (uint32_t)(e >
 //                           for the piece's length class, see tregion)
 // | kRecDoc when the piece starts a document: k_emit then leaves the piece's first id within the
 // tile in its slot (for k_tokoff).
-//   kRecList | cls << 12 | q  a piece of class list cls (0..3) at index q of its tile's list (k_segment,
-//                           Work::lrec): the pass that merges it writes count | pos << 16 into that
-//                           list slot (consecutive slots: whole lines), not here
-constexpr uint32_t kRecHit = 0x80000000u, kRecLong = 0x40000000u, kRecDoc = 0x20000000u, kRecList = 0x10000000u;
+constexpr uint32_t kRecHit = 0x80000000u, kRecLong = 0x40000000u, kRecDoc = 0x20000000u;
 constexpr uint32_t kRecIdMask = (1u << kIdBits) - 1u, kRecLongMask = kRecDoc - 1u;
 // Per-tile id regions of the register merge passes in scratch (kTileSlots u32 per tile): class c
 // (c = 0..3) starts at the total bytes of the tile's class lists < c (ids <= bytes), packed as
@@ -86,7 +83,6 @@ __host__ __device__ inline uint32_t region_base(uint2 r, int cls) {
   return cls <= 0 ? 0u : cls == 1 ? (r.x & 0xFFFFu) : cls == 2 ? (r.x >> 16) : r.y;
 }
 __host__ __device__ inline uint32_t rec_short(uint32_t count, uint32_t sl) { return count | (sl << 16); }
-__host__ __device__ inline uint32_t rec_list(uint32_t cls, uint32_t q) { return kRecList | (cls << 12) | q; }
 
 // 24-bit multiply (v_mul_u32_u24: full rate; a 32-bit v_mul_lo_u32 is quarter rate on CDNA)
 __host__ __device__ inline uint32_t mul24(uint32_t a, uint32_t b) {
@@ -233,7 +229,6 @@ struct Work {              // device pointers, sized by the host for one call
                            // NFC might change (zeroed by the host; nfc_splice flags docs from it)
   uint32_t keep_first;     // 1: k_emit leaves every piece's first id within its tile in tcnt (not
                            // only doc-start pieces'), for ctok_encode_offsets
-  uint32_t lrec;           // 1: class-list pieces' records go to their list slots (kRecList in tcnt)
   uint16_t* wpref;         // [n_tiles * 64] pieces of the tile before each 64-byte word
   uint32_t* tile_np;       // [n_tiles] pieces starting in the tile
   uint32_t* tile_tok;      // [n_tiles + 1] tokens per tile, scanned in place to the tile's first id

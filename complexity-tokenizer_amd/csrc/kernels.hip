@@ -594,7 +594,7 @@ __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(
           cls[u] = 3;
         } else {
           n[u] = el - sl[u];
-          cls[u] = generic ? 0 : n[u] > 32 ? (t.dbg == 31 ? 3 : 6) : n[u] > 16 ? 2 : n[u] > 8 ? 1 : 5;  // (dbg 31, A/B: 33..64 B to the wave tiers)
+          cls[u] = generic ? 0 : n[u] > 32 ? 6 : n[u] > 16 ? 2 : n[u] > 8 ? 1 : 5;
         }
       }
       // whole-piece probe key: the piece's raw bytes (from LDS), zero-padded to 8
@@ -609,7 +609,7 @@ __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(
     }
     // all first probes in flight together (unrolled by hand: a loop over u around the probing
     // loop would not unroll, and the arrays would go to scratch)
-    uint32_t hitv[U], rec[U];
+    uint32_t hitv[U];
 #define CTOK_PROBE_LOAD(u) const uint4 e##u = t.piece_tab[h[u]];
 #define CTOK_PROBE_USE(u) hitv[u] = piece_probe(t, e##u, h[u], plo[u], phi[u], n[u]);
     static_assert(U == 4 || U == 8, "kSegUnroll: 4 or 8");
@@ -623,15 +623,17 @@ __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(
 #undef CTOK_PROBE_USE
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      rec[u] = 0;  // placeholder, rewritten by the pass that merges the piece
+      const uint32_t j = j0 + 64 * u + lane;
+      uint32_t rec = 0;  // placeholder, rewritten by the pass that merges the piece
       // (written as flag arithmetic: an if / else-if chain assigning cls[u] in each arm was
       // miscompiled by this hipcc in the unrolled loop)
       if (cls[u] == 5) {
         const bool hit = hitv[u] != kNone;
-        rec[u] = hit ? kRecHit | hitv[u] | (doc[u] ? kRecDoc : 0u) : 0u;
+        rec = hit ? kRecHit | hitv[u] | (doc[u] ? kRecDoc : 0u) : 0u;
         hits += hit ? 1u : 0u;
         cls[u] = hit ? 4u : 0u;
       }
+      if (j < np) tcnt[j] = rec;  // every piece's slot: whole coalesced lines
     }
     {  // the tile's class-0 list is full: the rest of its class-0 pieces go to the long list (one
        // uniform test per round; the per-piece fix-up only in the rare round that crosses w.k0)
@@ -657,19 +659,10 @@ __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(
         const uint64_t m1 = __ballot(cls[u] == 1), m2 = __ballot(cls[u] == 2);
         const uint64_t m3 = __ballot(cls[u] == 6);
         const uint64_t below = lanemask_lt();
-        const uint32_t q0 = n0 + __popcll(m0 & below), q1 = n1 + __popcll(m1 & below);
-        const uint32_t q2 = n2 + __popcll(m2 & below), q3 = n3 + __popcll(m3 & below);
-        if (cls[u] == 0) w.list0[(size_t)tile * w.k0 + q0] = e;
-        if (cls[u] == 1) w.list1[(size_t)tile * kCap1 + q1] = e;
-        if (cls[u] == 2) w.list2[(size_t)tile * kCap2 + q2] = e;
-        if (cls[u] == 6) w.list3[(size_t)tile * kCap3 + q3] = e;
-        // the piece's record (every piece's slot: whole coalesced lines): a class-0/1 piece
-        // points at its list slot, where k_bpe_short leaves count | pos (Work::lrec)
-        if (w.lrec && !generic) {
-          const uint32_t dr = doc[u] ? kRecDoc : 0u;
-          rec[u] = cls[u] == 0 ? rec_list(0, q0) | dr : cls[u] == 1 ? rec_list(1, q1) | dr : rec[u];
-        }
-        if (j < np) tcnt[j] = rec[u];
+        if (cls[u] == 0) w.list0[(size_t)tile * w.k0 + n0 + __popcll(m0 & below)] = e;
+        if (cls[u] == 1) w.list1[(size_t)tile * kCap1 + n1 + __popcll(m1 & below)] = e;
+        if (cls[u] == 2) w.list2[(size_t)tile * kCap2 + n2 + __popcll(m2 & below)] = e;
+        if (cls[u] == 6) w.list3[(size_t)tile * kCap3 + n3 + __popcll(m3 & below)] = e;
         by0 += cls[u] == 0 ? n[u] : 0u;
         by1 += cls[u] == 1 ? n[u] : 0u;
         by2 += cls[u] == 2 ? n[u] : 0u;
@@ -685,7 +678,8 @@ __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(
         if (lane == leader) b = atomicAdd(&w.counters[0], (uint32_t)__popcll(lm));
         b = __builtin_amdgcn_readlane(b, leader);
         const uint32_t li = b + __popcll(lm & lanemask_lt());
-        if (cls[u] == 3 && li < w.long_cap) {
+        if (cls[u] == 3 && li < w.long_cap)
+        {
           // the length when the piece ends within the look-ahead (0: k_long_len finds its end)
           const uint32_t el = s_pos[64 * u + lane + 1];
           const uint32_t ln = el == 0xFFFFu ? 0u : min(el - sl[u], 0x7FFFFu);
@@ -1147,51 +1141,6 @@ __device__ __forceinline__ bool merge_slots(const Tables& t, const PairLds& P, u
   }
 }
 
-// merge_slots for compact tables over a narrow vocabulary (every id and every merge value < 0xFFFF):
-// a slot holds its token and the rank of the pair it starts in one register, rank << 16 | token
-// (0xFFFF: none), so N slots take N registers instead of 2N and a shift moves one value.  Same
-// semantics: the lowest (rank, position) pair merges (src/bpe.rs:118-149).  (The 33..64 B pass
-// spilled at 2N registers per thread.)
-#ifndef CTOK_PACK_MIN
-#define CTOK_PACK_MIN 32
-#endif
-constexpr int kPackMin = CTOK_PACK_MIN;  // slot counts >= this use merge_packed (narrow compact tables)
-
-template <int N, bool HOT>
-__device__ __forceinline__ bool merge_packed(const Tables& t, const PairLds& P, uint32_t* pk, uint32_t& m,
-                                             uint32_t stop, uint32_t* err) {
-  for (;;) {
-    if (m <= stop) return true;
-    uint32_t key = ~0u;  // rank << 16 | position
-#pragma unroll
-    for (int k = 0; k < N - 1; k++) key = min(key, (pk[k] & 0xFFFF0000u) | (uint32_t)k);
-    if (key >= 0xFFFF0000u) return false;
-    const uint32_t nid = key >> 16, bi = key & 63u;  // (compact: the value is the new id)
-    uint32_t L = 0, R = 0;
-#pragma unroll
-    for (int k = 0; k < N; k++) {
-      L = ((uint32_t)k + 1 == bi) ? pk[k] : L;
-      R = ((uint32_t)k == bi + 2) ? pk[k] : R;
-    }
-    const bool has_l = bi > 0, has_r = bi + 2 < m;
-    Probe<true, HOT> pl, pr;
-    pl.start(t, P, L & 0xFFFFu, nid, has_l);
-    pr.start(t, P, nid, R & 0xFFFFu, has_r);
-#pragma unroll
-    for (int k = 0; k < N; k++) {  // ascending: pk[k+1] is read before it is overwritten
-      const uint32_t nxt = k + 1 < N ? pk[k + 1] : ~0u;
-      pk[k] = (uint32_t)k > bi ? nxt : ((uint32_t)k == bi ? nid : pk[k]);
-    }
-    m--;
-    const uint32_t rl = has_l ? pl.finish(t, err) : kNoRank;
-    const uint32_t rr = has_r ? pr.finish(t, err) : kNoRank;
-    const uint32_t hl = (rl >= 0xFFFFu ? 0xFFFFu : rl) << 16, hr = (rr >= 0xFFFFu ? 0xFFFFu : rr) << 16;
-#pragma unroll
-    for (int k = 0; k < N - 1; k++)
-      pk[k] = ((uint32_t)k + 1 == bi) ? ((pk[k] & 0xFFFFu) | hl) : ((uint32_t)k == bi ? ((pk[k] & 0xFFFFu) | hr) : pk[k]);
-  }
-}
-
 // The last tier (<= 8 tokens) with the working state in LDS instead of registers: positions stay
 // fixed, a live mask says which slots still hold a token, and slot s keeps the key
 // rank << 3 | s of the pair its token starts (~0 when the slot is dead or last).  A merge then
@@ -1348,86 +1297,11 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
     };
     auto start_of = [&](uint32_t e, uint32_t kt) { return (c0 + kt) * kTile + (e & 0xFFFu); };
     // one piece: list entry e of chunk tile kt, its first N bytes in wv
-    // (i: the piece's entry in the chunk; its list slot is found again from LDS when the record is
-    // stored, so that no register holds it through the merges)
-    auto body = [&](uint32_t e, uint32_t kt, uint32_t i, const uint32_t* wv) {
+    auto body = [&](uint32_t e, uint32_t kt, const uint32_t* wv) {
         const uint32_t tile = c0 + kt;
         const uint32_t s = tile * kTile + (e & 0xFFFu);
         const uint32_t j = ent_j(e);
         const uint32_t n = ent_len(e);
-        // ids go to the next free slots of the tile's region for this class (dense: a wave's
-        // stores fill whole lines), the record points at them
-        uint32_t pos = 0;
-        auto out_of = [&](uint32_t mm) {
-          pos = atomicAdd(&S.tsum[kt], mm);
-          return w.scratch + (size_t)tile * kTileSlots + pos;
-        };
-        auto store_rec = [&](uint32_t mm) {
-          if (t.dbg == 30) return;  // (A/B measurement only: 30 drops the record stores, ids wrong)
-          if (N <= 16 && w.lrec) {  // the list slot the piece came from (k_segment's record points at it;
-                                    // classes 0 and 1 only: the sparse classes keep tcnt records)
-            const uint32_t qi = (sorted ? (uint32_t)S.perm[i] : i) - S.pre[kt];
-            const_cast<uint32_t*>(list)[(size_t)tile * cap + qi] = rec_short(mm, pos);
-          } else {
-            w.tcnt[(size_t)tile * kTileSlots + j] = rec_short(mm, pos) | ((e & kEntDoc) ? kRecDoc : 0u);
-          }
-        };
-        auto to_mid = [&]() {  // a byte char absent from the vocab is dropped: generic path
-          const uint32_t mi = atomicAdd(&w.counters[4], 1u);
-          if (mi < w.mid_cap)
-            w.mid_list[mi] = (uint64_t)s | ((uint64_t)j << 32) | ((uint64_t)n << 48) | ((e & kEntDoc) ? kMidDoc : 0ull);
-          else
-            atomicOr(&w.counters[kCtrOverflow], 1u);
-        };
-        if constexpr (COMPACT && L8 && N >= kPackMin) {
-          // packed slots (merge_packed): the 17..64 B passes of narrow vocabularies
-          uint32_t pk[N];
-          bool missing = false;
-#pragma unroll
-          for (int k = 0; k < N; k++) {
-            const int32_t id = s_b2id[byte_of(wv[k >> 2], k)];
-            missing |= ((uint32_t)k < n) & (id < 0);
-            pk[k] = (uint32_t)k < n ? ((uint32_t)id & 0xFFFFu) : 0xFFFFu;
-          }
-          if (missing) {
-            to_mid();
-            return;
-          }
-#pragma unroll
-          for (int k = 0; k < N - 1; k++) {
-            const uint32_t r = t.pair0[(byte_of(wv[k >> 2], k) << 8) | byte_of(wv[(k + 1) >> 2], k + 1)];
-            const bool live = (uint32_t)k + 1 < n;
-            if (live && r != kNoRank && value_panics(t, r)) atomicOr(err, kErrPanic);
-            const uint32_t h = (live && r < 0xFFFFu) ? r : 0xFFFFu;  // (a panicking value is not < 0xFFFF)
-            pk[k] |= h << 16;
-          }
-          pk[N - 1] |= 0xFFFF0000u;
-          uint32_t m = n;
-          bool more = true;
-          if constexpr (N >= 64) more = merge_packed<64, HOT>(t, P, pk, m, 32, err);
-          if constexpr (N >= 32) {
-            if (more) more = merge_packed<32, HOT>(t, P, pk, m, 16, err);
-          }
-          if (more) more = merge_packed<16, HOT>(t, P, pk, m, 8, err);
-          if (more) {
-            uint32_t tk8[8], rk8[8];
-#pragma unroll
-            for (int k = 0; k < 8; k++) {
-              tk8[k] = pk[k] & 0xFFFFu;
-              rk8[k] = (pk[k] >> 16) == 0xFFFFu ? kNoRank : (pk[k] >> 16);
-            }
-            m = merge_lds8<COMPACT, HOT, NT>(t, P, tk8, rk8, m, s_key, s_tok, err, out_of);
-          } else {
-            uint32_t* out = out_of(m);
-#pragma unroll
-            for (int k = 0; k < N; k++)
-              if ((uint32_t)k < m) out[k] = pk[k] & 0xFFFFu;
-          }
-          store_rec(m);
-          st_bytes += n;
-          st_ids += m;
-          return;
-        }
         uint32_t tk[N], rk[N];
         bool missing = false;
         {
@@ -1438,8 +1312,12 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
             tk[k] = (uint32_t)id;
           }
         }
-        if (missing) {
-          to_mid();
+        if (missing) {  // a byte char absent from the vocab is dropped: generic path
+          const uint32_t mi = atomicAdd(&w.counters[4], 1u);
+          if (mi < w.mid_cap)
+            w.mid_list[mi] = (uint64_t)s | ((uint64_t)j << 32) | ((uint64_t)n << 48) | ((e & kEntDoc) ? kMidDoc : 0ull);
+          else
+            atomicOr(&w.counters[kCtrOverflow], 1u);
           return;
         }
         // initial pair ranks: every initial pair is a byte pair, one load each from the 256 x 256
@@ -1468,6 +1346,13 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
         if constexpr (N >= 16) {
           if (more) more = merge_slots<16, COMPACT, HOT, L8>(t, P, tk, rk, m, 8, err);
         }
+        // ids go to the next free slots of the tile's region for this class (dense: a wave's
+        // stores fill whole lines), the record points at them
+        uint32_t pos = 0;
+        auto out_of = [&](uint32_t mm) {
+          pos = atomicAdd(&S.tsum[kt], mm);
+          return w.scratch + (size_t)tile * kTileSlots + pos;
+        };
         if (L8 && more) {
           m = merge_lds8<COMPACT, HOT, NT>(t, P, tk, rk, m, s_key, s_tok, err, out_of);
         } else {
@@ -1477,7 +1362,7 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
           for (int k = 0; k < N; k++)
             if ((uint32_t)k < m) out[k] = tk[k];
         }
-        store_rec(m);
+        w.tcnt[(size_t)tile * kTileSlots + j] = rec_short(m, pos) | ((e & kEntDoc) ? kRecDoc : 0u);
         st_bytes += n;
         st_ids += m;
     };
@@ -1488,7 +1373,7 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
         const uint32_t e = entry(i, kt);
         uint32_t wv[N / 4];
         load_words<N / 4>(w.text, start_of(e, kt), w.n_bytes, wv);
-        body(e, kt, i, wv);
+        body(e, kt, wv);
       }
     } else {
       // Each wavefront takes blocks of 64 entries from S.next (one LDS atomic per block): a wave
@@ -1526,7 +1411,7 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
         if (b2 + lane < E) e1 = entry(b2 + lane, kt1);
         b0 = b1;
         b1 = b2;
-        if (i < E) body(e, kt, i, wv);
+        if (i < E) body(e, kt, wv);
       }
     }
     tile_share_flush<K>(w, c0, tb1, S.tsum, S.tbase, LC::cls);
@@ -1598,25 +1483,17 @@ __global__ __launch_bounds__(1024) void k_bpe_short(Work w, Tables t) {
 // stream's passes, and a large class 3 (multilingual text) is shared by both as CUs free up.
 // Most tiles per chunk of the 17..32 B / 33..64 B passes: these classes can be sparse (C4: ~5
 // class-2 pieces per tile), where 64 tiles left most of a 512-thread workgroup idle per chunk.
-// Threads per workgroup: 512 (two waves per SIMD at <= 256 VGPRs); the packed 32-slot pass of
-// narrow compact tables (merge_packed, ~126 VGPRs) runs 768 (three waves per SIMD; its LDS: the
-// image, 36 KiB of merge_lds8 state and the pass scratch, ~153 KiB)
-template <int CLS, bool COMPACT, bool NARROW> struct MidCfg {
-  static constexpr int KT = 256;
-  static constexpr uint32_t NT = (CLS == 2 && COMPACT && NARROW) ? 768 : 512;
-};
+template <int CLS> struct MidCfg { static constexpr int KT = 256; };
 
 template <bool COMPACT, int CLS, bool NARROW>
-__global__ __launch_bounds__((MidCfg<CLS, COMPACT, NARROW>::NT)) void k_bpe_mid(Work w, Tables t) {
+__global__ __launch_bounds__(512) void k_bpe_mid(Work w, Tables t) {
   if (spec_failed(w)) return;
-  using Cfg = MidCfg<CLS, COMPACT, NARROW>;
-  constexpr int KT = Cfg::KT;
-  constexpr uint32_t NT = Cfg::NT;
+  constexpr int KT = MidCfg<CLS>::KT;
   extern __shared__ __attribute__((aligned(16))) uint4 s_img[];
   __shared__ int32_t s_b2id[256];
   __shared__ PassLds<kSortCap, KT> S;
-  __shared__ uint32_t s_key[NARROW ? 8 * NT : 1];
-  __shared__ uint16_t s_tok[NARROW ? 8 * NT : 1];
+  __shared__ uint32_t s_key[NARROW ? 8 * 512 : 1];
+  __shared__ uint16_t s_tok[NARROW ? 8 * 512 : 1];
   // (the image is loaded up front: a lazy load pushes the 64-slot pass into scratch; the kernel
   // returns at once when k_segment found no piece of its class)
   if (w.counters[CLS == 2 ? kCtrAnyMid : kCtrAnyC3] == 0) return;
@@ -1629,12 +1506,12 @@ __global__ __launch_bounds__((MidCfg<CLS, COMPACT, NARROW>::NT)) void k_bpe_mid(
   if (!s_left) return;
   const uint32_t tid = threadIdx.x;
   const uint4* img = NARROW ? t.lds16_image : t.lds_image;
-  for (uint32_t i = tid; i < kLdsImageBytes / 16; i += NT) s_img[i] = img[i];
-  for (uint32_t i = tid; i < 256; i += NT) s_b2id[i] = t.byte2id[i];
+  for (uint32_t i = tid; i < kLdsImageBytes / 16; i += 512) s_img[i] = img[i];
+  for (uint32_t i = tid; i < 256; i += 512) s_b2id[i] = t.byte2id[i];
   bool loaded = true;
   const PairLds P{(const lds_u64*)s_img, (const lds_u32*)(s_img + kHotBuckets)};
-  class_pass<CLS == 2 ? 32 : 64, COMPACT, true, NT, kSortCap, NARROW, KT>(w, t, P, s_b2id, S, loaded, [] {},
-                                                                        (lds_u32*)s_key, (lds_u16*)s_tok);
+  class_pass<CLS == 2 ? 32 : 64, COMPACT, true, 512, kSortCap, NARROW, KT>(w, t, P, s_b2id, S, loaded, [] {},
+                                                                         (lds_u32*)s_key, (lds_u16*)s_tok);
 }
 
 // hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device): the attribute is set
@@ -1660,7 +1537,7 @@ static hipError_t launch_mid_t(const Work& w, const Tables& t, hipStream_t s) {
   static LdsAttr attr;
   HIPCHK(lds_attr_once(attr, (const void*)k_bpe_mid<C, CLS, NW>, kLdsImageBytes));
   if (!w.n_tiles) return hipSuccess;
-  k_bpe_mid<C, CLS, NW><<<min((w.n_tiles + w.unit - 1) / w.unit, w.n_cus), MidCfg<CLS, C, NW>::NT, kLdsImageBytes, s>>>(w, t);
+  k_bpe_mid<C, CLS, NW><<<min((w.n_tiles + w.unit - 1) / w.unit, w.n_cus), 512, kLdsImageBytes, s>>>(w, t);
   return hipGetLastError();
 }
 template <bool C, int CLS>
@@ -2913,15 +2790,6 @@ constexpr uint32_t kEmitStage = 1024;  // ids of one round staged in LDS (4 KiB 
 __device__ __forceinline__ uint32_t rec_count(const Work& w, uint32_t v) {
   return (v & kRecHit) ? 1u : (v & kRecLong) ? w.long_cnt[v & kRecLongMask] : (v & 0xFFFFu);
 }
-// A kRecList record's merged form (count | pos << 16) from its list slot, with the flags kept;
-// every other record as it is.
-__device__ __forceinline__ uint32_t rec_resolve(const Work& w, uint32_t tile, uint32_t v) {
-  if ((v & (kRecHit | kRecLong | kRecList)) != kRecList) return v;
-  const uint32_t c = (v >> 12) & 3u, q = v & 0xFFFu;
-  const uint32_t* l = c == 0 ? w.list0 + (size_t)tile * w.k0 : c == 1 ? w.list1 + (size_t)tile * kCap1
-                    : c == 2 ? w.list2 + (size_t)tile * kCap2 : w.list3 + (size_t)tile * kCap3;
-  return l[q] | (v & kRecDoc);
-}
 
 __global__ __launch_bounds__(64 * kEmitWaves) void k_emit(Work w, uint32_t* __restrict__ ids, uint64_t ids_cap,
                                                          uint64_t* __restrict__ tok_off) {
@@ -2944,28 +2812,11 @@ __global__ __launch_bounds__(64 * kEmitWaves) void k_emit(Work w, uint32_t* __re
   uint32_t r_first = 0;  // the current round's first id within the tile (wave-uniform)
   __shared__ uint32_t s_stage[kEmitWaves][kEmitStage];
   lds_u32* stage = (lds_u32*)s_stage[threadIdx.x >> 6];
-  // records two rounds deep: round r's are resolved (kRecList: their list slots loaded) while
-  // round r - 1 runs, and loaded while round r - 2 runs -- the extra load of a list record is off
-  // the round's critical path
   uint4 nx = load(4 * lane);
-  uint32_t cur[4];
-  {
-    const uint32_t v[4] = {nx.x, nx.y, nx.z, nx.w};
-#pragma unroll
-    for (int k = 0; k < 4; k++) cur[k] = 4 * lane + k < np ? rec_resolve(w, tile, v[k]) : v[k];
-  }
-  if (256 < np) nx = load(4 * lane + 256);
   for (uint32_t r0 = 0; r0 < np; r0 += 256) {
     const uint32_t j0 = r0 + 4 * lane;
-    uint32_t rec[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) rec[k] = cur[k];
-    if (r0 + 256 < np) {  // the next round's records, resolved now; the round after next's loaded
-      const uint32_t v[4] = {nx.x, nx.y, nx.z, nx.w};
-#pragma unroll
-      for (int k = 0; k < 4; k++) cur[k] = j0 + 256 + k < np ? rec_resolve(w, tile, v[k]) : v[k];
-      if (r0 + 512 < np) nx = load(j0 + 512);
-    }
+    const uint32_t rec[4] = {nx.x, nx.y, nx.z, nx.w};
+    if (r0 + 256 < np) nx = load(j0 + 256);
     uint32_t c[4], sum = 0;
 #pragma unroll
     for (int k = 0; k < 4; k++) {

@@ -62,6 +62,13 @@ for step in "$@"; do
             | sed "s|^|$arm${envs:+ $envs} |" | tee -a "$OUT/abpenv_${cfg}.txt"
         done
       done ;;
+    trace:*)  # kernel trace of tools/probe.py (trace:CFG:FIX[:LIB]) and the last call's timeline
+      IFS=: read -r _ cfg fx lib <<< "$step"
+      lib=${lib:-complexity-tokenizer_amd/complexity_tokenizer/libctok.so}
+      d="$OUT/trace_${cfg}_$(basename "$lib" .so)"
+      (cd /tmp && CTOK_LIB="$ROOT/$lib" timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$d" -o run -- \
+        python3 "$ROOT/tools/probe.py" "$cfg" "$fx" 2 > "$d.log" 2>&1) || { tail -20 "$d.log"; exit 1; }
+      python3 tools/trace_timeline.py "$d" | tee "$d.txt" ;;
     probe:*)
       IFS=: read -r _ cfg fx <<< "$step"
       timeout -k 10 300 python -u tools/probe.py "$cfg" "$fx" 5 2>&1 | tee -a "$OUT/probe_${cfg}_${fx}.txt" ;;
