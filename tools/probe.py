@@ -34,6 +34,7 @@ for _ in range(reps):
     tok.encode_packed_device(*args, timing=True)
     ts.append(time.perf_counter() - t)
 st = tok.last_stats
-print("%s %s: %d docs %d B, call %.3f ms (%.0f MB/s), device %.3f ms, long %.3f ms, long pieces %d" % (
-    cfg, fx, nd, nb, min(ts) * 1e3, nb / min(ts) / 1e6, st["ms_device"], st["ms_bpe_long"], st["long_pieces"]), flush=True)
+print("%s %s: %d docs %d B, call %.3f ms (%.0f MB/s), device %.3f ms, long %.3f ms, long pieces %d, nfc docs %d" % (
+    cfg, fx, nd, nb, min(ts) * 1e3, nb / min(ts) / 1e6, st["ms_device"], st["ms_bpe_long"], st["long_pieces"],
+    st.get("nfc_docs", -1)), flush=True)
 print({k: v for k, v in st.items() if k.startswith("ms_")}, flush=True)
