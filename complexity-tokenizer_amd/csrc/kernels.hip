@@ -412,7 +412,17 @@ __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
   for (int k = 0; k < 4; k++)
     *reinterpret_cast<uint4*>(s_all + lane * 16 + 4 * k) = make_uint4(x[4 * k], x[4 * k + 1], x[4 * k + 2], x[4 * k + 3]);
-  if (last) s_all[64 * 16] = 0;
+  if (last) {  // the 4 bytes after the look-ahead word: a code point starting in its last bytes
+               // runs into them (zero past the text)
+    const int64_t xe = g * 64 + 64;
+    uint32_t v = 0;
+    if (xe + 4 <= (int64_t)B) {
+      v = *reinterpret_cast<const uint32_t*>(w.text + xe);
+    } else {
+      for (int64_t i = xe; i < (int64_t)B && i < xe + 4; i++) v |= (uint32_t)w.text[i] << (8 * (uint32_t)(i - xe));
+    }
+    s_all[64 * 16] = v;
+  }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");

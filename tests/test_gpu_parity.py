@@ -332,8 +332,11 @@ def test_multi_sample(multi_path):
     tok = Tokenizer.from_file(multi_path)
     rc = ref_c.RefC(obj)
     text, off = corpus.corpus_c5(20_000, seed=55)
-    ids, toff = tok.encode_packed(text, off)
+    ids, toff = tok.encode_packed(text, off, timing=True)
     assert_same(ids, toff, *rc.encode_packed(text, off))
+    # C5 holds no code point NFC changes: the speculation flags no document (k_segment decodes each
+    # code point from LDS, including one that starts at the end of the look-ahead word)
+    assert tok.last_stats["nfc_docs"] == 0
 
 
 def test_multi_nfc_sample(multi_path):
