@@ -5,6 +5,7 @@
 #   prof    rocprofv3 kernel trace of bench.py   pmc     FETCH_SIZE / WRITE_SIZE passes -> traffic
 #   ab:CFG:FIX:LIB_A:LIB_B   alternating kernel-only probes (tools/probe.py) of two libraries
 #   matrix  tools/bench_matrix.py (every config)  probe:CFG:FIX  one probe of the working tree
+#   ptest:FILE[,FILE]  a subset of the GPU tests
 #   abenv:VAR=VAL   bench.py A/B (tools/ab.sh) without / with VAR=VAL     ablib:LIB_A:LIB_B   the same for two libraries
 #   usage: TAG=name bash tools/session.sh STEP [STEP ...]
 set -e
@@ -22,6 +23,13 @@ for step in "$@"; do
       tail -3 "$OUT/gpu_tests.log"
       if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "tests: exit $rc"; exit 1; fi
       grep -E "^(FAILED|ERROR)" "$OUT/gpu_tests.log" || true ;;
+    ptest:*)  # a subset of the GPU tests: ptest:FILE[,FILE...] (paths under tests/)
+      rc=0; files=$(echo "${step#ptest:}" | tr , ' ' | sed 's|\([^ ]*\)|tests/\1|g')
+      timeout -k 10 900 python -u -m pytest $files -m gpu -v --maxfail=5 --timeout 600 --timeout-method thread \
+        > "$OUT/ptest.log" 2>&1 || rc=$?
+      tail -3 "$OUT/ptest.log"
+      if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "ptest: exit $rc"; exit 1; fi
+      grep -E "^(FAILED|ERROR)" "$OUT/ptest.log" || true ;;
     bench)
       timeout -k 10 500 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.log" || { tail -20 "$OUT/bench.log"; exit 1; }
       cat "$OUT/bench.json" ;;
