@@ -1455,7 +1455,20 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
 // (hot table + Bloom filter); a workgroup moves on to class 1 as soon as class 0 has no chunk
 // left, with no kernel boundary in between.  NARROW (every id < 2^16): 960 threads, the last
 // tier's state in LDS (merge_lds8); else 1024 threads, all tiers in registers.
-template <bool NARROW> struct ShortCfg { static constexpr uint32_t NT = NARROW ? 960 : 1024; };
+// Narrow: the workgroup size and the sort buffer share the LDS left beside the image with
+// merge_lds8's 48 B per thread; 1024 threads with a 7168-entry sort buffer (LDS 163,648 B) take
+// k_bpe_short 3.57 -> 3.51 ms on C4 against 960 with 8192 (profiles/r04/v12_ab_short_nt1024_c4.txt).
+// (Compile-time knobs for A/B builds.)
+#ifndef CTOK_SHORT_NT
+#define CTOK_SHORT_NT 1024
+#endif
+#ifndef CTOK_SHORT_SORTCAP
+#define CTOK_SHORT_SORTCAP 7168
+#endif
+template <bool NARROW> struct ShortCfg {
+  static constexpr uint32_t NT = NARROW ? CTOK_SHORT_NT : 1024;
+  static constexpr uint32_t SORTCAP = NARROW ? CTOK_SHORT_SORTCAP : kSortCap;
+};
 // tiles per chunk of the <= 16 B passes (dense classes: ~100 + ~60 pieces per tile on C4; 128
 // tiles per chunk measured 3% slower, profiles/r02/v30_ab_short_kt128.txt)
 constexpr int kShortKT = 64;
@@ -1466,7 +1479,7 @@ __global__ __launch_bounds__(1024) void k_bpe_short(Work w, Tables t) {
   constexpr uint32_t NT = ShortCfg<NARROW>::NT;
   extern __shared__ __attribute__((aligned(16))) uint4 s_img[];
   __shared__ int32_t s_b2id[256];
-  __shared__ PassLds<kSortCap, kShortKT> S;
+  __shared__ PassLds<ShortCfg<NARROW>::SORTCAP, kShortKT> S;
   __shared__ uint32_t s_key[NARROW ? 8 * NT : 1];
   __shared__ uint16_t s_tok[NARROW ? 8 * NT : 1];
   const uint32_t tid = threadIdx.x;
@@ -1479,8 +1492,8 @@ __global__ __launch_bounds__(1024) void k_bpe_short(Work w, Tables t) {
   const PairLds P{(const lds_u64*)s_img, (const lds_u32*)(s_img + kHotBuckets)};
   lds_u32* sk = (lds_u32*)s_key;
   lds_u16* st = (lds_u16*)s_tok;
-  class_pass<8, COMPACT, true, NT, kSortCap, NARROW, kShortKT>(w, t, P, s_b2id, S, loaded, load, sk, st);
-  class_pass<16, COMPACT, true, NT, kSortCap, NARROW, kShortKT>(w, t, P, s_b2id, S, loaded, load, sk, st);
+  class_pass<8, COMPACT, true, NT, ShortCfg<NARROW>::SORTCAP, NARROW, kShortKT>(w, t, P, s_b2id, S, loaded, load, sk, st);
+  class_pass<16, COMPACT, true, NT, ShortCfg<NARROW>::SORTCAP, NARROW, kShortKT>(w, t, P, s_b2id, S, loaded, load, sk, st);
 }
 
 // Pieces of 17..32 bytes (CLS = 2, on the main stream after k_bpe_short) or 33..64 bytes (CLS = 3,
