@@ -1156,7 +1156,7 @@ __device__ __forceinline__ bool merge_slots(const Tables& t, const PairLds& P, u
 // rank << 3 | s of the pair its token starts (~0 when the slot is dead or last).  A merge then
 // reads the keys (four ds_read2st64, a v_min tree), writes three keys and one token, and reads its
 // two neighbours by index; the register tiers' N-wide select / shift chains (~100 VALU per merge
-// at N = 8) are gone.  Tokens are u16 (narrow vocabularies: every id < 2^16), so 960 threads'
+// at N = 8) are gone.  Tokens are u16 (narrow vocabularies: every id < 2^16), so 1024 threads'
 // state (48 B each) fits beside the 96 KiB image.  Pair lookups use the 32-bit-key tables.
 //   keys:   s_key[s * NT + tid] (u32; read two at a time with ds_read2st64)
 //   tokens: s_tok[s * NT + tid] (u16)
@@ -1453,7 +1453,7 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
 
 // Pieces of <= 16 bytes (classes 0 and 1): one workgroup per CU holding the whole LDS image
 // (hot table + Bloom filter); a workgroup moves on to class 1 as soon as class 0 has no chunk
-// left, with no kernel boundary in between.  NARROW (every id < 2^16): 960 threads, the last
+// left, with no kernel boundary in between.  NARROW (every id < 2^16): 1024 threads, the last
 // tier's state in LDS (merge_lds8); else 1024 threads, all tiers in registers.
 // Narrow: the workgroup size and the sort buffer share the LDS left beside the image with
 // merge_lds8's 48 B per thread; 1024 threads with a 7168-entry sort buffer (LDS 163,648 B) take
