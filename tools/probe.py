@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
 """Device-path probe for one matrix config (profiling helper for rocprofv3, not product code):
 usage probe.py CONFIG [fixture] [reps] -- e.g. probe.py c5 multi_32k 5."""
+import hashlib
+import json
 import os
 import sys
 import time
@@ -34,7 +36,16 @@ for _ in range(reps):
     tok.encode_packed_device(*args, timing=True)
     ts.append(time.perf_counter() - t)
 st = tok.last_stats
-print("%s %s: %d docs %d B, call %.3f ms (%.0f MB/s), device %.3f ms, long %.3f ms, long pieces %d, nfc docs %d" % (
+# the last call's output against the golden digest of the config (tests/golden/digests.json)
+gold = json.load(open(os.path.join(ROOT, "tests", "golden", "digests.json"))).get(cfg)
+parity = "no golden digest"
+if gold is not None and gold["tokenizer"] == fx:
+    torch.cuda.synchronize()
+    h = hashlib.sha256()
+    h.update(d_tok.cpu().numpy().view(np.uint64).tobytes())
+    h.update(d_ids[: int(d_tok[-1])].cpu().numpy().view(np.uint32).tobytes())
+    parity = "digest ok" if h.hexdigest() == gold["sha256"] else "DIGEST MISMATCH"
+print("%s %s: %d docs %d B, call %.3f ms (%.0f MB/s), device %.3f ms, long %.3f ms, long pieces %d, nfc docs %d, %s" % (
     cfg, fx, nd, nb, min(ts) * 1e3, nb / min(ts) / 1e6, st["ms_device"], st["ms_bpe_long"], st["long_pieces"],
-    st.get("nfc_docs", -1)), flush=True)
+    st.get("nfc_docs", -1), parity), flush=True)
 print({k: v for k, v in st.items() if k.startswith("ms_")}, flush=True)
