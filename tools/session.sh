@@ -5,7 +5,7 @@
 #   prof    rocprofv3 kernel trace of bench.py   pmc     FETCH_SIZE / WRITE_SIZE passes -> traffic
 #   ab:CFG:FIX:LIB_A:LIB_B   alternating kernel-only probes (tools/probe.py) of two libraries
 #   matrix  tools/bench_matrix.py (every config)  probe:CFG:FIX  one probe of the working tree
-#   ptest:FILE[,FILE]  a subset of the GPU tests
+#   ptest:FILE[,FILE]  a subset of the GPU tests    pmcp:CFG:FIX:CTR,CTR  a PMC pass over probe.py (per-kernel)
 #   abenv:VAR=VAL   bench.py A/B (tools/ab.sh) without / with VAR=VAL     ablib:LIB_A:LIB_B   the same for two libraries
 #   usage: TAG=name bash tools/session.sh STEP [STEP ...]
 set -e
@@ -77,6 +77,12 @@ for step in "$@"; do
       (cd /tmp && CTOK_LIB="$ROOT/$lib" timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$d" -o run -- \
         python3 "$ROOT/tools/probe.py" "$cfg" "$fx" 2 > "$d.log" 2>&1) || { tail -20 "$d.log"; exit 1; }
       python3 tools/trace_timeline.py "$d" | tee "$d.txt" ;;
+    pmcp:*)  # one PMC pass over tools/probe.py: pmcp:CFG:FIX:COUNTER,COUNTER,... (per-kernel sums)
+      IFS=: read -r _ cfg fx ctrs <<< "$step"
+      d="$OUT/pmc_${cfg}_$(echo "$ctrs" | tr , _ | cut -c1-40)"
+      (cd /tmp && timeout -s KILL 240 rocprofv3 --pmc $(echo "$ctrs" | tr , ' ') --output-format csv -d "$d" -o run -- \
+        python3 "$ROOT/tools/probe.py" "$cfg" "$fx" 2 > "$d.log" 2>&1) || { tail -20 "$d.log"; exit 1; }
+      python3 tools/pmc_sum.py "$d" | tee "$d.txt" ;;
     probe:*)
       IFS=: read -r _ cfg fx <<< "$step"
       timeout -k 10 300 python -u tools/probe.py "$cfg" "$fx" 5 2>&1 | tee -a "$OUT/probe_${cfg}_${fx}.txt" ;;
