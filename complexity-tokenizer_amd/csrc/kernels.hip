@@ -258,24 +258,6 @@ __device__ __forceinline__ uint16_t nfc16(const Tables& t, uint32_t cp) {
   return t.nfc_s2[t.nfc_s1[cp >> 8] * 256 + (cp & 255)];
 }
 
-// class of the code point byte x belongs to (x < B; non-ASCII slow path), | 4 when NFC might
-// change that code point (NFC_QC != Yes or non-zero combining class)
-__device__ __forceinline__ int seg_cls_wide(const uint8_t* text, uint32_t B, uint32_t x, const Tables& t) {
-  uint32_t j = x;
-#pragma unroll
-  for (int k = 0; k < 3; k++)
-    if (j > 0 && (text[j] & 0xC0) == 0x80) j--;
-  const uint32_t b0 = text[j];
-  const int len = u8len((uint8_t)b0);
-  auto at = [&](uint32_t i) -> uint32_t { return text[min(i, B - 1)] & 0x3Fu; };
-  uint32_t c;
-  if (len == 1) c = b0;
-  else if (len == 2) c = ((b0 & 0x1Fu) << 6) | at(j + 1);
-  else if (len == 3) c = ((b0 & 0x0Fu) << 12) | (at(j + 1) << 6) | at(j + 2);
-  else c = ((b0 & 0x07u) << 18) | (at(j + 1) << 12) | (at(j + 2) << 6) | at(j + 3);
-  return cls_of(c, t) | (nfc16(t, c) != 0 ? 4 : 0);
-}
-
 // Neighbour lanes' words (k_segment: lane l needs lanes l - 1 and l + 1), by DPP wave shifts
 // (wave_shr:1 / wave_shl:1, GFX9) instead of ds_bpermute: lane 0 (shr) and lane 63 (shl) keep
 // their own value, as __shfl_up / __shfl_down leave it.  Uniform control flow only.
@@ -360,7 +342,9 @@ __device__ __forceinline__ uint32_t select_bit(uint64_t x, uint32_t k) {
 // profiles/r03/v30_ab_seg_waves_per_eu.txt)
 __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(7))) void k_segment(Work w, Tables t) {
   __shared__ uint16_t s_pos_all[kSegWaves][64 * kSegUnroll + 8];  // one round's piece starts
-  __shared__ uint32_t s_text_all[kSegWaves][(kTileWords + 2) * 16 + 4];  // context word + tile + look-ahead word
+  // the 4 bytes before the context word, the context word, the tile, the look-ahead word, the 4
+  // bytes after it
+  __shared__ uint32_t s_text_all[kSegWaves][(kTileWords + 2) * 16 + 5];
   __shared__ uint64_t s_D_all[kSegWaves][64];  // doc starts per word (piece records carry kRecDoc)
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wid = uni(threadIdx.x >> 6);
@@ -407,8 +391,12 @@ __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(
   s_D_all[wid][lane] = D;
   // every lane's word in LDS: the tile's bytes (and the look-ahead word) for the whole-piece
   // probes (s_text: the tile's first byte), the context word too for the code point decoding below
-  uint32_t* s_all = s_text_all[wid];
+  uint32_t* s_all = s_text_all[wid] + 1;  // (s_all[-1]: the 4 bytes before the context word)
   uint32_t* s_text = s_all + 16;
+  // the context word's first code point can start in the word before it (its first byte is a
+  // continuation byte): the 4 bytes before it
+  if (first && (x[0] & 0xC0u) == 0x80u && g * 64 >= 4)
+    s_all[-1] = *reinterpret_cast<const uint32_t*>(w.text + g * 64 - 4);
 #pragma unroll
   for (int k = 0; k < 4; k++)
     *reinterpret_cast<uint4*>(s_all + lane * 16 + 4 * k) = make_uint4(x[4 * k], x[4 * k + 1], x[4 * k + 2], x[4 * k + 3]);
@@ -445,7 +433,20 @@ __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(
     cont &= m.NA;
     const uint64_t lead_cont = cont & ~(cont + 1);  // continuation bytes at the start of the word
     if (lead_cont) {  // a code point whose lead is in the previous word: classified on its own
-      const int cw = seg_cls_wide(w.text, B, x0, t);
+      // the bytes before this word are staged just before it (the previous lane's word, or for
+      // the context word s_all[-1]): the lead is 1..3 bytes back (at most 3 steps back, as a
+      // walk over the text would take)
+      const uint32_t pw = s_all[lane * 16 - 1];  // bytes x0 - 4 .. x0 - 1
+      const int32_t back = ((pw >> 24) & 0xC0u) != 0x80u ? 1 : ((pw >> 16) & 0xC0u) != 0x80u ? 2 : 3;
+      const int32_t a = (int32_t)lane * 64 - back;  // byte address in s_all (-3 .. -1 for the context word)
+      const uint32_t v = __builtin_amdgcn_alignbyte(s_all[(a >> 2) + 1], s_all[a >> 2], (uint32_t)a & 3u);
+      const uint32_t b0 = v & 255u, b1 = (v >> 8) & 0x3Fu, b2 = (v >> 16) & 0x3Fu, b3 = (v >> 24) & 0x3Fu;
+      const int l = u8len((uint8_t)b0);
+      const uint32_t c = l == 2 ? ((b0 & 0x1Fu) << 6) | b1
+                       : l == 3 ? ((b0 & 0x0Fu) << 12) | (b1 << 6) | b2
+                       : l == 4 ? ((b0 & 0x07u) << 18) | (b1 << 12) | (b2 << 6) | b3 : b0;
+      const int rc = t.cp_fast ? cp_range_class(c) : -1;
+      const int cw = rc >= 0 ? rc : (cls_of(c, t) | (nfc16(t, c) != 0 ? 4 : 0));
       nfc_bad |= (cw & 4) != 0;
       set_class(cw & 3, lead_cont);
     }
