@@ -20,7 +20,8 @@ cfg = sys.argv[1].upper() if len(sys.argv) > 1 else "C3"
 fx = sys.argv[2] if len(sys.argv) > 2 else {"C3": "llama3_128k", "C5": "multi_32k", "C5NFC": "multi_32k"}.get(cfg, "gpt2_50k")
 reps = int(sys.argv[3]) if len(sys.argv) > 3 else 5
 tok = Tokenizer.from_file(fixture_path(fx, "/tmp"))
-text, off = corpus.CONFIGS[cfg]()
+print("building %s" % cfg, flush=True)  # (C4 on worker processes: one process takes minutes)
+text, off = corpus.corpus_c4(workers=min(16, len(os.sched_getaffinity(0)))) if cfg == "C4" else corpus.CONFIGS[cfg]()
 nb, nd = int(off[-1]), len(off) - 1
 d_text = torch.zeros(nb + 64, dtype=torch.uint8, device="cuda")
 d_text[:nb] = torch.from_numpy(text).cuda()
