@@ -215,9 +215,9 @@ struct DeviceState {
   DevBuf<uint64_t> comp_key;
   Tables t{};
   // workspace
-  DevBuf<uint32_t> docbits, pbits, tile_np, tile_tok, tile_doc, tcls, list0, list1, list2, list3, tcnt, slots, counters;
-  DevBuf<uint32_t> lids, lw, long_pos, lw_pos, lwn, tlong, ovf, cps;
-  DevBuf<uint64_t> dbits;
+  DevBuf<uint32_t> docbits, pbits, tile_np, tile_tok, tile_doc, tcls, list0, list1, list2, list3, tcnt, scratch, counters;
+  DevBuf<uint32_t> lids, lw, long_pos, lw_pos, lwn, rend, cps;
+  DevBuf<uint64_t> tregion;
   DevBuf<uint16_t> wpref;
   DevBuf<uint32_t> long_cnt, long_ord, long_hist;
   DevBuf<uint64_t> long_list, mid_list, scan_tmp, scan_tmp2;
@@ -252,7 +252,7 @@ struct DeviceState {
     uint64_t b = 0;
     auto add = [&](const auto& x) { b += (uint64_t)x.cap * sizeof(*x.p); };
     add(docbits), add(pbits), add(tile_np), add(tile_tok), add(tile_doc), add(tcls), add(list0), add(list1);
-    add(list2), add(list3), add(tcnt), add(slots), add(counters), add(lids), add(lw), add(dbits), add(tlong), add(ovf);
+    add(list2), add(list3), add(tcnt), add(scratch), add(counters), add(lids), add(lw), add(tregion), add(rend);
     add(wpref), add(long_cnt), add(long_ord), add(long_hist), add(long_pos), add(lw_pos), add(lwn), add(long_list);
     add(mid_list), add(scan_tmp), add(scan_tmp2), add(cps);
     add(doc_flag), add(ncp), add(norm_off), add(norm_text);
@@ -317,9 +317,7 @@ struct ctok {
   std::vector<uint8_t> at_flags;
   bool proper = true;
   bool compact = false;
-  bool narrow = false;  // every vocab id < kSlotEsc16 (u16 merge-pass tokens and id slots)
-  bool at16 = true;     // every added-token id < kSlotEsc16 (the generic pass writes them into u16 slots)
-  bool rec16_ok = false;  // every vocab id < kR16List: u16 piece records possible
+  bool narrow = false;  // every vocab id < 2^16
   bool ids16 = false;   // every id encode can emit (vocab and added tokens) < 2^16: 16-bit ids on PCIe
   // decode (src/huggingface/mod.rs:710-747): decoder kind, per-id decoded bytes
   int decoder = 1;                  // 1 ByteLevel, 0 raw concatenation (unknown decoder type), -1 unsupported
@@ -755,8 +753,7 @@ void load_root(ctok* t, const ctj::Value& root) {
   {
     uint32_t max_id = 0;
     for (const auto& kv : t->vocab) max_id = std::max(max_id, kv.second);
-    t->narrow = max_id < kSlotEsc16;
-    t->rec16_ok = max_id < kR16List;
+    t->narrow = max_id < 0xFFFFu;
   }
   // compact table: values are the new ids themselves when new id is strictly increasing in rank
   {
@@ -1133,7 +1130,6 @@ void load_root(ctok* t, const ctj::Value& root) {
 
   t->ids16 = t->narrow;
   for (uint32_t id : t->at_id) t->ids16 = t->ids16 && id < 0xFFFFu;
-  for (uint32_t id : t->at_id) t->at16 = t->at16 && id < kSlotEsc16;
   t->nfc = parse_normalizer(root.get("normalizer")) != 0;
   std::vector<std::pair<char, bool>> chain;
   parse_pre_tokenizer(root.get("pre_tokenizer"), chain, 0);
@@ -1469,26 +1465,15 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   w.mid_cap = (uint32_t)(safe ? B + 8 : std::min<uint64_t>(B + 8, std::max<uint64_t>(65536, B / 256)));
   ds->tcls.ensure(kNumClasses * nt + 8);
   ds->list0.ensure(nt * w.k0 + 8);
+  ds->rend.ensure(kNumClasses * nt + 8);
   if (tb.n_at == 0) {
     ds->list1.ensure(nt * kCap1 + 8);
     ds->list2.ensure(nt * kCap2 + 8);
     ds->list3.ensure(nt * kCap3 + 8);
   }
   ds->tcnt.ensure(nt * kTileSlots + 8);
-  // records: u16 for narrow vocabularies with lean lists (kR16List); id slots of the class lists:
-  // u16 units for narrow vocabularies (ctok_internal.h slot_base)
-  w.s16 = (tb.narrow && (tb.n_at == 0 || t->at16)) ? 1u : 0u;
-  static const bool no_rec16 = getenv("CTOK_NO_REC16") != nullptr;
-  w.rec16 = (w.s16 && t->rec16_ok && !safe && !keep_first && !no_rec16) ? 1u : 0u;
-  w.slot_stride = slot_stride(w.k0);
-  const size_t unit_bytes = w.s16 ? 2 : 4;
-  ds->slots.ensure((nt * w.slot_stride * unit_bytes + 64) / 4 + 8);
-  // ids past a slot (pieces with more ids than their slot holds: rare); every id of the class
-  // lists in the safe rerun
-  w.ovf_cap = (uint32_t)(B + 64);
-  ds->ovf.ensure(((uint64_t)w.ovf_cap * unit_bytes + 64) / 4 + 8);
-  ds->dbits.ensure(nt * (kTileSlots / 64) + 8);
-  if (w.rec16) ds->tlong.ensure(nt * kTLong + 8);
+  ds->scratch.ensure(nt * kTileSlots + 8);  // per tile: the class regions of the register passes
+  ds->tregion.ensure(nt + 8);
   ds->long_list.ensure(w.long_cap + 8);
   ds->long_cnt.ensure(w.long_cap + 8);
   ds->long_ord.ensure(w.long_cap + 8);
@@ -1510,10 +1495,9 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   w.long_ord = ds->long_ord.p;
   w.long_hist = ds->long_hist.p;
   w.tcnt = ds->tcnt.p;
-  w.slots = ds->slots.p;
-  w.ovf = ds->ovf.p;
-  w.dbits = ds->dbits.p;
-  w.tlong = ds->tlong.p;
+  w.scratch = ds->scratch.p;
+  w.rend = ds->rend.p;
+  w.tregion = (uint2*)ds->tregion.p;
   w.long_list = ds->long_list.p;
   w.mid_list = ds->mid_list.p;
   w.counters = ds->counters.p;

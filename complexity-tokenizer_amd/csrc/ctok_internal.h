@@ -47,59 +47,42 @@ constexpr int kCtrSink = 31;       // counters[31]: panic bits of lookups whose 
 constexpr int kCtrOverflow = 25;   // counters[25] != 0: a list outgrew its lean capacity (the host reruns the call safe)
 constexpr int kCtrLongIds = 26;    // counters[26]: long-piece id slots reserved (k_long_len: a piece's bytes)
 constexpr int kCtrLwWords = 27;    // counters[27]: global-memory long-piece state reserved (4 u32 per byte)
-constexpr int kCtrOvf = 28;        // counters[28]: id units taken from Work::ovf
 // Long-piece order (long_hist, u32[kLhWords], zeroed per call): pieces in descending length
 // buckets of 64 B (bucket d = 64 - (n - 1) / 64, d = 0 for n > 4096), so every wave tier's pieces
 // are a contiguous range of long_ord, longest first.
 constexpr int kLhBuckets = 65;
 constexpr int kLhHist = 0, kLhScan = 80, kLhFill = 160, kLhTake = 240, kLhWords = 320;
 __host__ __device__ inline uint32_t long_bucket(uint32_t n) { return n > 4096 ? 0u : 64u - (n - 1) / 64; }
-// List entry (u32): start within the tile [0,12), the entry's own index q in its list [12,24) (its
-// id slot, see slot_base), length [24,31) (<= kMedMax = 64).
-__host__ __device__ inline uint32_t list_entry(uint32_t sl, uint32_t q, uint32_t n) { return sl | (q << 12) | (n << 24); }
+// List entry (u32): start within the tile [0,12), piece index within the tile [12,24), length [24,31)
+// (<= kMedMax = 64), kEntDoc: the piece starts a document.
+constexpr uint32_t kEntDoc = 1u << 31;
+__host__ __device__ inline uint32_t list_entry(uint32_t sl, uint32_t j, uint32_t n) { return sl | (j << 12) | (n << 24); }
 __host__ __device__ inline uint32_t ent_len(uint32_t e) { return (e >> 24) & 127u; }
-__host__ __device__ inline uint32_t ent_q(uint32_t e) { return (e >> 12) & 0xFFFu; }
-// long_list entry (u64): start byte | j << 32 | n << 44 (n: the piece's length when k_segment
-// knows it -- its end lies within the tile's look-ahead --, else 0); mid_list entry:
-// start | (cls << 12 | q) << 32 | n << 48 (the piece's class-list slot, see below).
+__host__ __device__ inline uint32_t ent_j(uint32_t e) { return (e >> 12) & 0xFFFu; }
+// long_list entry (u64): start byte | j << 32 | n << 44 | kLongDoc (n: the piece's length when
+// k_segment knows it -- its end lies within the tile's look-ahead --, else 0); mid_list entry:
+// start | j << 32 | kMidDoc | n << 48.
+constexpr uint64_t kLongDoc = 1ull << 63, kMidDoc = 1ull << 44;
 __host__ __device__ inline uint32_t long_j(uint64_t e) { return (uint32_t)(e >> 32) & 0xFFFu; }
 __host__ __device__ inline uint32_t long_len(uint64_t e) { return (uint32_t)(e >> 44) & 0x7FFFFu; }
 
-// Piece record of piece j of a tile, written once, by k_segment, as it routes the piece:
-//   u32 records (tcnt[tile * kTileSlots + j]):
-//     kRecHit | id          one id, the whole-piece probe's
-//     kRecLong | li         long piece li: count long_cnt[li], ids at lids[long_pos[li] ..]
-//     cls << 12 | q         entry q of the tile's class-cls list: the merge pass writes the
-//                           piece's ids into that entry's id slot (below)
-//   u16 records (Work::rec16; tcnt16[tile * kTileSlots + j]; narrow vocabularies whose ids are all
-//   < kR16List, lean capacities): id | kR16List + r16_base(cls) + q | kR16Long + k: the k-th long
-//   piece of its group of 64 pieces (j / 64), li = tlong[tile * kTLong + j / 64] + k.
-// Whether piece j starts a document is bit j of the tile's dbits words (kTileSlots / 64 u64 per
-// tile), not part of the record.  k_emit may overwrite a doc-start piece's record with the
-// piece's first id within the tile (for k_tokoff; every piece's with Work::keep_first).
-constexpr uint32_t kRecHit = 0x80000000u, kRecLong = 0x40000000u;
-constexpr uint32_t kRecIdMask = (1u << kIdBits) - 1u, kRecLongMask = kRecLong - 1u;
-constexpr uint32_t kR16List = 0xE000u, kR16Long = 0xF000u;
-constexpr uint32_t kTLong = kTileSlots / 64;  // groups of 64 pieces per tile (tlong: each group's first long-list index)
-__host__ __device__ inline uint32_t r16_base(uint32_t cls) {
-  return cls == 0 ? 0u : cls == 1 ? kCap0Lean : cls == 2 ? kCap0Lean + kCap1 : kCap0Lean + kCap1 + kCap2;
+// Piece record (tcnt[tile][j], u32), written by whichever pass finishes piece j:
+//   kRecHit | id            one id, the whole-piece probe's (no scratch entry)
+//   kRecLong | li           long piece li: count long_cnt[li], ids at lids[long_pos[li] ..]
+//   count | pos << 16       merged piece (<= 64 B: register passes, generic pass): ids at
+//                           scratch[tile * kTileSlots + pos ..] (pos: a slot of the tile's region
+//                           for the piece's length class, see tregion)
+// | kRecDoc when the piece starts a document: k_emit then leaves the piece's first id within the
+// tile in its slot (for k_tokoff).
+constexpr uint32_t kRecHit = 0x80000000u, kRecLong = 0x40000000u, kRecDoc = 0x20000000u;
+constexpr uint32_t kRecIdMask = (1u << kIdBits) - 1u, kRecLongMask = kRecDoc - 1u;
+// Per-tile id regions of the register merge passes in scratch (kTileSlots u32 per tile): class c
+// (c = 0..3) starts at the total bytes of the tile's class lists < c (ids <= bytes), packed as
+// tregion[tile] = {R1 | R2 << 16, R3}.
+__host__ __device__ inline uint32_t region_base(uint2 r, int cls) {
+  return cls <= 0 ? 0u : cls == 1 ? (r.x & 0xFFFFu) : cls == 2 ? (r.x >> 16) : r.y;
 }
-// Id slots of the class lists (Work::slots; a tile's slots at tile * slot_stride, class c's after
-// the classes below it at slot_base): entry q of class c owns slot_ids(c) id units -- u16 for
-// narrow vocabularies (Work::s16), else u32 -- written whole by the merge pass (consecutive entries:
-// whole lines), read by k_emit.  Classes 0, 1: a piece of n <= 4 ids fills the first n units and,
-// when n < 4, ends with kSlotEnd.  Classes 2, 3: unit 0 = n, the ids after it (n < slot_ids(c)).
-// A longer piece writes kSlotEsc, n, and the position of its ids in Work::ovf (two u16 units, or
-// one u32).  Ids are < kSlotEsc (u16: the host checks).
-__host__ __device__ constexpr uint32_t slot_ids(int cls) { return cls == 0 ? 4u : cls == 1 ? 4u : cls == 2 ? 8u : 16u; }
-// (in id units; every class region and the tile stride start on 16 units: 32-byte aligned)
-__host__ __device__ inline uint32_t slot_base(uint32_t k0, int cls) {
-  const uint32_t b2 = (4u * (k0 + kCap1) + 15u) & ~15u;
-  return cls == 0 ? 0u : cls == 1 ? 4u * k0 : cls == 2 ? b2 : b2 + 8u * kCap2;
-}
-__host__ __device__ inline uint32_t slot_stride(uint32_t k0) { return (slot_base(k0, 3) + 16u * kCap3 + 15u) & ~15u; }
-constexpr uint32_t kSlotEnd16 = 0xFFFFu, kSlotEsc16 = 0xFFFEu;
-constexpr uint32_t kSlotEnd32 = 0xFFFFFFFFu, kSlotEsc32 = 0xFFFFFFFEu;
+__host__ __device__ inline uint32_t rec_short(uint32_t count, uint32_t sl) { return count | (sl << 16); }
 
 // 24-bit multiply (v_mul_u32_u24: full rate; a 32-bit v_mul_lo_u32 is quarter rate on CDNA)
 __host__ __device__ inline uint32_t mul24(uint32_t a, uint32_t b) {
@@ -256,22 +239,18 @@ struct Work {              // device pointers, sized by the host for one call
   uint32_t* list1;         // [n_tiles * kCap1]
   uint32_t* list2;         // [n_tiles * kCap2]
   uint32_t* list3;         // [n_tiles * kCap3]
-  uint32_t* tcnt;          // [n_tiles * kTileSlots] record of piece j (see kRecHit; u16 when rec16), then
-                           // (k_emit) a doc-start piece's first id within the tile
-  uint32_t rec16;          // 1: u16 records (kR16List)
-  uint32_t s16;            // 1: u16 id slots (narrow vocabularies, every id < kSlotEsc16)
-  uint64_t* dbits;         // [n_tiles * kTileSlots / 64] bit j: piece j of the tile starts a document
-  uint32_t* tlong;         // [n_tiles * kTLong] (rec16) first long-list index of each group of 64 pieces
-  void* slots;             // [n_tiles * slot_stride] id slots of the class lists (u16 when s16, else u32)
-  uint32_t slot_stride;    // id units per tile (slot_stride(k0))
-  void* ovf;               // ids of class-list pieces longer than their slot (u16 when s16, else u32)
-  uint32_t ovf_cap;        // id units of ovf (an append past it sets counters[kCtrOverflow])
+  uint32_t* tcnt;          // [n_tiles * kTileSlots] record of piece j (see kRecHit), then (k_emit) its
+                           // first id within the tile
   uint32_t* long_cnt;      // ids of long piece li (its length in bytes until a tier has run it)
   uint32_t* long_ord;      // long-list indices in descending length buckets (k_long_order)
   uint32_t* long_hist;     // [kLhWords] bucket counts | their exclusive scan | fill cursors | per-tier take counters
+  uint32_t* scratch;       // [n_tiles * kTileSlots] ids of the register passes' pieces, per tile and class region
   uint32_t* lids;          // ids of the long pieces: piece li's at lids[long_pos[li] ..] (sized after k_long_len)
   uint32_t* long_pos;      // [long capacity] id slot of long piece li (k_long_len: reserved from counters[kCtrLongIds])
   uint32_t* lw_pos;        // [long capacity] global-memory tier state of long piece li at lw + 4 * lw_pos[li]
+  uint32_t* rend;          // [kNumClasses][n_tiles] end of the consumed part of each class region (merge passes;
+                           // the dropped-byte pass allocates after it)
+  uint2* tregion;          // [n_tiles] class region bases of the tile in scratch (region_base)
   uint32_t long_cap, mid_cap;
   uint32_t unit;  // tiles per work unit of the register merge passes (8..64; chunks take 1..KT / unit units)  // long_list / mid_list entries (appends past them set counters[kCtrOverflow])
   uint64_t* long_list;     // pieces > kMedMax B (> kShortMax B in generic mode), or of unknown length

@@ -13,9 +13,9 @@
 //   docbits / pbits: 1 bit per byte (doc start / piece start), 4 KiB tiles of 64 64-byte words ->
 //   per tile: wpref (pieces before each word), three class lists of pieces still to merge,
 //   tile_np, tile_tok ->
-//   tcnt[tile][j] record of piece j (a whole-piece hit's id, a class-list entry, a long piece),
-//   the merge passes' ids in the class-list entries' id slots, tile_tok scanned to each tile's
-//   first id ->
+//   scratch[B] u32: the ids of a merged piece starting at byte s at scratch[s ...] ->
+//   tcnt[tile][j] record of piece j (a whole-piece hit carries its id), tile_tok scanned to each
+//   tile's first id ->
 //   ids[T] u32 + tok_off[D+1] u64 (output).
 // No array is indexed by a global piece number, so no pass has to wait for a global piece count.
 //
@@ -345,7 +345,7 @@ __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(
   // the 4 bytes before the context word, the context word, the tile, the look-ahead word, the 4
   // bytes after it
   __shared__ uint32_t s_text_all[kSegWaves][(kTileWords + 2) * 16 + 5];
-  __shared__ uint64_t s_D_all[kSegWaves][64];  // doc starts per word (-> the tile's dbits)
+  __shared__ uint64_t s_D_all[kSegWaves][64];  // doc starts per word (piece records carry kRecDoc)
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wid = uni(threadIdx.x >> 6);
   const uint32_t tile = uni(blockIdx.x * kSegWaves + wid);
@@ -564,10 +564,9 @@ __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(
   // table probes issued together (each round is one dependent global round trip)
   const bool generic = t.n_at != 0;  // added tokens can match inside pieces: no whole-piece shortcut
   uint32_t* tcnt = w.tcnt + (size_t)tile * kTileSlots;
-  uint16_t* tcnt16 = reinterpret_cast<uint16_t*>(w.tcnt) + (size_t)tile * kTileSlots;
-  const bool r16 = w.rec16 != 0;
   uint32_t hits = 0;
   uint32_t n0 = 0, n1 = 0, n2 = 0, n3 = 0;  // class-list lengths (wave-uniform)
+  uint32_t by0 = 0, by1 = 0, by2 = 0;        // this lane's bytes in class lists 0..2 (id regions)
   constexpr int U = kSegUnroll;
   constexpr uint32_t W = 64 * U;  // pieces per round
   for (uint32_t j0 = 0; j0 < np; j0 += W) {
@@ -635,16 +634,17 @@ __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(
 #undef CTOK_PROBE_USE
 #pragma unroll
     for (int u = 0; u < U; u++) {
+      const uint32_t j = j0 + 64 * u + lane;
+      uint32_t rec = 0;  // placeholder, rewritten by the pass that merges the piece
       // (written as flag arithmetic: an if / else-if chain assigning cls[u] in each arm was
       // miscompiled by this hipcc in the unrolled loop)
       if (cls[u] == 5) {
         const bool hit = hitv[u] != kNone;
+        rec = hit ? kRecHit | hitv[u] | (doc[u] ? kRecDoc : 0u) : 0u;
         hits += hit ? 1u : 0u;
         cls[u] = hit ? 4u : 0u;
       }
-      // doc-start pieces of the round: one bit per piece (k_emit writes tok_off from them)
-      const uint64_t dm = __ballot(doc[u] && j0 + 64 * u + lane < np);
-      if (lane == 0) w.dbits[(size_t)tile * (kTileSlots / 64) + (j0 >> 6) + u] = dm;
+      if (j < np) tcnt[j] = rec;  // every piece's slot: whole coalesced lines
     }
     {  // the tile's class-0 list is full: the rest of its class-0 pieces go to the long list (one
        // uniform test per round; the per-piece fix-up only in the rare round that crosses w.k0)
@@ -664,24 +664,19 @@ __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const uint32_t j = j0 + 64 * u + lane;
-      // the piece's record (written once, here): its id, its class-list entry, or its long-list index
-      uint32_t rec = r16 ? hitv[u] : kRecHit | hitv[u];
+      const uint32_t e = list_entry(sl[u], j, n[u]) | (doc[u] ? kEntDoc : 0u);
       {  // the wave owns its tile's lists: running counts in scalar registers, no atomics
         const uint64_t m0 = __ballot(cls[u] == 0);
         const uint64_t m1 = __ballot(cls[u] == 1), m2 = __ballot(cls[u] == 2);
         const uint64_t m3 = __ballot(cls[u] == 6);
         const uint64_t below = lanemask_lt();
-        const uint32_t c = cls[u] == 6 ? 3u : cls[u] <= 2 ? cls[u] : 4u;  // 4: not a class list
-        const uint32_t q = cls[u] == 0 ? n0 + __popcll(m0 & below)
-                         : cls[u] == 1 ? n1 + __popcll(m1 & below)
-                         : cls[u] == 2 ? n2 + __popcll(m2 & below)
-                                       : n3 + __popcll(m3 & below);
-        const uint32_t e = list_entry(sl[u], q, n[u]);  // (q: the entry's own index, for its id slot)
-        if (cls[u] == 0) w.list0[(size_t)tile * w.k0 + q] = e;
-        if (cls[u] == 1) w.list1[(size_t)tile * kCap1 + q] = e;
-        if (cls[u] == 2) w.list2[(size_t)tile * kCap2 + q] = e;
-        if (cls[u] == 6) w.list3[(size_t)tile * kCap3 + q] = e;
-        if (c < 4) rec = r16 ? kR16List + r16_base(c) + q : (c << 12) | q;
+        if (cls[u] == 0) w.list0[(size_t)tile * w.k0 + n0 + __popcll(m0 & below)] = e;
+        if (cls[u] == 1) w.list1[(size_t)tile * kCap1 + n1 + __popcll(m1 & below)] = e;
+        if (cls[u] == 2) w.list2[(size_t)tile * kCap2 + n2 + __popcll(m2 & below)] = e;
+        if (cls[u] == 6) w.list3[(size_t)tile * kCap3 + n3 + __popcll(m3 & below)] = e;
+        by0 += cls[u] == 0 ? n[u] : 0u;
+        by1 += cls[u] == 1 ? n[u] : 0u;
+        by2 += cls[u] == 2 ? n[u] : 0u;
         n0 += __popcll(m0);
         n1 += __popcll(m1);
         n2 += __popcll(m2);
@@ -693,25 +688,15 @@ __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(
         uint32_t b = 0;
         if (lane == leader) b = atomicAdd(&w.counters[0], (uint32_t)__popcll(lm));
         b = __builtin_amdgcn_readlane(b, leader);
-        const uint32_t below = __popcll(lm & lanemask_lt());
-        const uint32_t li = b + below;
-        if (cls[u] == 3) {
-          // u16 records: the piece's rank among this group's long pieces; the group's first
-          // long-list index in tlong (a group = 64 consecutive pieces j)
-          rec = r16 ? kR16Long + below : kRecLong | min(li, kRecLongMask);
-          if (li < w.long_cap) {
-            // the length when the piece ends within the look-ahead (0: k_long_len finds its end)
-            const uint32_t el = s_pos[64 * u + lane + 1];
-            const uint32_t ln = el == 0xFFFFu ? 0u : min(el - sl[u], 0x7FFFFu);
-            w.long_list[li] = (uint64_t)(t0 + sl[u]) | ((uint64_t)j << 32) | ((uint64_t)ln << 44);
-          }
+        const uint32_t li = b + __popcll(lm & lanemask_lt());
+        if (cls[u] == 3 && li < w.long_cap)
+        {
+          // the length when the piece ends within the look-ahead (0: k_long_len finds its end)
+          const uint32_t el = s_pos[64 * u + lane + 1];
+          const uint32_t ln = el == 0xFFFFu ? 0u : min(el - sl[u], 0x7FFFFu);
+          w.long_list[li] = (uint64_t)(t0 + sl[u]) | ((uint64_t)j << 32) | ((uint64_t)ln << 44) | (doc[u] ? kLongDoc : 0ull);
         }
-        if (r16 && lane == leader) w.tlong[(size_t)tile * kTLong + (j0 >> 6) + u] = b;
         if (lane == leader && b + __popcll(lm) > w.long_cap) atomicOr(&w.counters[kCtrOverflow], 1u);
-      }
-      if (j < np) {  // every piece's record: whole coalesced lines
-        if (r16) tcnt16[j] = (uint16_t)rec;
-        else tcnt[j] = rec;
       }
     }
     // every lane has read this round's s_pos before the next round's expansion overwrites it
@@ -720,12 +705,20 @@ __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
   hits = wave_sum_full_u32(hits);
+  by0 = wave_sum_full_u32(by0);
+  by1 = wave_sum_full_u32(by1);
+  by2 = wave_sum_full_u32(by2);
   nd = wave_sum_full_u32(nd);
   if (lane == 0) {
     w.tile_tok[tile] = hits;  // initial token count (the merge passes add theirs atomically)
     w.tile_doc[tile] = nd;
     w.tile_np[tile] = np;
+    // id regions of the register passes (ids <= bytes per piece; all four fit in kTileSlots:
+    // the lists hold pieces that start in the tile and end within its 62-byte look-ahead)
+    w.tregion[tile] = make_uint2(by0 | ((by0 + by1) << 16), by0 + by1 + by2);
   }
+  if (lane < kNumClasses)  // (the merge passes move them to the end of what they consumed)
+    w.rend[(size_t)lane * w.n_tiles + tile] = lane == 0 ? 0u : lane == 1 ? by0 : lane == 2 ? by0 + by1 : by0 + by1 + by2;
   if (lane < kNumClasses)
     w.tcls[(size_t)lane * w.n_tiles + tile] = lane == 0 ? n0 : lane == 1 ? n1 : lane == 2 ? n2 : n3;
   if (lane == 0 && n2) w.counters[kCtrAnyMid] = 1;  // plain stores: every writer stores 1
@@ -782,12 +775,12 @@ struct AddedMatch {  // first occurrence of added token k in bytes[0, n) honouri
 #define TOK(i) s_tok[(i) * NT + tid]
 #define RK(i) s_rk[(i) * NT + tid]
 
-// BPE over bytes[0, n) (n <= the slots per thread), ids to out[0], out[ostride], ...; returns the id count.
+// BPE over bytes[0, n) (n <= the slots per thread), appending ids to out; returns the id count.
 // s_tok / s_rk hold NT threads' slots interleaved.
 template <uint32_t NT>
 __device__ __forceinline__ uint32_t bpe_short(const Tables& t, const uint8_t* bytes, uint32_t n,
                                               const int32_t* s_b2id, uint32_t* s_tok, uint32_t* s_rk,
-                                              uint32_t tid, uint32_t* out, uint32_t ostride, uint32_t* err) {
+                                              uint32_t tid, uint32_t* out, uint32_t* err) {
   uint32_t m = 0;
   for (uint32_t i = 0; i < n; i++) {
     const int32_t id = s_b2id[bytes[i]];
@@ -810,7 +803,7 @@ __device__ __forceinline__ uint32_t bpe_short(const Tables& t, const uint8_t* by
       if (bi + 1 < m) RK(bi) = rank_of(t, TOK(bi), TOK(bi + 1), err);
     }
   }
-  for (uint32_t i = 0; i < m; i++) out[i * ostride] = TOK(i);
+  for (uint32_t i = 0; i < m; i++) out[i] = TOK(i);
   return m;
 }
 
@@ -820,12 +813,14 @@ __device__ __forceinline__ uint32_t bpe_short(const Tables& t, const uint8_t* by
 // binary search over those K offsets.  Token counts are summed per tile in LDS and added to
 // tile_tok with one atomic per (workgroup, tile); no two workgroups share a (class, tile).
 
-// s_tsum[l] counts the ids the pass produces in tile t0 + l (added to tile_tok at the flush).
+// s_tsum[l] starts at tile t0 + l's region base for class cls (tregion, cls >= 0) or at 0: the
+// merge passes allocate their ids from it (and add the difference to tile_tok at the flush).
 // (K <= 256 tiles: the first K/64 waves scan 64 counts each, then add the earlier waves' totals;
 // the workgroup has at least K threads)
 template <int K>
 __device__ __forceinline__ uint32_t tile_share_init(const uint32_t* counts, uint32_t n_tiles, uint32_t t0,
-                                                    uint32_t* s_pre, uint32_t* s_tsum) {
+                                                    uint32_t* s_pre, uint32_t* s_tsum, const uint2* tregion = nullptr,
+                                                    int cls = -1, uint32_t* s_tbase = nullptr) {
   static_assert(K >= 1 && K <= 256 && (K & (K - 1)) == 0, "K: power of two <= 256");
   constexpr uint32_t kW = (K + 63) / 64;
   __shared__ uint32_t s_wsum[4];
@@ -843,7 +838,10 @@ __device__ __forceinline__ uint32_t tile_share_init(const uint32_t* counts, uint
     for (uint32_t v = 0; v + 1 < kW; v++) inc += v < wv ? s_wsum[v] : 0u;
     if (l < K) {
       s_pre[l] = inc - c;
-      s_tsum[l] = 0;
+      uint32_t b0 = 0;
+      if (cls > 0 && in) b0 = region_base(tregion[t0 + l], cls);
+      s_tsum[l] = b0;
+      if (s_tbase) s_tbase[l] = b0;
     }
     if (l == (K < 64 ? 63u : (uint32_t)K - 1)) s_pre[K] = inc;
   }
@@ -861,114 +859,14 @@ __device__ __forceinline__ uint32_t tile_of(const uint32_t* s_pre, uint32_t q) {
 }
 
 template <int K>
-__device__ __forceinline__ void tile_share_flush(const Work& w, uint32_t t0, uint32_t t1, const uint32_t* s_tsum) {
+__device__ __forceinline__ void tile_share_flush(const Work& w, uint32_t t0, uint32_t t1, const uint32_t* s_tsum,
+                                                 const uint32_t* s_tbase = nullptr, int cls = -1) {
   __syncthreads();
   if (threadIdx.x < K && t0 + threadIdx.x < t1) {
-    const uint32_t v = s_tsum[threadIdx.x];
+    const uint32_t v = s_tsum[threadIdx.x] - (s_tbase ? s_tbase[threadIdx.x] : 0u);
     if (v) atomicAdd(&w.tile_tok[t0 + threadIdx.x], v);
+    if (cls >= 0 && v) w.rend[(size_t)cls * w.n_tiles + t0 + threadIdx.x] = s_tsum[threadIdx.x];
   }
-}
-
-// ------------------------------------------------------------------------------------------
-// Id slots of the class lists (ctok_internal.h slot_base): the merge pass that finishes entry q
-// of a tile's class-c list writes the piece's ids there, k_emit reads them; the record k_segment
-// wrote for the piece names the entry.
-
-template <bool S16>
-using SlotT = std::conditional_t<S16, uint16_t, uint32_t>;
-
-template <bool S16>
-__device__ __forceinline__ SlotT<S16>* slot_of(const Work& w, uint32_t tile, uint32_t c, uint32_t q) {
-  return reinterpret_cast<SlotT<S16>*>(w.slots) + (size_t)tile * w.slot_stride + slot_base(w.k0, (int)c) + q * slot_ids((int)c);
-}
-
-// ids past the slot: m units of Work::ovf (kCtrOvf counts them; past ovf_cap the call runs again
-// with the safe capacities); returns the position, or ~0 when out of room
-__device__ __forceinline__ uint32_t ovf_take(const Work& w, uint32_t m) {
-  const uint32_t o = atomicAdd(&w.counters[kCtrOvf], m);
-  if (o + m > w.ovf_cap) {
-    atomicOr(&w.counters[kCtrOverflow], 1u);
-    return ~0u;
-  }
-  return o;
-}
-
-// The slot of a class-C piece from the ids in registers tk[0 .. m) (compile-time indices): one to
-// four 16-byte stores (whole lines across the wave's consecutive entries).
-template <bool S16, int C, int N>
-__device__ __forceinline__ void put_slot(const Work& w, SlotT<S16>* slot, const uint32_t* tk, uint32_t m) {
-  constexpr uint32_t S = slot_ids(C);
-  static_assert(N >= (int)S, "slot wider than the tier");
-  constexpr uint32_t kEnd = S16 ? kSlotEnd16 : kSlotEnd32;
-  constexpr uint32_t H = C >= 2 ? 1u : 0u;  // classes 2, 3: the count first
-  uint32_t u[S];
-  if (m + H <= S) {
-#pragma unroll
-    for (int k = 0; k < (int)S; k++) {
-      const uint32_t v = tk[k >= (int)H ? k - (int)H : 0];
-      u[k] = k < (int)H ? m : (uint32_t)k < m + H ? v : kEnd;
-    }
-  } else {
-    const uint32_t o = ovf_take(w, m);
-    if (o != ~0u) {
-      SlotT<S16>* ov = reinterpret_cast<SlotT<S16>*>(w.ovf) + o;
-#pragma unroll
-      for (int k = 0; k < N; k++)
-        if ((uint32_t)k < m) ov[k] = (SlotT<S16>)tk[k];
-    }
-#pragma unroll
-    for (int k = 0; k < (int)S; k++) u[k] = kEnd;
-    u[0] = S16 ? kSlotEsc16 : kSlotEsc32;
-    u[1] = m;
-    if (S16) {
-      u[2] = o & 0xFFFFu;
-      u[3] = o >> 16;
-    } else {
-      u[2] = o;
-    }
-  }
-  if constexpr (S16) {
-    if constexpr (S == 4) {
-      *reinterpret_cast<uint2*>(slot) = make_uint2(u[0] | (u[1] << 16), u[2] | (u[3] << 16));
-    } else {
-#pragma unroll
-      for (int k = 0; k < (int)S; k += 8)
-        *reinterpret_cast<uint4*>(slot + k) = make_uint4(u[k] | (u[k + 1] << 16), u[k + 2] | (u[k + 3] << 16),
-                                                         u[k + 4] | (u[k + 5] << 16), u[k + 6] | (u[k + 7] << 16));
-    }
-  } else {
-#pragma unroll
-    for (int k = 0; k < (int)S; k += 4)
-      *reinterpret_cast<uint4*>(slot + k) = make_uint4(u[k], u[k + 1], u[k + 2], u[k + 3]);
-  }
-}
-
-// The same for the generic passes: class c and slot width chosen at run time, ids in LDS
-// (ids[k * stride]).
-__device__ void put_slot_any(const Work& w, uint32_t tile, uint32_t c, uint32_t q, const uint32_t* ids, uint32_t stride,
-                             uint32_t m) {
-  const uint32_t S = slot_ids((int)c), H = c >= 2 ? 1u : 0u;
-  auto put = [&](auto* slot, uint32_t kEnd, uint32_t kEsc) {
-    using T = std::remove_reference_t<decltype(*slot)>;
-    if (m + H <= S) {
-      for (uint32_t k = 0; k < S; k++) slot[k] = (T)(k < H ? m : k < m + H ? ids[(k - H) * stride] : kEnd);
-      return;
-    }
-    const uint32_t o = ovf_take(w, m);
-    if (o != ~0u)
-      for (uint32_t k = 0; k < m; k++) reinterpret_cast<T*>(w.ovf)[o + k] = (T)ids[k * stride];
-    for (uint32_t k = 0; k < S; k++) slot[k] = (T)kEnd;
-    slot[0] = (T)kEsc;
-    slot[1] = (T)m;
-    if (sizeof(T) == 2) {
-      slot[2] = (T)(o & 0xFFFFu);
-      slot[3] = (T)(o >> 16);
-    } else {
-      slot[2] = (T)o;
-    }
-  };
-  if (w.s16) put(slot_of<true>(w, tile, c, q), kSlotEnd16, kSlotEsc16);
-  else put(slot_of<false>(w, tile, c, q), kSlotEnd32, kSlotEsc32);
 }
 
 constexpr int kTilesGeneric = 2;  // tiles per workgroup, generic pass over list0
@@ -985,7 +883,6 @@ __global__ __launch_bounds__(MID ? 128 : 256) void k_bpe_generic(Work w, Tables 
   constexpr uint32_t SLOTS = MID ? kMedMax : kShortMax;
   __shared__ uint32_t s_tok[SLOTS * NT];
   __shared__ uint32_t s_rk[SLOTS * NT];
-  __shared__ uint32_t s_out[SLOTS * NT];  // the piece's ids (thread-interleaved), then its slot
   __shared__ int32_t s_b2id[256];
   __shared__ uint32_t s_pre[kTilesGeneric + 1], s_tsum[kTilesGeneric];
   const uint32_t tid = threadIdx.x;
@@ -1000,29 +897,33 @@ __global__ __launch_bounds__(MID ? 128 : 256) void k_bpe_generic(Work w, Tables 
     E = tile_share_init<kTilesGeneric>(w.tcls, w.n_tiles, t0, s_pre, s_tsum);
   }
   const uint32_t stride = MID ? gridDim.x * NT : NT;
-  uint32_t* out = s_out + tid;
   for (uint32_t q = (MID ? blockIdx.x * NT : 0) + tid; q < E; q += stride) {
-    uint32_t s, n, tile, kt = 0, c, qe;
+    uint32_t s, j, n, tile, kt = 0, doc;
     if (MID) {
       const uint64_t e = w.mid_list[q];
       s = (uint32_t)e;
-      c = (uint32_t)(e >> 44) & 3u;
-      qe = (uint32_t)(e >> 32) & 0xFFFu;
+      j = (uint32_t)(e >> 32) & 0xFFFu;
       n = (uint32_t)(e >> 48);
+      doc = (e & kMidDoc) ? kRecDoc : 0u;
       tile = s / kTile;
     } else {
       kt = tile_of<kTilesGeneric>(s_pre, q);
       tile = t0 + kt;
       const uint32_t e = w.list0[(size_t)tile * w.k0 + (q - s_pre[kt])];
       s = tile * kTile + (e & 0xFFFu);
-      c = 0;
-      qe = ent_q(e);
+      j = ent_j(e);
       n = ent_len(e);
+      doc = (e & kEntDoc) ? kRecDoc : 0u;
     }
     const uint8_t* bytes = w.text + s;
+    // ids go to the tile's region of the piece's length class, after what the merge passes used
+    // there (the region holds the bytes of every piece of the class: ids <= bytes)
+    const uint32_t cl = n <= 8 ? 0u : n <= 16 ? 1u : n <= 32 ? 2u : 3u;
+    const uint32_t pos = atomicAdd(&w.rend[(size_t)(MID ? cl : 0u) * w.n_tiles + tile], n);
+    uint32_t* out = w.scratch + (size_t)tile * kTileSlots + pos;
     uint32_t cnt = 0;
     if (t.n_at == 0) {
-      cnt = bpe_short<NT>(t, bytes, n, s_b2id, s_tok, s_rk, tid, out, NT, err);
+      cnt = bpe_short<NT>(t, bytes, n, s_b2id, s_tok, s_rk, tid, out, err);
     } else {
       // added-token split of the word (src/huggingface/mod.rs:566-610), on raw bytes
       uint32_t pos = 0;
@@ -1033,17 +934,17 @@ __global__ __launch_bounds__(MID ? 128 : 256) void k_bpe_generic(Work w, Tables 
           const uint32_t m = t.at_off[k + 1] - t.at_off[k];
           if (AddedMatch::find(t, k, bytes + pos, n - pos) == 0 && (best < 0 || m > blen)) { best = (int32_t)k; blen = m; }
         }
-        if (best >= 0) { out[NT * cnt++] = t.at_id[best]; pos += blen; continue; }
+        if (best >= 0) { out[cnt++] = t.at_id[best]; pos += blen; continue; }
         uint32_t nxt = n - pos;
         for (uint32_t k = 0; k < t.n_at; k++) {
           const int64_t f = AddedMatch::find(t, k, bytes + pos, n - pos);
           if (f > 0 && (uint32_t)f < nxt) nxt = (uint32_t)f;
         }
-        cnt += bpe_short<NT>(t, bytes + pos, nxt, s_b2id, s_tok, s_rk, tid, out + NT * cnt, NT, err);
+        cnt += bpe_short<NT>(t, bytes + pos, nxt, s_b2id, s_tok, s_rk, tid, out + cnt, err);
         pos += nxt;
       }
     }
-    put_slot_any(w, tile, c, qe, out, NT, cnt);
+    w.tcnt[(size_t)tile * kTileSlots + j] = rec_short(cnt, pos) | doc;
     if (MID) atomicAdd(&w.tile_tok[tile], cnt);
     else atomicAdd(&s_tsum[kt], cnt);
   }
@@ -1263,10 +1164,11 @@ __device__ __forceinline__ bool merge_slots(const Tables& t, const PairLds& P, u
 // Semantics are merge_slots': the lowest (rank, position) pair merges (src/bpe.rs:118-149).
 typedef __attribute__((address_space(3))) uint16_t lds_u16;
 
-// On return tk[0 .. m) holds the piece's ids.
-template <bool COMPACT, bool HOT, uint32_t NT>
-__device__ __forceinline__ uint32_t merge_lds8(const Tables& t, const PairLds& P, uint32_t* tk, const uint32_t* rk,
-                                               uint32_t m, lds_u32* s_key, lds_u16* s_tok, uint32_t* err) {
+// out_of(m) returns where the piece's m ids go (called once, after the last merge).
+template <bool COMPACT, bool HOT, uint32_t NT, typename OutOf>
+__device__ __forceinline__ uint32_t merge_lds8(const Tables& t, const PairLds& P, const uint32_t* tk, const uint32_t* rk,
+                                               uint32_t m, lds_u32* s_key, lds_u16* s_tok, uint32_t* err,
+                                               OutOf&& out_of) {
   const uint32_t tid = threadIdx.x;
 #pragma unroll
   for (int k = 0; k < 8; k++) {
@@ -1302,27 +1204,18 @@ __device__ __forceinline__ uint32_t merge_lds8(const Tables& t, const PairLds& P
     if (has_l) s_key[pv * NT + tid] = (rl << 3) | pv;
     s_key[bi * NT + tid] = has_r ? (rr << 3) | bi : ~0u;
   }
-  // live tokens in slot order to tk[0 .. m) (selects: compile-time register indices)
-  uint32_t tv[8];
+  // live tokens in slot order to out[0 .. m)
+  uint32_t* out = out_of(m);
 #pragma unroll
-  for (int k = 0; k < 8; k++) {
-    tv[k] = s_tok[k * NT + tid];
-    tk[k] = kDead;
-  }
-#pragma unroll
-  for (int k = 0; k < 8; k++) {
-    const bool live = (lv >> k) & 1u;
-    const uint32_t o = (uint32_t)__popc(lv & ((1u << k) - 1u));
-#pragma unroll
-    for (int i = 0; i <= k; i++) tk[i] = (live && o == (uint32_t)i) ? tv[k] : tk[i];
-  }
+  for (int k = 0; k < 8; k++)
+    if ((lv >> k) & 1u) out[__popc(lv & ((1u << k) - 1u))] = s_tok[k * NT + tid];
   return m;
 }
 
 // Workgroup-shared scratch of a merge pass.
 template <uint32_t SORTCAP, int KT = 64>
 struct PassLds {
-  uint32_t pre[KT + 1], tsum[KT], stat[2], bcnt[4], bfill[4], chunk, take, next;
+  uint32_t pre[KT + 1], tsum[KT], tbase[KT], stat[2], bcnt[4], bfill[4], chunk, take, next;
   uint16_t perm[SORTCAP];  // the chunk's entries ordered by length bucket
 };
 
@@ -1368,7 +1261,7 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
     const uint32_t c0 = S.chunk * U;
     if (c0 >= w.n_tiles) break;
     const uint32_t tb1 = min(w.n_tiles, c0 + U * S.take);
-    const uint32_t E = tile_share_init<K>(counts, tb1, c0, S.pre, S.tsum);
+    const uint32_t E = tile_share_init<K>(counts, tb1, c0, S.pre, S.tsum, w.tregion, LC::cls, S.tbase);
     if (E && !loaded) {  // E is workgroup-uniform (read from LDS after a barrier)
       load();
       loaded = true;
@@ -1418,7 +1311,7 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
     auto body = [&](uint32_t e, uint32_t kt, const uint32_t* wv) {
         const uint32_t tile = c0 + kt;
         const uint32_t s = tile * kTile + (e & 0xFFFu);
-        const uint32_t q = ent_q(e);
+        const uint32_t j = ent_j(e);
         const uint32_t n = ent_len(e);
         uint32_t tk[N], rk[N];
         bool missing = false;
@@ -1433,7 +1326,7 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
         if (missing) {  // a byte char absent from the vocab is dropped: generic path
           const uint32_t mi = atomicAdd(&w.counters[4], 1u);
           if (mi < w.mid_cap)
-            w.mid_list[mi] = (uint64_t)s | ((uint64_t)((LC::cls << 12) | q) << 32) | ((uint64_t)n << 48);
+            w.mid_list[mi] = (uint64_t)s | ((uint64_t)j << 32) | ((uint64_t)n << 48) | ((e & kEntDoc) ? kMidDoc : 0ull);
           else
             atomicOr(&w.counters[kCtrOverflow], 1u);
           return;
@@ -1464,15 +1357,23 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
         if constexpr (N >= 16) {
           if (more) more = merge_slots<16, COMPACT, HOT, L8>(t, P, tk, rk, m, 8, err);
         }
-        // the ids go to the entry's id slot (consecutive entries of a wave: whole lines); the
-        // record k_segment wrote names the entry
+        // ids go to the next free slots of the tile's region for this class (dense: a wave's
+        // stores fill whole lines), the record points at them
+        uint32_t pos = 0;
+        auto out_of = [&](uint32_t mm) {
+          pos = atomicAdd(&S.tsum[kt], mm);
+          return w.scratch + (size_t)tile * kTileSlots + pos;
+        };
         if (L8 && more) {
-          m = merge_lds8<COMPACT, HOT, NT>(t, P, tk, rk, m, s_key, s_tok, err);  // (tk[0 .. m): the ids)
-        } else if (!L8 && more) {
-          merge_slots<8, COMPACT, HOT, L8>(t, P, tk, rk, m, 0, err);
+          m = merge_lds8<COMPACT, HOT, NT>(t, P, tk, rk, m, s_key, s_tok, err, out_of);
+        } else {
+          if (!L8 && more) merge_slots<8, COMPACT, HOT, L8>(t, P, tk, rk, m, 0, err);
+          uint32_t* out = out_of(m);
+#pragma unroll
+          for (int k = 0; k < N; k++)
+            if ((uint32_t)k < m) out[k] = tk[k];
         }
-        put_slot<L8, LC::cls, N>(w, slot_of<L8>(w, tile, LC::cls, q), tk, m);
-        atomicAdd(&S.tsum[kt], m);  // (the tile's id count)
+        w.tcnt[(size_t)tile * kTileSlots + j] = rec_short(m, pos) | ((e & kEntDoc) ? kRecDoc : 0u);
         st_bytes += n;
         st_ids += m;
     };
@@ -1524,7 +1425,7 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
         if (i < E) body(e, kt, wv);
       }
     }
-    tile_share_flush<K>(w, c0, tb1, S.tsum);
+    tile_share_flush<K>(w, c0, tb1, S.tsum, S.tbase, LC::cls);
     // size the next chunk for about two entries per thread (up to K tiles): sparse classes take
     // several units at once, dense ones one; never more than a fair share of the units left, so
     // the last chunks stay small (C2: 504 units for 256 workgroups)
@@ -1937,6 +1838,8 @@ __global__ __launch_bounds__(256) void k_bpe_long(Work w, Tables t) {
   for (uint32_t li = uni(blockIdx.x * (blockDim.x >> 6) + wid); li < n_long; li += n_waves) {
     const uint64_t e = w.long_list[li];
     const uint32_t s = uni((uint32_t)e);
+    const uint32_t j = uni(long_j(e));
+    const uint32_t doc = (e & kLongDoc) ? kRecDoc : 0u;
     const uint32_t n = uni(piece_end(w, s) - s);
     // tiers: LDS up to kLdsPos positions, global memory beyond (only beyond the dense wave tiers
     // when those run, i.e. without added tokens)
@@ -1956,7 +1859,8 @@ __global__ __launch_bounds__(256) void k_bpe_long(Work w, Tables t) {
     }
     if (lane == 0) {
       const uint32_t tile = s / kTile;
-      w.long_cnt[li] = cnt;  // (k_segment's record of the piece names li)
+      w.long_cnt[li] = cnt;
+      w.tcnt[(size_t)tile * kTileSlots + j] = kRecLong | li | doc;
       atomicAdd(&w.tile_tok[tile], cnt);
     }
   }
@@ -2791,6 +2695,8 @@ __global__ __launch_bounds__(64 * NW) void k_bpe_wave(Work w, Tables t) {
     if (!SEG && n > HI) continue;
     const uint64_t e = w.long_list[li];
     const uint32_t s = uni((uint32_t)e);
+    const uint32_t j = uni(long_j(e));
+    const uint32_t doc = (e & kLongDoc) ? kRecDoc : 0u;
     uint32_t cnt;
     uint32_t* sink = &w.counters[kCtrSink];
     uint32_t* out = w.lids + w.long_pos[li];
@@ -2798,7 +2704,8 @@ __global__ __launch_bounds__(64 * NW) void k_bpe_wave(Work w, Tables t) {
     else cnt = bpe_wave_dense<K, HOT>(t, P, s_b2id, w.text + s, n, WaveSlice<K>{slice}, out, err, sink);
     if (lane == 0) {
       const uint32_t tile = s / kTile;
-      w.long_cnt[li] = cnt;  // (k_segment's record of the piece names li)
+      w.long_cnt[li] = cnt;
+      w.tcnt[(size_t)tile * kTileSlots + j] = kRecLong | li | doc;
       atomicAdd(&w.tile_tok[tile], cnt);
     }
   }
@@ -2891,53 +2798,26 @@ hipError_t launch_bpe_long(const Work& w, const Tables& t, hipStream_t s, uint32
 
 // ------------------------------------------------------------------------------------------
 // emission.  tile_tok is scanned to each tile's first id (tile_doc to its first document); then
-// one wavefront per tile walks the tile's piece records in rounds of 256 pieces: lane l takes
-// pieces 256 r + 4 l .. + 3 (one 8- or 16-byte record load; the next round's loads are issued
-// before this round's stores).  A whole-piece hit carries its id in the record; a merged piece's
-// record names its class-list entry, whose id slot is loaded at once (8 or 16 bytes: the ids of
-// nearly every <= 16 B piece, or the count and first ids of a longer one); a long piece's ids are
-// in lids.  A wave scan of the counts gives each piece's first id within the tile; the round's ids
-// are staged in LDS and written by the whole wave as consecutive dwords (whole lines).  Doc-start
-// pieces (the tile's dbits) give tok_off directly, or, with empty documents, leave their first id
-// within the tile in their record for k_tokoff.
+// one wavefront per tile walks the
+// tile's piece records in rounds of 256 pieces: lane l takes pieces 256 r + 4 l .. + 3 (one
+// 16-byte record load; the next round's loads are issued before this round's stores), a wave
+// scan gives each piece's first id within the tile, and the lane writes the ids itself: a
+// whole-piece hit carries its id in the record, a merged piece's ids are copied from scratch.
+// Consecutive lanes write consecutive id runs, so every cache line of the output is written
+// whole within a few store instructions.  A doc-start piece (kRecDoc) leaves its first id
+// within the tile in its record slot for k_tokoff.  No LDS, no barrier: occupancy is set by
+// VGPRs alone and the record -> scratch chains of 8 waves per SIMD overlap.
 
 constexpr int kEmitWaves = 4;  // tiles per k_emit workgroup
 constexpr uint32_t kEmitStage = 1024;  // ids of one round staged in LDS (4 KiB per wave)
 
-// One piece as k_emit sees it: n ids, the first ninl of them in the loaded words (from unit
-// off on), id i >= ninl at far[i] (u16 when far16, else u32).
-template <bool S16>
-struct EmitPiece {
-  uint32_t n, ninl, off;
-  std::conditional_t<S16, uint2, uint4> raw;
-  const void* far;
-  bool far16;
-  __device__ __forceinline__ uint32_t unit(int u) const {  // compile-time u
-    if constexpr (S16) {
-      const uint32_t d = u < 2 ? raw.x : u < 4 ? raw.y : 0u;
-      return (u & 1) ? d >> 16 : d & 0xFFFFu;
-    } else {
-      return u == 0 ? raw.x : u == 1 ? raw.y : u == 2 ? raw.z : u == 3 ? raw.w : 0u;
-    }
-  }
-  __device__ __forceinline__ uint32_t inl(int i) const { return off ? unit(i + 1) : unit(i); }
-  __device__ __forceinline__ uint32_t at(uint32_t i) const {
-    return far16 ? (uint32_t)reinterpret_cast<const uint16_t*>(far)[i] : reinterpret_cast<const uint32_t*>(far)[i];
-  }
-};
+__device__ __forceinline__ uint32_t rec_count(const Work& w, uint32_t v) {
+  return (v & kRecHit) ? 1u : (v & kRecLong) ? w.long_cnt[v & kRecLongMask] : (v & 0xFFFFu);
+}
 
-#ifndef CTOK_EMIT_WPE
-#define CTOK_EMIT_WPE 7
-#endif
-template <bool R16, bool S16>
-__global__ __launch_bounds__(64 * kEmitWaves) __attribute__((amdgpu_waves_per_eu(CTOK_EMIT_WPE))) void k_emit(Work w, uint32_t* __restrict__ ids, uint64_t ids_cap,
+__global__ __launch_bounds__(64 * kEmitWaves) void k_emit(Work w, uint32_t* __restrict__ ids, uint64_t ids_cap,
                                                          uint64_t* __restrict__ tok_off) {
   if (spec_failed(w)) return;
-  // a list outgrew its capacity (records may name entries nothing was written for): the host runs
-  // the call again with the safe capacities
-  if (uni(w.counters[kCtrOverflow]) != 0) return;
-  using Slot = SlotT<S16>;
-  constexpr uint32_t kEnd = S16 ? kSlotEnd16 : kSlotEnd32, kEsc = S16 ? kSlotEsc16 : kSlotEsc32;
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t tile = uni(blockIdx.x * kEmitWaves + (threadIdx.x >> 6));
   if (tile >= w.n_tiles) return;
@@ -2948,17 +2828,9 @@ __global__ __launch_bounds__(64 * kEmitWaves) __attribute__((amdgpu_waves_per_eu
   const bool direct = uni(w.counters[kCtrEmptyDocs]) == 0;
   uint32_t drun = uni(w.tile_doc[tile]);
   uint32_t* tcnt = w.tcnt + (size_t)tile * kTileSlots;
-  uint16_t* tcnt16 = reinterpret_cast<uint16_t*>(w.tcnt) + (size_t)tile * kTileSlots;
-  const uint64_t* dbits = w.dbits + (size_t)tile * (kTileSlots / 64);
-  const Slot* slots = reinterpret_cast<const Slot*>(w.slots) + (size_t)tile * w.slot_stride;
-  auto load = [&](uint32_t j0) -> uint4 {
-    if (j0 >= np) return make_uint4(0, 0, 0, 0);
-    if constexpr (R16) {
-      const uint2 v = *reinterpret_cast<const uint2*>(tcnt16 + j0);
-      return make_uint4(v.x & 0xFFFFu, v.x >> 16, v.y & 0xFFFFu, v.y >> 16);
-    } else {
-      return *reinterpret_cast<const uint4*>(tcnt + j0);
-    }
+  const uint32_t* src0 = w.scratch + (size_t)tile * kTileSlots;
+  auto load = [&](uint32_t j0) {
+    return j0 < np ? *reinterpret_cast<const uint4*>(tcnt + j0) : make_uint4(0, 0, 0, 0);
   };
   uint32_t run = 0;  // ids of the earlier rounds (wave-uniform)
   uint32_t r_first = 0;  // the current round's first id within the tile (wave-uniform)
@@ -2969,117 +2841,79 @@ __global__ __launch_bounds__(64 * kEmitWaves) __attribute__((amdgpu_waves_per_eu
     const uint32_t j0 = r0 + 4 * lane;
     const uint32_t rec[4] = {nx.x, nx.y, nx.z, nx.w};
     if (r0 + 256 < np) nx = load(j0 + 256);
-    const uint32_t nlive = j0 < np ? min(np - j0, 4u) : 0u;
-    const uint32_t dm = (uint32_t)(dbits[(r0 >> 6) + (lane >> 4)] >> ((4 * lane) & 63)) & ((1u << nlive) - 1u);
-    // the records; every slot / long-piece load of the lane's pieces in flight together (records
-    // past np are stale: nothing is followed for them)
-    EmitPiece<S16> pc[4];
-    uint32_t kind[4];  // 0 none, 1 hit, 2 slot of class 0/1, 3 slot of class 2/3, 4 long
+    uint32_t c[4], sum = 0;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-      const uint32_t r = rec[k];
-      EmitPiece<S16>& p = pc[k];
-      p.n = 0;
-      p.ninl = 0;
-      p.off = 0;
-      p.far = w.lids;
-      p.far16 = false;
-      if constexpr (S16) p.raw = make_uint2(0, 0);
-      else p.raw = make_uint4(0, 0, 0, 0);
-      uint32_t c, q, id;
-      bool hit, lng;
-      if constexpr (R16) {
-        hit = r < kR16List;
-        lng = r >= kR16Long;
-        const uint32_t x = r - kR16List;
-        c = x < r16_base(1) ? 0u : x < r16_base(2) ? 1u : x < r16_base(3) ? 2u : 3u;
-        q = x - r16_base(c);
-        id = r;
-      } else {
-        hit = (r & kRecHit) != 0;
-        lng = !hit && (r & kRecLong) != 0;
-        c = (r >> 12) & 3u;
-        q = r & 0xFFFu;
-        id = r & kRecIdMask;
-      }
-      kind[k] = (uint32_t)k >= nlive ? 0u : hit ? 1u : lng ? 4u : c < 2 ? 2u : 3u;
-      if (kind[k] == 1) {
-        p.n = 1;
-        p.ninl = 1;
-        p.raw.x = id;
-      } else if (kind[k] == 4) {
-        const uint32_t li = R16 ? w.tlong[(size_t)tile * kTLong + ((j0 + k) >> 6)] + (r - kR16Long) : (r & kRecLongMask);
-        p.n = w.long_cnt[li];
-        p.far = w.lids + w.long_pos[li];
-      } else if (kind[k] >= 2) {
-        const Slot* sp = slots + slot_base(w.k0, (int)c) + q * slot_ids((int)c);
-        if constexpr (S16) p.raw = *reinterpret_cast<const uint2*>(sp);
-        else p.raw = *reinterpret_cast<const uint4*>(sp);
-        p.far = sp;
-        p.far16 = S16;
-      }
-    }
-    // the merged pieces' counts from their slots
-    uint32_t sum = 0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      EmitPiece<S16>& p = pc[k];
-      if (kind[k] == 2 || kind[k] == 3) {
-        const uint32_t u0 = p.unit(0), u1 = p.unit(1), u2 = p.unit(2), u3 = p.unit(3);
-        if (u0 == kEsc) {  // the ids in ovf
-          p.n = u1;
-          p.far = reinterpret_cast<const Slot*>(w.ovf) + (S16 ? (u2 | (u3 << 16)) : u2);
-        } else if (kind[k] == 3) {  // count, then the ids: id i at unit i + 1
-          p.n = u0;
-          p.off = 1;
-          p.ninl = min(u0, 3u);
-          p.far = reinterpret_cast<const Slot*>(p.far) + 1;
-        } else {
-          p.n = u0 == kEnd ? 0u : u1 == kEnd ? 1u : u2 == kEnd ? 2u : u3 == kEnd ? 3u : 4u;
-          p.ninl = p.n;
-        }
-      }
-      sum += p.n;
+      c[k] = j0 + k < np ? rec_count(w, rec[k]) : 0u;
+      sum += c[k];
     }
     const uint32_t inc = wave_incl_scan(sum);
     uint32_t o = run + inc - sum;
     run = uni(run + lane63(inc));
     uint32_t dord = 0;  // this lane's first doc-start piece's document (direct mode)
     if (direct) {
-      const uint32_t nd = (uint32_t)__popc(dm);
+      uint32_t nd = 0;
+#pragma unroll
+      for (int k = 0; k < 4; k++) nd += (j0 + k < np && (rec[k] & kRecDoc)) ? 1u : 0u;
       const uint32_t dinc = wave_incl_scan(nd);
       dord = drun + dinc - nd;
       drun = uni(drun + lane63(dinc));
     }
+    // first ids: all loads of this lane's pieces in flight together
+    // (records past np are stale: c[k] == 0 keeps them from being followed)
+    const uint32_t* sp[4];
+    uint32_t v0[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint32_t r = rec[k];
+      const bool follow = c[k] != 0 && !(r & kRecHit);
+      sp[k] = !follow ? src0
+              : (r & kRecLong) ? w.lids + w.long_pos[r & kRecLongMask]
+              : src0 + ((r >> 16) & 0xFFFu);
+      v0[k] = (r & kRecHit) ? (r & kRecIdMask) : (follow ? sp[k][0] : 0u);
+    }
     // the round's ids: staged in LDS when they fit, then written out by the whole wave as 64
-    // consecutive dwords per store (whole lines); else each lane stores its runs itself
+    // consecutive dwords per store (whole lines; the lanes' own runs are ~5 ids apart, so direct
+    // stores touch a dozen partial lines each); else each lane stores its runs itself
     const uint32_t r_ids = run - r_first;
     const bool staged = r_ids <= kEmitStage;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-      const EmitPiece<S16>& p = pc[k];
-      const uint32_t cj = p.n;
-      auto put = [&](uint32_t i, uint32_t v) {
-        if (staged) stage[o - r_first + i] = v;
-        else if (base + o + i < ids_cap) ids[base + o + i] = v;  // the host reports CTOK_E_CAPACITY when short
-      };
+      const uint32_t r = rec[k], cj = c[k];
+      const uint64_t dst = base + o;
+      if (staged) {
+        const uint32_t so = o - r_first;
+        if (cj > 0) stage[so] = v0[k];
+        if (cj > 1) {
+          const uint32_t* spk = sp[k];
+          for (uint32_t m = 1; m < cj; m += 4) {
+            uint32_t x[4];
 #pragma unroll
-      for (int i = 0; i < 4; i++)
-        if ((uint32_t)i < p.ninl) put(i, p.inl(i));
-      for (uint32_t m = p.ninl; m < cj; m += 4) {  // the rest: four loads in flight at a time
-        uint32_t x[4];
+            for (int i = 0; i < 4; i++) x[i] = m + i < cj ? spk[m + i] : 0u;
 #pragma unroll
-        for (int i = 0; i < 4; i++) x[i] = m + i < cj ? p.at(m + i) : 0u;
+            for (int i = 0; i < 4; i++)
+              if (m + i < cj) stage[so + m + i] = x[i];
+          }
+        }
+      } else {
+        if (cj > 0 && dst < ids_cap) ids[dst] = v0[k];
+        if (cj > 1) {  // merged / long piece: the rest of its ids, four loads in flight at a time
+          const uint32_t* spk = sp[k];
+          for (uint32_t m = 1; m < cj; m += 4) {
+            uint32_t x[4];
 #pragma unroll
-        for (int i = 0; i < 4; i++)
-          if (m + i < cj) put(m + i, x[i]);
+            for (int i = 0; i < 4; i++) x[i] = m + i < cj ? spk[m + i] : 0u;
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+              if (m + i < cj && dst + m + i < ids_cap) ids[dst + m + i] = x[i];  // the host reports CTOK_E_CAPACITY when short
+          }
+        }
       }
-      if ((dm >> k) & 1u) {
+      if ((r & kRecDoc) && j0 + k < np) {
         if (direct) tok_off[dord++] = base + o;
-        else if (R16) tcnt16[j0 + k] = (uint16_t)o;  // read by k_tokoff
-        else tcnt[j0 + k] = o;
+        else tcnt[j0 + k] = o;  // read by k_tokoff
       }
-      if (!R16 && w.keep_first && (uint32_t)k < nlive) tcnt[j0 + k] = o;  // ctok_encode_offsets
+      if (w.keep_first && j0 + k < np) tcnt[j0 + k] = o;  // ctok_encode_offsets
       o += cj;
     }
     if (staged) {
@@ -3106,8 +2940,7 @@ __device__ __forceinline__ void tokoff_one(const Work& w, uint64_t* __restrict__
     uint32_t below = __popc(w.pbits[2 * g] & (b >= 32 ? ~0u : ((1u << b) - 1u)));
     if (b > 32) below += __popc(w.pbits[2 * g + 1] & ((1u << (b - 32)) - 1u));
     const uint32_t j = w.wpref[(size_t)tile * 64 + (g - tile * kTileWords)] + below;
-    r = (uint64_t)w.tile_tok[tile] + (w.rec16 ? (uint32_t)reinterpret_cast<const uint16_t*>(w.tcnt)[(size_t)tile * kTileSlots + j]
-                                             : w.tcnt[(size_t)tile * kTileSlots + j]);
+    r = (uint64_t)w.tile_tok[tile] + w.tcnt[(size_t)tile * kTileSlots + j];
   }
   tok_off[d] = r;
 }
@@ -3125,12 +2958,8 @@ __global__ void k_tokoff(Work w, uint64_t* __restrict__ tok_off) {
 hipError_t launch_emit(const Work& w, uint32_t* ids, uint64_t ids_cap, uint64_t* tok_off, hipStream_t s) {
   HIPCHK(scan_u32(w.tile_tok, w.tile_tok, (uint64_t)w.n_tiles, nullptr, w.scan_tmp, w.scan_tmp_cap, s));
   HIPCHK(scan_u32(w.tile_doc, w.tile_doc, (uint64_t)w.n_tiles, nullptr, w.scan_tmp, w.scan_tmp_cap, s));
-  if (w.n_tiles) {
-    const uint32_t g = (w.n_tiles + kEmitWaves - 1) / kEmitWaves;
-    if (w.rec16) k_emit<true, true><<<g, 64 * kEmitWaves, 0, s>>>(w, ids, ids_cap, tok_off);
-    else if (w.s16) k_emit<false, true><<<g, 64 * kEmitWaves, 0, s>>>(w, ids, ids_cap, tok_off);
-    else k_emit<false, false><<<g, 64 * kEmitWaves, 0, s>>>(w, ids, ids_cap, tok_off);
-  }
+  if (w.n_tiles)
+    k_emit<<<(w.n_tiles + kEmitWaves - 1) / kEmitWaves, 64 * kEmitWaves, 0, s>>>(w, ids, ids_cap, tok_off);
   // (grid-stride: with no empty document only tok_off[n_docs] is left to write)
   k_tokoff<<<std::min<uint32_t>((w.n_docs + 1 + 255) / 256, 4096), 256, 0, s>>>(w, tok_off);
   return hipGetLastError();
