@@ -32,6 +32,7 @@
 
 #include "../../include/ctok.h"
 #include "ctok_internal.h"
+#include "gen/regex_props.h"
 #include "gen/unicode_data.h"
 #include "json.hpp"
 
@@ -501,50 +502,212 @@ void parse_post_processor(ctok* t, const ctj::Value* v) {
   }
 }
 
-// Does the Rust regex crate compile pattern p?  It has no look-around, atomic groups or
-// backreferences, and rejects unbalanced groups and classes; the reference then drops the Split
-// (src/pretokenizers.rs:298-302).  Returns "" when none of these is found (taken as compiling),
-// else the construct that makes it fail.  Scanned token by token: an escaped character or anything
-// inside a character class ([...], nested classes allowed) is a literal, so "[(?=]" or "\\(?="
-// do not count as look-ahead.  (Other reasons the crate may reject a pattern -- an unknown \p{..}
-// name, a bad repetition -- are not detected: such a Split is refused loudly, never applied.)
+// Does the Rust regex crate compile pattern p?  The reference compiles a Split's pattern and, when
+// Regex::new fails, leaves the text unsplit (src/pretokenizers.rs:277-302): the Split is a no-op.
+// The crate (regex ^1.10, Cargo.toml:19; the regex-syntax grammar) has no look-around,
+// backreferences, atomic groups, branch resets, comments or conditionals, rejects unknown escapes,
+// a repetition with nothing to repeat, an inverted {n,m}, unbalanced groups / classes, unknown ASCII
+// classes and \p{..} names that are not Unicode property names or values (UAX #44 loose matching;
+// gen/regex_props.h, from the `regex` module's tables: a superset of the crate's).  This walks the
+// pattern with that grammar and returns the first construct the crate rejects, "" when there is
+// none.  It errs one way only: what it cannot decide counts as compiling (verbose-mode patterns,
+// hex escapes, Age=), and a compiling Split is refused by the loader (CTOK_E_UNSUPPORTED), never
+// silently dropped.  Possessive quantifiers (a++) are a repetition of a repetition to regex-syntax:
+// they compile.  Restated for the tests by oracle/rust_regex.py.
+namespace rxs {
+
+std::string canon(std::string_view s) {
+  std::string o;
+  for (char c : s)
+    if (c != ' ' && c != '_' && c != '-' && c != '\t' && c != '\n') o += (char)toupper((unsigned char)c);
+  return o;
+}
+
+template <size_t N>
+bool in_table(const char* const (&tab)[N], const std::string& k) {
+  return std::binary_search(tab, tab + N, k.c_str(), [](const char* a, const char* b) { return strcmp(a, b) < 0; });
+}
+
+bool single_known(const std::string& c) {
+  if (in_table(ct_prop_single, c)) return true;
+  return c.size() > 2 && c.compare(0, 2, "IS") == 0 && in_table(ct_prop_single, c.substr(2));  // "is" prefix
+}
+
+// \p{body}: a property the crate may know (name=value for gc / sc / scx / gcb / wb / sb, age
+// taken as known; other properties the tables know: taken as known, a name they do not: unknown)
+bool property_known(std::string_view body) {
+  for (std::string_view sep : {std::string_view("!="), std::string_view("="), std::string_view(":")}) {
+    const size_t at = body.find(sep);
+    if (at == std::string_view::npos) continue;
+    std::string k = canon(body.substr(0, at)), v = canon(body.substr(at + sep.size()));
+    if (k == "AGE") return true;
+    static const std::map<std::string, std::string> kv = {
+        {"GC", "GC"}, {"GENERALCATEGORY", "GC"}, {"SC", "SC"}, {"SCRIPT", "SC"}, {"SCX", "SCX"},
+        {"SCRIPTEXTENSIONS", "SCX"}, {"GCB", "GCB"}, {"GRAPHEMECLUSTERBREAK", "GCB"}, {"WB", "WB"},
+        {"WORDBREAK", "WB"}, {"SB", "SB"}, {"SENTENCEBREAK", "SB"}};
+    auto it = kv.find(k);
+    if (it != kv.end()) return in_table(ct_prop_kv, it->second + "=" + v);
+    return in_table(ct_prop_other, k);
+  }
+  return single_known(canon(body));
+}
+
+}  // namespace rxs
+
 std::string rust_regex_rejects(const std::string& p) {
-  int cls = 0;    // character-class nesting depth
-  int group = 0;  // open groups
-  for (size_t i = 0; i < p.size(); i++) {
+  const size_t n = p.size();
+  size_t i = 0;
+  int depth = 0;
+  std::vector<bool> empty{true};  // per open group: nothing to repeat yet
+  auto is_alnum = [](char c) { return isalnum((unsigned char)c) != 0; };
+  // at p[j] == '\\' (inside or outside a class): "" or the reason; j moves past the escape
+  auto escape = [&](size_t& j) -> std::string {
+    if (j + 1 >= n) return "trailing backslash";
+    const char c = p[j + 1];
+    if (c >= '1' && c <= '9') return std::string("backreference \\") + c;
+    if (c == 'k') return "named backreference \\k";
+    if (c == 'g') return "backreference \\g";
+    if (c == 'p' || c == 'P') {
+      if (j + 2 >= n) return "incomplete \\p escape";
+      if (p[j + 2] == '{') {
+        const size_t e = p.find('}', j + 3);
+        if (e == std::string::npos) return "unclosed \\p{";
+        const std::string body = p.substr(j + 3, e - j - 3);
+        j = e + 1;
+        return rxs::property_known(body) ? "" : "unknown Unicode property \\p{" + body + "}";
+      }
+      const std::string body(1, p[j + 2]);
+      j += 3;
+      return rxs::property_known(body) ? "" : "unknown Unicode property \\p" + body;
+    }
+    j += 2;
+    if (c == 'x' || c == 'u' || c == 'U') return "";  // (hex escapes: taken as valid)
+    if (is_alnum(c) && !strchr("aftnrvAzbBdDsSwW", c)) return std::string("unrecognized escape \\") + c;
+    return "";
+  };
+  while (i < n) {
     const char c = p[i];
     if (c == '\\') {
-      if (i + 1 < p.size() && p[i + 1] >= '1' && p[i + 1] <= '9') return "backreference \\" + std::string(1, p[i + 1]);
-      i++;
+      const std::string why = escape(i);
+      if (!why.empty()) return why;
+      empty.back() = false;
       continue;
     }
-    if (cls) {
-      if (c == '[') cls++;
-      else if (c == ']') cls--;
-      continue;
-    }
-    if (c == '[') {
-      cls = 1;
-      if (i + 1 < p.size() && p[i + 1] == '^') i++;
-      if (i + 1 < p.size() && p[i + 1] == ']') i++;  // a leading ']' is a literal
+    if (c == '[') {  // class: nested classes, escapes, [:name:]; a leading ']' is literal
+      size_t j = i + 1;
+      if (j < n && p[j] == '^') j++;
+      if (j < n && p[j] == ']') j++;
+      int cd = 1;
+      while (j < n && cd) {
+        const char d = p[j];
+        if (d == '\\') {
+          const std::string why = escape(j);
+          if (!why.empty()) return why;
+          continue;
+        }
+        if (d == '[' && j + 1 < n && p[j + 1] == ':') {
+          const size_t e = p.find(":]", j + 2);
+          if (e != std::string::npos) {
+            std::string nm = p.substr(j + 2, e - j - 2);
+            if (!nm.empty() && nm[0] == '^') nm.erase(0, 1);
+            static const char* const kAscii[] = {"alnum", "alpha", "ascii", "blank", "cntrl", "digit", "graph",
+                                                 "lower", "print", "punct", "space", "upper", "word", "xdigit"};
+            if (std::find_if(std::begin(kAscii), std::end(kAscii), [&](const char* a) { return nm == a; }) == std::end(kAscii))
+              return "unknown ASCII class [:" + nm + ":]";
+            j = e + 2;
+            continue;
+          }
+        }
+        if (d == '[') {
+          cd++;
+          j++;
+          if (j < n && p[j] == '^') j++;
+          if (j < n && p[j] == ']') j++;
+          continue;
+        }
+        if (d == ']') cd--;
+        j++;
+      }
+      if (cd) return "unclosed character class";
+      i = j;
+      empty.back() = false;
       continue;
     }
     if (c == '(') {
-      group++;
-      if (i + 2 < p.size() && p[i + 1] == '?') {
-        const char d = p[i + 2];
-        if (d == '=') return "look-ahead (?=";
-        if (d == '!') return "negative look-ahead (?!";
-        if (d == '>') return "atomic group (?>";
-        if (d == '<' && i + 3 < p.size() && p[i + 3] == '=') return "look-behind (?<=";
-        if (d == '<' && i + 3 < p.size() && p[i + 3] == '!') return "negative look-behind (?<!";
+      if (i + 1 < n && p[i + 1] == '?') {
+        const std::string_view rest = std::string_view(p).substr(i + 2);
+        auto starts = [&](const char* s) { return rest.compare(0, strlen(s), s) == 0; };
+        if (starts("=") || starts("!")) return std::string("look-ahead (?") + rest[0];
+        if (starts("<=") || starts("<!")) return "look-behind (?" + std::string(rest.substr(0, 2));
+        if (starts(">")) return "atomic group (?>";
+        if (starts("P=")) return "named backreference (?P=";
+        if (!rest.empty() && (strchr("|#('&R+0", rest[0]) || isdigit((unsigned char)rest[0])))
+          return std::string("unsupported group (?") + rest[0];
+        if (starts("P<") || starts("<")) {
+          const size_t k = i + 2 + (starts("P<") ? 2 : 1);
+          const size_t e = p.find('>', k);
+          if (e == std::string::npos) return "unclosed group name";
+          const std::string name = p.substr(k, e - k);
+          bool ok = !name.empty() && (isalpha((unsigned char)name[0]) || name[0] == '_');
+          for (char ch : name) ok = ok && (is_alnum(ch) || ch == '_' || ch == '.' || ch == '[' || ch == ']');
+          if (!ok) return "invalid group name " + name;
+          i = e + 1;
+        } else {  // flags: (?flags) or (?flags:...)
+          size_t k = i + 2;
+          while (k < n && strchr("imsxuUR-", p[k])) {
+            if (p[k] == 'x') return "";  // verbose mode (comments, ignored space): not walked; taken as compiling
+            k++;
+          }
+          if (k >= n || (p[k] != ':' && p[k] != ')')) return std::string("unrecognized flag ") + (k < n ? p.substr(k, 1) : "(end)");
+          i = k + 1;
+          if (p[k] == ')') continue;
+        }
+      } else {
+        i++;
       }
-    } else if (c == ')') {
-      if (--group < 0) return "unbalanced ')'";
+      depth++;
+      empty.push_back(true);
+      continue;
     }
+    if (c == ')') {
+      if (--depth < 0) return "unbalanced ')'";
+      empty.pop_back();
+      empty.back() = false;
+      i++;
+      continue;
+    }
+    if (c == '|') {
+      empty.back() = true;
+      i++;
+      continue;
+    }
+    if (c == '*' || c == '+' || c == '?') {
+      if (empty.back()) return "repetition operator missing expression";
+      i++;
+      continue;
+    }
+    if (c == '{') {  // counted repetition {n}, {n,}, {n,m}; anything else is not walked further
+      const size_t e = p.find('}', i);
+      if (e != std::string::npos) {
+        const std::string body = p.substr(i + 1, e - i - 1);
+        const size_t comma = body.find(',');
+        const std::string a = body.substr(0, comma), b = comma == std::string::npos ? "" : body.substr(comma + 1);
+        auto digits = [](const std::string& s) { return !s.empty() && std::all_of(s.begin(), s.end(), ::isdigit); };
+        if (digits(a) && (comma == std::string::npos || b.empty() || digits(b))) {
+          if (empty.back()) return "repetition operator missing expression";
+          if (!b.empty() && std::stoull(b) < std::stoull(a)) return "invalid repetition range {" + body + "}";
+          i = e + 1;
+          continue;
+        }
+      }
+      empty.back() = false;
+      i++;
+      continue;
+    }
+    empty.back() = false;
+    i++;
   }
-  if (cls) return "unclosed character class";
-  if (group) return "unclosed group";
+  if (depth) return "unclosed group";
   return "";
 }
 
@@ -570,8 +733,9 @@ void parse_pre_tokenizer(const ctj::Value* v, std::vector<std::pair<char, bool>>
     }
     if (rust_regex_rejects(pat).empty())
       throw_err(CTOK_E_UNSUPPORTED, "Split pre-tokenizer with a pattern the Rust regex crate compiles is outside the "
-                                    "encode hot path: no look-around, atomic group, backreference or unbalanced "
-                                    "group / class found, so the pattern is taken as compiling (pattern: " + pat + ")");
+                                    "encode hot path: nothing the crate rejects (look-around, backreference, atomic "
+                                    "group, unknown escape or \\p{..} name, unbalanced group / class) was found, so "
+                                    "the pattern is taken as compiling (pattern: " + pat + ")");
     chain.push_back({'S', false});
   } else if (ty == "Sequence" && depth == 0) {
     const ctj::Value* ps = v->get("pretokenizers");

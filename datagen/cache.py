@@ -17,13 +17,22 @@ import time
 import numpy as np
 
 
+def _generator_key() -> str:
+    """Short hash of the corpus generator's source: a cached corpus is reused only by the
+    generator that wrote it (a changed generator writes new files instead of reading stale ones)."""
+    import hashlib
+    src = os.path.join(os.path.dirname(os.path.abspath(__file__)), "corpus.py")
+    with open(src, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:12]
+
+
 def path_of(outdir: str, name: str) -> str:
-    return os.path.join(outdir, name + ".npz")
+    return os.path.join(outdir, "%s.%s.npz" % (name, _generator_key()))
 
 
 def _save(outdir, name, text, off):
     p = path_of(outdir, name)
-    tmp = p + ".tmp.npz"
+    tmp = "%s.%d.tmp.npz" % (p, os.getpid())  # (per writer: concurrent builders never share a temp file)
     np.savez(tmp, text=text, off=off)
     os.replace(tmp, p)
 
@@ -41,6 +50,8 @@ def build(outdir: str, names) -> None:
             text, off = c5
         elif name == "C5NFC":
             text, off = corpus.corpus_c5nfc(base=c5)
+        elif name == "C4":  # 10M docs: independent 1M-doc blocks on worker processes
+            text, off = corpus.corpus_c4(workers=min(16, len(os.sched_getaffinity(0))))
         else:
             text, off = corpus.CONFIGS[name]()
         _save(outdir, name, text, off)

@@ -65,41 +65,10 @@ def deserialize_merges(items):
 
 
 def rust_regex_compiles(pattern: str) -> bool:
-    """Whether Rust `regex::Regex::new` accepts `pattern` (no look-around / backrefs / atomic
-    groups, balanced groups and classes).  Token scan: escaped characters and character-class
-    contents are literals."""
-    p, i, cls, group = pattern, 0, 0, 0
-    while i < len(p):
-        c = p[i]
-        if c == "\\":
-            if i + 1 < len(p) and p[i + 1] in "123456789":
-                return False
-            i += 2
-            continue
-        if cls:
-            cls += 1 if c == "[" else -1 if c == "]" else 0
-            i += 1
-            continue
-        if c == "[":
-            cls = 1
-            if p[i + 1:i + 2] == "^":
-                i += 1
-            if p[i + 1:i + 2] == "]":
-                i += 1
-            i += 1
-            continue
-        if c == "(":
-            group += 1
-            if p[i + 1:i + 2] == "?":
-                d = p[i + 2:i + 3]
-                if d in ("=", "!", ">") or (d == "<" and p[i + 3:i + 4] in ("=", "!")):
-                    return False
-        elif c == ")":
-            group -= 1
-            if group < 0:
-                return False
-        i += 1
-    return cls == 0 and group == 0
+    """Whether Rust `regex::Regex::new` accepts `pattern` (src/pretokenizers.rs:277-302): the
+    regex-syntax grammar walk of oracle/rust_regex.py."""
+    from oracle import rust_regex
+    return rust_regex.compiles(pattern)
 
 
 def parse_normalizer(value):

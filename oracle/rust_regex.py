@@ -1,0 +1,230 @@
+"""Does Rust's `regex::Regex::new` reject a Split pattern?  (Test infrastructure: the oracle's
+restatement of the decision the product makes in ctok_host.cpp `rust_regex_rejects`.)
+
+The reference compiles a Split pre-tokenizer's pattern on every call and, when `Regex::new` fails,
+returns the text unsplit (/root/reference/src/pretokenizers.rs:277-302): the Split is a no-op.  The
+regex crate (`regex ^1.10`, /root/reference/Cargo.toml:19; grammar of its regex-syntax crate) has
+no look-around, backreferences, atomic groups, branch resets, comments or conditionals, and its
+\\p{..} names are the Unicode property names and values of UAX #44 (loose matching: case,
+spaces, '_' and '-' ignored, an "is" prefix allowed).
+
+This walks the pattern with that grammar and returns the first construct Rust rejects ("" when
+none is found).  The decision errs one way only: a construct this module is unsure about counts
+as compiling, and a Split whose pattern compiles is refused by the loader with an error (this
+repo runs the fixed GPT-2 split only) -- never silently dropped.  Possessive quantifiers (`a++`)
+are not an error in regex-syntax (a repetition of a repetition), so such patterns compile.
+"""
+import os
+import sys
+
+_ESC_OK = set("aftnrvAzbBdDsSwW<>")  # escapes regex-syntax knows (besides p/P, x/u/U, meta characters)
+_ASCII_CLASSES = {"alnum", "alpha", "ascii", "blank", "cntrl", "digit", "graph", "lower", "print", "punct",
+                  "space", "upper", "word", "xdigit"}
+# properties regex-syntax takes in the name=value form; Age is not in the `regex` module's tables:
+# taken as known
+_KV_PROPS = {"GC": "GC", "GENERALCATEGORY": "GC", "SC": "SC", "SCRIPT": "SC", "SCX": "SCX",
+             "SCRIPTEXTENSIONS": "SCX", "GCB": "GCB", "GRAPHEMECLUSTERBREAK": "GCB", "WB": "WB",
+             "WORDBREAK": "WB", "SB": "SB", "SENTENCEBREAK": "SB"}
+_TABLES = None
+
+
+def tables():
+    """The property names of the `regex` module's tables (single names, PROP=VALUE, other
+    properties): what complexity-tokenizer_amd/tools/gen_regex_props.py writes into the product's
+    gen/regex_props.h."""
+    global _TABLES
+    if _TABLES is None:
+        here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        sys.path.insert(0, os.path.join(here, "complexity-tokenizer_amd", "tools"))
+        try:
+            import gen_regex_props
+        finally:
+            sys.path.pop(0)
+        single, kv, other = gen_regex_props.tables()
+        _TABLES = set(single), set(kv), set(other)
+    return _TABLES
+
+
+def canon(name: str) -> str:
+    return "".join(ch for ch in name.upper() if ch not in " _-\t\n")
+
+
+def property_known(body: str) -> bool:
+    """\\p{body} names a property the regex crate may know (loose matching; an "is" prefix allowed)."""
+    single, kv, other = tables()
+    for sep in ("!=", "=", ":"):
+        if sep in body:
+            k, v = body.split(sep, 1)
+            kc = canon(k)
+            if kc == "AGE":
+                return True
+            if kc in _KV_PROPS:
+                return "%s=%s" % (_KV_PROPS[kc], canon(v)) in kv
+            return kc in other
+    c = canon(body)
+    return c in single or (len(c) > 2 and c.startswith("IS") and c[2:] in single)
+
+
+def rejects(p: str) -> str:
+    """The first construct of `p` that Rust's regex crate rejects, or "" (taken as compiling)."""
+    n = len(p)
+    i = 0
+    depth = 0
+    empty = [True]  # per open group: nothing to repeat yet (start of the group / after '|')
+
+    def prop(j):  # at p[j] == 'p' / 'P' after a backslash: returns (reason, next index)
+        if j + 1 >= n:
+            return "incomplete \\p escape", n
+        if p[j + 1] == "{":
+            e = p.find("}", j + 2)
+            if e < 0:
+                return "unclosed \\p{", n
+            body = p[j + 2:e]
+            return ("" if property_known(body) else "unknown Unicode property \\p{%s}" % body), e + 1
+        return ("" if property_known(p[j + 1]) else "unknown Unicode property \\p%s" % p[j + 1]), j + 2
+
+    def escape(j):  # at p[j] == '\\': (reason, next index); inside or outside a class
+        if j + 1 >= n:
+            return "trailing backslash", n
+        c = p[j + 1]
+        if c in "123456789":
+            return "backreference \\" + c, n
+        if c == "k":
+            return "named backreference \\k", n
+        if c == "g":
+            return "backreference \\g", n
+        if c in "pP":
+            return prop(j + 1)
+        if c in "xuU":
+            return "", j + 2  # (hex escapes: taken as valid)
+        if c.isascii() and c.isalnum() and c not in _ESC_OK:
+            return "unrecognized escape \\" + c, n
+        return "", j + 2
+
+    while i < n:
+        c = p[i]
+        if c == "\\":
+            why, i = escape(i)
+            if why:
+                return why
+            empty[-1] = False
+            continue
+        if c == "[":
+            # character class: nested classes, escapes, [:name:] ASCII classes; ']' first is literal
+            j = i + 1
+            if j < n and p[j] == "^":
+                j += 1
+            if j < n and p[j] == "]":
+                j += 1
+            cdepth = 1
+            while j < n and cdepth:
+                d = p[j]
+                if d == "\\":
+                    why, j = escape(j)
+                    if why:
+                        return why
+                    continue
+                if d == "[" and p[j + 1:j + 2] == ":":
+                    e = p.find(":]", j + 2)
+                    if e >= 0:
+                        nm = p[j + 2:e].lstrip("^")
+                        if nm not in _ASCII_CLASSES:
+                            return "unknown ASCII class [:%s:]" % nm
+                        j = e + 2
+                        continue
+                if d == "[":
+                    cdepth += 1
+                    j += 1
+                    if j < n and p[j] == "^":
+                        j += 1
+                    if j < n and p[j] == "]":
+                        j += 1
+                    continue
+                if d == "]":
+                    cdepth -= 1
+                j += 1
+            if cdepth:
+                return "unclosed character class"
+            i = j
+            empty[-1] = False
+            continue
+        if c == "(":
+            if p.startswith("(?", i):
+                rest = p[i + 2:]
+                if rest.startswith(("=", "!")):
+                    return "look-ahead (?" + rest[0]
+                if rest.startswith(("<=", "<!")):
+                    return "look-behind (?" + rest[:2]
+                if rest.startswith(">"):
+                    return "atomic group (?>"
+                if rest.startswith("P="):
+                    return "named backreference (?P="
+                if rest.startswith(("|", "#", "(", "'", "&", "R", "+", "0")) or (rest[:1].isascii() and rest[:1].isdigit()):
+                    return "unsupported group (?" + rest[:1]
+                if rest.startswith(("P<", "<")):
+                    k = i + 2 + (2 if rest.startswith("P<") else 1)
+                    e = p.find(">", k)
+                    if e < 0:
+                        return "unclosed group name"
+                    name = p[k:e]
+                    if not name or not (name[0].isascii() and name[0].isalpha() or name[0] == "_") or \
+                            not all(ch.isascii() and ch.isalnum() or ch in "_.[]" for ch in name):
+                        return "invalid group name " + name
+                    i = e + 1
+                else:  # flags: (?flags) or (?flags:...)
+                    k = i + 2
+                    while k < n and p[k] in "imsxuUR-":
+                        if p[k] == "x":
+                            return ""  # verbose mode (comments, ignored space): not walked; taken as compiling
+                        k += 1
+                    if k >= n or p[k] not in ":)":
+                        return "unrecognized flag " + (p[k] if k < n else "(end)")
+                    if p[k] == ")":
+                        i = k + 1
+                        continue
+                    i = k + 1
+            else:
+                i += 1
+            depth += 1
+            empty.append(True)
+            continue
+        if c == ")":
+            depth -= 1
+            if depth < 0:
+                return "unbalanced ')'"
+            empty.pop()
+            empty[-1] = False
+            i += 1
+            continue
+        if c == "|":
+            empty[-1] = True
+            i += 1
+            continue
+        if c in "*+?":
+            if empty[-1]:
+                return "repetition operator missing expression"
+            i += 1
+            continue
+        if c == "{":
+            e = p.find("}", i)
+            body = p[i + 1:e] if e >= 0 else None
+            a, comma, b = (body or "").partition(",")
+            if body is not None and a.isascii() and a.isdigit() and (not b or b.isascii() and b.isdigit()):
+                if empty[-1]:
+                    return "repetition operator missing expression"
+                if b and int(b) < int(a):
+                    return "invalid repetition range {%s}" % body
+                i = e + 1
+                continue
+            i += 1  # (anything else: not walked further; taken as compiling)
+            empty[-1] = False
+            continue
+        empty[-1] = False
+        i += 1
+    if depth:
+        return "unclosed group"
+    return ""
+
+
+def compiles(p: str) -> bool:
+    return rejects(p) == ""

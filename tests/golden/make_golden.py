@@ -77,6 +77,38 @@ CONFIGS = {  # name -> (tokenizer fixture, corpus fn)
 }
 
 
+_PIN = {}
+
+
+def _pin_init(obj):
+    _PIN["py"] = ref_py.RefTokenizer(obj)
+
+
+def _pin_chunk(docs):
+    return _PIN["py"].encode_batch(docs)
+
+
+def ref_py_packed(obj, docs, workers=6):
+    """ref_py over `docs` on a pool of worker processes (the Python restatement is slow: ~1.5 ms per
+    C5 document); (ids, tok_off) packed like the C oracle's."""
+    import multiprocessing as mp
+    step = max(1, len(docs) // (workers * 8))
+    chunks = [docs[i:i + step] for i in range(0, len(docs), step)]
+    with mp.get_context("fork").Pool(workers, initializer=_pin_init, initargs=(obj,)) as pool:
+        res = [r for part in pool.map(_pin_chunk, chunks) for r in part]
+    ids = np.array([i for r in res for i in r], dtype=np.uint32)
+    tok_off = np.zeros(len(res) + 1, dtype=np.uint64)
+    np.cumsum([len(r) for r in res], out=tok_off[1:])
+    return ids, tok_off
+
+
+# The C oracle (which produces every full-config digest) pinned against the Python restatement on
+# the first PIN_DOCS documents of each config (SURVEY.md 8(d): >= 100k): ref_py uses the `regex`
+# module and `unicodedata` directly, the C oracle the generated tables of csrc/gen/unicode_data.h,
+# so the pin also covers the tables on the config's text.  Recorded as pin_ref_py in digests.json.
+PIN_DOCS = {"C2": 100_000, "C5": 100_000, "C5NFC": 100_000, "C3": 3000, "C3TT": 3000}
+
+
 def big(name):
     tok, fn = CONFIGS[name]
     obj = load(tok)
@@ -85,12 +117,15 @@ def big(name):
     print(name, "corpus", len(off) - 1, "docs", len(text), "bytes in %.1fs" % (time.time() - t))
     rc = ref_c.RefC(obj)
     py = ref_py.RefTokenizer(obj)
-    # pin the C oracle against the Python restatement on a sample of this corpus
-    ns = 3000
+    # pin the C oracle against the Python restatement on the config's first PIN_DOCS documents
+    ns = PIN_DOCS[name]
     sample_docs = [d.decode() for d in corpus.unpack(text[: int(off[ns])], off[: ns + 1])]
-    want = py.encode_batch(sample_docs)
-    got = rc.encode_batch(sample_docs)
-    assert want == got, name + ": C oracle disagrees with ref_py on the sample"
+    t = time.time()
+    pid, poff = ref_py_packed(obj, sample_docs)
+    cid, coff = rc.encode_packed(text[: int(off[ns])], off[: ns + 1])
+    assert np.array_equal(pid, cid) and np.array_equal(poff, coff), name + ": C oracle disagrees with ref_py"
+    print(name, "ref_py == C oracle on the first %d docs (%.0f s)" % (ns, time.time() - t), flush=True)
+    del py
     t = time.time()
     ids, tok_off = rc.encode_packed(text, off)
     print(name, "C oracle %.1fs" % (time.time() - t), len(ids), "ids")
@@ -100,7 +135,8 @@ def big(name):
     d = json.load(open(path)) if os.path.exists(path) else {}
     d[name] = {"tokenizer": tok, "docs": len(off) - 1, "bytes": int(len(text)), "tokens": int(len(ids)),
                "sha256": digest(ids, tok_off), "first_docs": n1, "first_tokens": int(len(ids1)),
-               "first_sha256": digest(ids1, off1)}
+               "first_sha256": digest(ids1, off1),
+               "pin_ref_py": {"docs": ns, "tokens": int(len(pid)), "sha256": digest(pid, poff)}}
     with open(path, "w") as f:
         json.dump(d, f, indent=1, sort_keys=True)
 

@@ -63,6 +63,11 @@ def test_full_config_digest(request, cfg):
     ids, toff = _encode_device(tok, text, off)
     assert len(ids) == gold["tokens"], cfg
     assert digest(ids, toff) == gold["sha256"], "%s (device path) differs from the C-oracle digest" % cfg
+    # the first 100k documents against the Python restatement's digest (regex + unicodedata, not
+    # the generated tables the C oracle shares with the product: make_golden.py pin_ref_py)
+    pin = gold["pin_ref_py"]
+    n = pin["docs"]
+    assert digest(ids[: int(toff[n])], toff[: n + 1]) == pin["sha256"], "%s: first %d docs differ from ref_py" % (cfg, n)
     if cfg == "C5NFC":
         assert tok.last_stats["nfc_docs"] > 0
     elif cfg == "C5":  # no NFC-active text: nothing flagged (a false flag costs a splice, round 4)

@@ -169,14 +169,33 @@ def test_shard_bounds_cover_and_balance():
     assert ids.tolist() == [1, 2, 3] and toff.tolist() == [0, 2, 2, 3]
 
 
-@pytest.mark.parametrize("pattern,compiles", [
-    ("\\s+(?!\\S)|\\s+", False),      # look-ahead: Rust's regex rejects it, the Split is a no-op
-    ("(?<=a)b", False), ("(?>ab)", False), ("(\\w)\\1", False),
-    ("[(?=]x", True),                 # '(?=' inside a character class is literal
-    ("\\(?=x", True),                 # escaped '(' : a literal paren, then an optional '='
-    ("[^]](?=x)", False), ("(?<name>a)b", True), ("\\s+", True),
-    ("(ab", False), ("ab)", False), ("[ab", False), ("(a[)]b)", True),  # unbalanced: rejected
-])
+# Split patterns and whether Rust's regex crate compiles them (regex-syntax grammar; the reference
+# drops a Split it cannot compile, src/pretokenizers.rs:298-302).  A compiling one is refused here.
+SPLIT_PATTERNS = [
+    ("\\s+(?!\\S)|\\s+", False),             # look-ahead: the Llama-3 / GPT-4 style patterns
+    ("(?i:'s|'t|'re|'ve|'m|'ll|'d)|[^\\r\\n\\p{L}\\p{N}]?\\p{L}+|\\p{N}{1,3}| ?[^\\s\\p{L}\\p{N}]+[\\r\\n]*|\\s*[\\r\\n]+|\\s+(?!\\S)|\\s+",
+     False),
+    ("(?<=a)b", False), ("(?<!a)b", False), ("a(?=b)", False),  # look-behind / look-ahead
+    ("(?>ab)", False),                       # atomic group
+    ("(\\w)\\1", False), ("(?P<x>a)(?P=x)", False), ("(?<x>a)\\k<x>", False),  # backreferences
+    ("(?|a|b)", False), ("(?#note)a", False), ("(?(1)a|b)", False),  # branch reset, comment, conditional
+    ("\\p{Foo}+", False), ("\\p{sc=Nope}", False), ("\\p{InBasicLatin}", False),  # unknown \p names
+    ("a\\Z", False), ("\\Ga", False),          # escapes the crate does not have
+    ("*a", False), ("a|+b", False), ("(?:*)", False), ("a{3,2}", False),  # nothing to repeat, bad range
+    ("[[:foo:]]", False),                    # unknown ASCII class
+    ("(ab", False), ("ab)", False), ("[ab", False),  # unbalanced
+    ("[(?=]x", True),                        # '(?=' inside a character class is literal
+    ("\\(?=x", True),                        # escaped '(' : a literal paren, then an optional '='
+    ("[^]](?=x)", False), ("(?<name>a)b", True), ("(?P<n>a)", True), ("\\s+", True),
+    ("(a[)]b)", True), ("\\p{L}+|\\p{N}+", True), ("\\p{Greek}\\p{IsLatin}\\pL", True),
+    ("\\p{Script=Han}|\\p{gc=Lu}|\\p{scx:Kana}", True), ("[\\p{L}&&\\p{Greek}]", True),
+    ("a++b*+", True),                        # possessive: a repetition of a repetition to regex-syntax
+    ("(?i)abc(?-i:d)", True), ("x{2,}y{,}z{3}", True), ("[[:alpha:][:digit:]]", True),
+    ("(?x) a # (?= comment", True),          # verbose mode: not walked, taken as compiling
+]
+
+
+@pytest.mark.parametrize("pattern,compiles", SPLIT_PATTERNS)
 def test_split_pattern_compilability(pattern, compiles):
     """A Split whose pattern Rust's regex compiles would split (unsupported here: loud error); one it
     cannot compile is skipped by the reference (src/pretokenizers.rs:298-330): the tokenizer loads.

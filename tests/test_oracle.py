@@ -102,6 +102,20 @@ def test_golden_c2_first_100k_c_oracle(gpt2_obj):
     assert len(ids) == gold["first_tokens"] and _digest(ids, toff) == gold["first_sha256"]
 
 
+@pytest.mark.parametrize("cfg", ["C2", "C5", "C5NFC"])
+def test_golden_digests_pinned_to_ref_py(cfg):
+    """The C oracle writes every full-config digest; tests/golden/make_golden.py first runs the
+    Python restatement (`regex` + `unicodedata`, no generated table) on the config's first 100k
+    documents and stores its digest (pin_ref_py), which must equal the C oracle's digest of the
+    same documents (first_sha256, recomputed for C2 by test_golden_c2_first_100k_c_oracle; the GPU
+    full-config tests compare the product's first 100k documents with it too)."""
+    with open(os.path.join(GOLDEN, "digests.json")) as f:
+        gold = json.load(f)[cfg]
+    pin = gold["pin_ref_py"]
+    assert pin["docs"] >= 100_000 and pin["docs"] == gold["first_docs"]
+    assert pin["sha256"] == gold["first_sha256"] and pin["tokens"] == gold["first_tokens"]
+
+
 # ----------------------------------------------------------------- the two oracles agree
 
 def test_c_oracle_matches_python_oracle(gpt2_obj):

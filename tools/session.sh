@@ -50,8 +50,9 @@ for step in "$@"; do
       IFS=: read -r _ cfg fx la lb <<< "$step"
       for i in 1 2 3; do
         for L in "$la" "$lb"; do
-          CTOK_LIB=$L timeout -k 10 300 python -u tools/probe.py "$cfg" "$fx" 5 2>/dev/null | grep -E "MB/s|ms_" | sed "s|^|$(basename "$L") |" \
-            | tee -a "$OUT/ab_${cfg}_${fx}.txt"
+          CTOK_LIB=$L timeout -k 10 300 python -u tools/probe.py "$cfg" "$fx" 5 2>>"$OUT/ab_${cfg}.err" > "$OUT/ab_run.txt" \
+            || { echo "probe failed: $L"; tail -5 "$OUT/ab_${cfg}.err"; exit 1; }
+          grep -E "MB/s|ms_" "$OUT/ab_run.txt" | sed "s|^|$(basename "$L") |" | tee -a "$OUT/ab_${cfg}_${fx}.txt"
         done
       done ;;
     abenv:*)  # bench.py A/B of the working tree's library without / with an environment setting
