@@ -374,14 +374,25 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(tok_path, text, off, args.cpu_seconds)
-        traffic = None  # HBM bytes per launch of the dominant kernel from the committed PMC passes
+        # HBM bytes per launch of the dominant kernel from the committed PMC passes -- only when
+        # they profiled this very library build (sha256 of the loaded libctok.so) and workload
+        traffic, traffic_src = None, "no PMC record for this workload"
         tr_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(tr_path):
+            from complexity_tokenizer import _native
+            with open(_native.LIB_PATH, "rb") as fh:
+                lib_sha = hashlib.sha256(fh.read()).hexdigest()
             tr = json.load(open(tr_path))
-            if tr.get("workload") == "%s/%d" % (args.config, n_docs):
+            if tr.get("workload") != "%s/%d" % (args.config, n_docs):
+                pass
+            elif tr.get("lib_sha256") != lib_sha:
+                traffic_src = "PMC record of another libctok.so build (%s), not this one (%s): unmeasured" % (
+                    str(tr.get("lib_sha256"))[:12], lib_sha[:12])
+            else:
                 per = tr.get("hbm_bytes_per_launch", {})
                 hits = [v for k, v in per.items() if k.split("<")[0] == dom]
                 traffic = hits[0] if len(hits) == 1 else None
+                traffic_src = "profiles/pmc_traffic.json (FETCH_SIZE x2 + WRITE_SIZE, libctok.so sha256 %s)" % lib_sha[:12]
         ms_step = elapsed_max / args.steps * 1e3
         cfg = dict(desc)
         cfg.update({"docs_per_gpu": n_docs, "bytes_per_gpu": n_bytes, "tokens_per_gpu": int(T),
@@ -402,6 +413,7 @@ def main():
             "config": cfg,
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(ach, 2), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 5), "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "alg_bytes_per_launch": int(alg_dom), "ms_per_launch": round(ms_dom, 4),
                          "kernels": {k: {"ms": round(v[0], 4), "alg_bytes": int(v[1]),
                                          "GBps": round(v[1] / (v[0] * 1e-3) / 1e9, 2)} for k, v in kernels.items()}},

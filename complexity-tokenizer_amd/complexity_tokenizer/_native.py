@@ -67,7 +67,8 @@ class Stats(ctypes.Structure):
                 ("tokens", ctypes.c_uint64), ("nfc_docs", ctypes.c_uint64), ("ms_segment", ctypes.c_double),
                 ("ms_bpe_lo", ctypes.c_double), ("ms_bpe_hi", ctypes.c_double),
                 ("class_bytes", ctypes.c_uint64 * 4), ("class_ids", ctypes.c_uint64 * 4),
-                ("ms_bpe_med", ctypes.c_double), ("workspace_bytes", ctypes.c_uint64)]
+                ("ms_bpe_med", ctypes.c_double), ("workspace_bytes", ctypes.c_uint64),
+                ("long_rounds", ctypes.c_uint64)]
 
     def as_dict(self):
         d = {}

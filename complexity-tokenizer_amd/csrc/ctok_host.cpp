@@ -9,6 +9,7 @@
 //   vocab getters     src/vocab.rs:34-100, src/huggingface/mod.rs:856-866
 //   decode            src/huggingface/mod.rs:698-785, src/decoders.rs:74-119, parsing.rs:272-364
 #include <emmintrin.h>
+#include <sched.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -41,6 +42,28 @@ using namespace ctok_dev;
 namespace {
 
 thread_local std::string g_err;
+
+// CPUs this process may run on: the affinity mask capped by the cgroup v2 quota (cpu.max), as
+// Rust's available_parallelism (rayon's default pool, reference src/huggingface/mod.rs:695)
+// counts them on Linux.  Cached: read once per process.
+unsigned usable_cpus_once() {
+  static const unsigned n = [] {
+    unsigned c = std::max(1u, std::thread::hardware_concurrency());
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof(set), &set) == 0) c = std::max(1, CPU_COUNT(&set));
+    if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+      char q[32] = {0};
+      unsigned long long period = 0;
+      if (fscanf(f, "%31s %llu", q, &period) == 2 && strcmp(q, "max") != 0 && period > 0) {
+        const unsigned long long quota = strtoull(q, nullptr, 10);
+        c = std::min<unsigned>(c, (unsigned)std::max<unsigned long long>(1, quota / period));
+      }
+      fclose(f);
+    }
+    return c;
+  }();
+  return n;
+}
 
 int fail(int code, const std::string& msg) {
   g_err = msg;
@@ -1171,7 +1194,7 @@ void load_root(ctok* t, const ctj::Value& root) {
     items.reserve(t->vocab.size());
     for (const auto& kv : t->vocab) items.push_back({&kv.first, kv.second});
     // the reference merge loop (src/bpe.rs:88-153) on each entry's bytes, vocab split over threads
-    const unsigned nth = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const unsigned nth = std::min(16u, usable_cpus_once());
     std::vector<std::vector<std::pair<std::string, uint32_t>>> part(nth);
     auto work = [&](unsigned w) {
       std::vector<uint32_t> cps, tk;
@@ -1778,6 +1801,7 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
     st->long_pieces = cnt[0];
     st->tokens = ntok;
     st->workspace_bytes = ds->workspace_bytes();
+    st->long_rounds = cnt[kCtrRounds];
     st->nfc_docs = nfc_docs;
     for (int c = 0; c < kNumClasses; c++) {
       st->class_bytes[c] = cnt[ctr_stat(c)];
@@ -2136,6 +2160,7 @@ RangeOut encode_host_range(ctok* t, DeviceState* ds, const uint8_t* text, const 
     if (st) {
       st->pieces += cs.pieces;
       st->long_pieces += cs.long_pieces;
+      st->long_rounds += cs.long_rounds;
       st->nfc_docs += cs.nfc_docs;
       st->workspace_bytes = std::max(st->workspace_bytes, cs.workspace_bytes);
       st->bytes_norm += cs.bytes_norm;
@@ -2190,6 +2215,7 @@ int run(const std::function<void()>& f);
 namespace ctok_host {
 [[noreturn]] void throw_error(int code, const std::string& msg) { throw_err(code, msg); }
 int run_guarded(const std::function<void()>& f) { return run(f); }
+unsigned usable_cpus() { return usable_cpus_once(); }
 
 // NFC (when the tokenizer normalises) + ByteLevel pre-tokenization of n_docs host texts on device
 // dev: the text the pieces index (normalised when normalisation ran), its doc offsets, and the
@@ -2502,7 +2528,7 @@ int ctok_encode_batch(const ctok* tc, const uint8_t* utf8_in, const uint64_t* do
     else devs.push_back(exec ? exec->device : 0);
     const bool timing = exec && (exec->flags & CTOK_F_TIMING);
     const uint64_t chunk = (uint64_t)(exec && exec->chunk_mb ? exec->chunk_mb : 64u) << 20;
-    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const unsigned hw = usable_cpus_once();
     const unsigned nthr = exec && exec->host_threads ? exec->host_threads
                                                      : std::max(1u, std::min(8u, hw / (unsigned)devs.size()));  // (widening threads: 4 / 8 / 16 within run-to-run noise on C2, profiles/r03/v22_e2e_probe.txt, v27_*; 8 + the pipeline threads stay inside a 16-CPU quota)
     if (stats) *stats = ctok_stats{};
@@ -2605,6 +2631,7 @@ int ctok_encode_batch(const ctok* tc, const uint8_t* utf8_in, const uint64_t* do
       for (size_t g = 0; g < G; g++) {
         const ctok_stats& q = sst[g];
         stats->pieces += q.pieces, stats->long_pieces += q.long_pieces, stats->nfc_docs += q.nfc_docs;
+        stats->long_rounds += q.long_rounds;
         stats->workspace_bytes += q.workspace_bytes;  // (shards on one device report it once each)
         stats->bytes_norm += q.bytes_norm;
         for (int c = 0; c < kNumClasses; c++)
@@ -2967,7 +2994,7 @@ int ctok_encode_offsets(const ctok* tc, const uint8_t* utf8, const uint64_t* doc
       if (k != toff[d + 1]) throw_err(CTOK_E_DEVICE, "offsets: ids and words disagree");
     }
     };
-    const unsigned nth = n_docs < 256 ? 1u : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const unsigned nth = n_docs < 256 ? 1u : std::min(16u, usable_cpus_once());
     std::vector<std::exception_ptr> errs(nth);
     std::vector<std::thread> th;
     for (unsigned w = 0; w < nth; w++) {

@@ -47,6 +47,7 @@ constexpr int kCtrSink = 31;       // counters[31]: panic bits of lookups whose 
 constexpr int kCtrOverflow = 25;   // counters[25] != 0: a list outgrew its lean capacity (the host reruns the call safe)
 constexpr int kCtrLongIds = 26;    // counters[26]: long-piece id slots reserved (k_long_len: a piece's bytes)
 constexpr int kCtrLwWords = 27;    // counters[27]: global-memory long-piece state reserved (4 u32 per byte)
+constexpr int kCtrRounds = 29;     // counters[29]: rounds of the LDS wave tiers (statistics: ctok_stats.long_rounds)
 // Long-piece order (long_hist, u32[kLhWords], zeroed per call): pieces in descending length
 // buckets of 64 B (bucket d = 64 - (n - 1) / 64, d = 0 for n > 4096), so every wave tier's pieces
 // are a contiguous range of long_ord, longest first.

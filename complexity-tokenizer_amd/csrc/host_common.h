@@ -16,4 +16,7 @@ int run_guarded(const std::function<void()>& f);
 // (NFC-normalised when normalisation ran), its doc offsets and the piece-start bitmap.
 void pretokenize(ctok* t, int dev, const uint8_t* utf8, const uint64_t* doc_off, uint64_t n_docs,
                  std::vector<uint8_t>& text, std::vector<uint64_t>& off, std::vector<uint32_t>& pbits);
+// CPUs this process may run on: the affinity mask, capped by the cgroup v2 CPU quota (cpu.max) --
+// what Rust's available_parallelism (rayon's default pool size) reports on Linux; >= 1
+unsigned usable_cpus();
 }  // namespace ctok_host

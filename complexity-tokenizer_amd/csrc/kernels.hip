@@ -342,9 +342,10 @@ __device__ __forceinline__ uint32_t select_bit(uint64_t x, uint32_t k) {
 // profiles/r03/v30_ab_seg_waves_per_eu.txt)
 __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(7))) void k_segment(Work w, Tables t) {
   __shared__ uint16_t s_pos_all[kSegWaves][64 * kSegUnroll + 8];  // one round's piece starts
-  // the 4 bytes before the context word, the context word, the tile, the look-ahead word, the 4
-  // bytes after it
-  __shared__ uint32_t s_text_all[kSegWaves][(kTileWords + 2) * 16 + 5];
+  // per wave: 3 spare words, the 4 bytes before the context word, the context word, the tile, the
+  // look-ahead word, the 4 bytes after it, 3 spare words (rows of 1032 words: every lane's 64-byte
+  // word starts 16-byte aligned for its four 16-byte stores)
+  __shared__ __attribute__((aligned(16))) uint32_t s_text_all[kSegWaves][(kTileWords + 2) * 16 + 8];
   __shared__ uint64_t s_D_all[kSegWaves][64];  // doc starts per word (piece records carry kRecDoc)
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wid = uni(threadIdx.x >> 6);
@@ -391,7 +392,7 @@ __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(
   s_D_all[wid][lane] = D;
   // every lane's word in LDS: the tile's bytes (and the look-ahead word) for the whole-piece
   // probes (s_text: the tile's first byte), the context word too for the code point decoding below
-  uint32_t* s_all = s_text_all[wid] + 1;  // (s_all[-1]: the 4 bytes before the context word)
+  uint32_t* s_all = s_text_all[wid] + 4;  // (s_all[-1]: the 4 bytes before the context word)
   uint32_t* s_text = s_all + 16;
   // the context word's first code point can start in the word before it (its first byte is a
   // continuation byte): the 4 bytes before it
@@ -416,7 +417,6 @@ __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   if (m.NA) {  // non-ASCII code points: classes and NFC flags from the two-level tables
     constexpr int kSegCp = 4;
-    const uint32_t x0 = (uint32_t)(g * 64);
     bool nfc_bad = false;
     auto set_class = [&](int cl, uint64_t bits) {
       if (cl == 0) m.W |= bits & m.NA;
@@ -1916,7 +1916,8 @@ __device__ __forceinline__ uint32_t rank_pair(const Tables& t, const PairLds& P,
 
 template <int K, bool HOT>
 __device__ uint32_t bpe_wave_dense(const Tables& t, const PairLds& P, const int32_t* s_b2id, const uint8_t* bytes,
-                                   uint32_t n, const WaveSlice<K>& S, uint32_t* out, uint32_t* err, uint32_t* sink) {
+                                   uint32_t n, const WaveSlice<K>& S, uint32_t* out, uint32_t* err, uint32_t* sink,
+                                 uint32_t* rounds = nullptr) {
   const uint32_t lane = threadIdx.x & 63;
   lds_u32* tok = S.tok();
   lds_u32* rk = S.rk();
@@ -1956,7 +1957,9 @@ __device__ uint32_t bpe_wave_dense(const Tables& t, const PairLds& P, const int3
   }
   const uint32_t m0 = m;  // initial positions (window rounds: token spans are in these units)
   wave_sync_lds();
+  uint32_t nr = 0;  // rounds (statistics: ctok_stats.long_rounds)
   for (;;) {
+    nr++;
     uint32_t lmin = kNoRank;
 #pragma unroll 8
     for (uint32_t p = lane; p < m; p += 64) lmin = min(lmin, (uint32_t)rk[p]);
@@ -2083,6 +2086,7 @@ __device__ uint32_t bpe_wave_dense(const Tables& t, const PairLds& P, const int3
   }
 #pragma unroll 4
   for (uint32_t p = lane; p < m; p += 64) out[p] = tok[p];
+  if (rounds && lane == 0) atomicAdd(rounds, nr);
   return m;
 }
 
@@ -2114,7 +2118,8 @@ constexpr uint32_t kNoPos = 0xFFFFu;
 
 template <int K, bool HOT>
 __device__ uint32_t bpe_wave_seg(const Tables& t, const PairLds& P, const int32_t* s_b2id, const uint8_t* bytes,
-                                 uint32_t n, const SegSlice<K>& S, uint32_t* out, uint32_t* err, uint32_t* sink) {
+                                 uint32_t n, const SegSlice<K>& S, uint32_t* out, uint32_t* err, uint32_t* sink,
+                                 uint32_t* rounds = nullptr) {
   static_assert(K % 16 == 0 && K <= 64, "segment width: a multiple of 16, at most 64");
   constexpr uint32_t R = K / 4;  // registers per group
   const uint32_t lane = threadIdx.x & 63;
@@ -2190,7 +2195,9 @@ __device__ uint32_t bpe_wave_seg(const Tables& t, const PairLds& P, const int32_
   uint32_t v[K];
   uint32_t gm[4] = {kNoRank, kNoRank, kNoRank, kNoRank};
   wave_sync_lds();
+  uint32_t nr = 0;  // rounds (statistics: ctok_stats.long_rounds)
   for (;;) {
+    nr++;
     const uint32_t dw = dirty32[lane];
     if (dw) {  // (re)load the changed groups' ranks and their minima
 #pragma unroll
@@ -2564,6 +2571,7 @@ __device__ uint32_t bpe_wave_seg(const Tables& t, const PairLds& P, const int32_
       c = uni(c + __popcll(bal));
     }
   }
+  if (rounds && lane == 0) atomicAdd(rounds, nr);
   return c;
 }
 
@@ -2700,8 +2708,9 @@ __global__ __launch_bounds__(64 * NW) void k_bpe_wave(Work w, Tables t) {
     uint32_t cnt;
     uint32_t* sink = &w.counters[kCtrSink];
     uint32_t* out = w.lids + w.long_pos[li];
-    if constexpr (SEG) cnt = bpe_wave_seg<K, HOT>(t, P, s_b2id, w.text + s, n, SegSlice<K>{slice}, out, err, sink);
-    else cnt = bpe_wave_dense<K, HOT>(t, P, s_b2id, w.text + s, n, WaveSlice<K>{slice}, out, err, sink);
+    uint32_t* rounds = &w.counters[kCtrRounds];
+    if constexpr (SEG) cnt = bpe_wave_seg<K, HOT>(t, P, s_b2id, w.text + s, n, SegSlice<K>{slice}, out, err, sink, rounds);
+    else cnt = bpe_wave_dense<K, HOT>(t, P, s_b2id, w.text + s, n, WaveSlice<K>{slice}, out, err, sink, rounds);
     if (lane == 0) {
       const uint32_t tile = s / kTile;
       w.long_cnt[li] = cnt;

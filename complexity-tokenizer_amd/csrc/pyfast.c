@@ -145,6 +145,12 @@ static PyObject* fast_split(PyObject* self, PyObject* args) {
   const Py_ssize_t nc = PyList_GET_SIZE(cache);
   const uint64_t T = n > 0 ? off[n] : 0;
   if (T < 65536) return split_serial(ids, off, n, cache);  /* (small batches: no histogram to clear) */
+#ifdef Py_GIL_DISABLED
+  /* free-threaded CPython: the shared int objects' reference counts may be changed by other
+   * threads meanwhile, and Py_SET_REFCNT below is not atomic there -- one Py_NewRef per item */
+  return split_serial(ids, off, n, cache);
+#endif
+  /* (per-thread histogram counts are u32: a call holds < 2^32 ids, off[n] < 3.75 GiB of text) */
   if (threads < 1) threads = 1;
   if (threads > 64) threads = 64;
   if (n < (Py_ssize_t)threads) threads = 1;

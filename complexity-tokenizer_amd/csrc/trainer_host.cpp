@@ -190,7 +190,7 @@ struct ctok_trainer {
     std::vector<uint32_t> pb;
     ctok_host::pretokenize(pretok, device, utf8, off, n, text, noff, pb);
     auto is_start = [&](uint64_t g) { return (pb[g >> 5] >> (g & 31)) & 1u; };
-    const unsigned nth = n < 64 ? 1u : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const unsigned nth = n < 64 ? 1u : std::min(16u, ctok_host::usable_cpus());
     std::vector<std::unordered_map<std::string, uint32_t>> part(nth);
     auto walk = [&](unsigned w) {
       auto& m = part[w];

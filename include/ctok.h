@@ -138,6 +138,7 @@ typedef struct ctok_stats {
   uint64_t class_ids[4];    /* ids produced per length class                             */
   double ms_bpe_med;      /* k_bpe_mid<3>, main-stream instance: pieces of 33..64 bytes    */
   uint64_t workspace_bytes; /* device workspace held by the device for this tokenizer's calls */
+  uint64_t long_rounds;     /* merge rounds of the long-piece wave tiers (<= 4096 B pieces), summed over pieces */
 } ctok_stats;
 
 /* Upper bound on the ids of a batch whose docs total `n_bytes` bytes (ids <= 3*bytes + docs:

@@ -105,38 +105,52 @@ def test_c4_shards_of_four(tok, c4, rank):
     _check_shard(tok, c4, rank, 4)
 
 
-@pytest.mark.timeout(600)
-def test_bench_two_ranks_share_one_gpu(c4):
-    """`bench.py --gpus 2`: two ranks spawned by bench.py (RANK / LOCAL_RANK / WORLD_SIZE set
-    before any GPU call), gloo barrier + max-over-ranks timing + parity vote, both ranks on
-    device 0 here.  The ranks' shards are pre-built into bench.py's corpus cache from the
-    module's corpus, so the ranks load them instead of rebuilding."""
+def _bench_ranks(c4, world, extra=()):
+    """`bench.py --gpus world` with every rank on device 0 (RANK / LOCAL_RANK / WORLD_SIZE set by
+    bench.py before any GPU call; gloo barrier, max-over-ranks timing, per-rank parity vote).  The
+    ranks' shards are pre-built into bench.py's corpus cache from the module's corpus, so the ranks
+    load them instead of rebuilding."""
     text, off = c4
     cache = os.path.join(os.environ.get("TMPDIR", "/tmp"), "ctok_corpus")
     os.makedirs(cache, exist_ok=True)
     n = corpus.C4_DOCS
-    for r in range(2):
-        d0, d1 = shard_bounds(off, 2, r)
+    for r in range(world):
+        d0, d1 = shard_bounds(off, world, r)
         p = os.path.join(cache, "c4_%d_%d_%d.npz" % (n, d0, d1))
         if not os.path.exists(p):
             a, z = int(off[d0]), int(off[d1])
-            np.savez(p + ".tmp.npz", text=text[a:z], off=(off[d0:d1 + 1] - off[d0]).astype(np.uint64))
-            os.replace(p + ".tmp.npz", p)
+            np.savez(p + ".%d.tmp.npz" % os.getpid(), text=text[a:z], off=(off[d0:d1 + 1] - off[d0]).astype(np.uint64))
+            os.replace(p + ".%d.tmp.npz" % os.getpid(), p)
     env = dict(os.environ)
     env.pop("WORLD_SIZE", None)
-    proc = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2",
-                           "--warmup", "1", "--no-cpu-baseline"], cwd=ROOT, env=env, capture_output=True, text=True,
-                          timeout=540)
+    proc = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--steps", "2",
+                           "--warmup", "1", "--no-cpu-baseline"] + list(extra), cwd=ROOT, env=env, capture_output=True,
+                          text=True, timeout=540)
     sys.stderr.write(proc.stderr[-4000:])
     assert proc.returncode == 0, proc.stderr[-4000:]
     lines = [ln for ln in proc.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, proc.stdout
     out = json.loads(lines[0])
     if os.path.isdir(os.path.join(ROOT, "gpurun_out")):  # evidence for the GPU-box session log
-        with open(os.path.join(ROOT, "gpurun_out", "bench_2rank_one_gpu.json"), "w") as f:
+        with open(os.path.join(ROOT, "gpurun_out", "bench_%drank_one_gpu.json" % world), "w") as f:
             f.write(lines[0] + "\n")
-    assert out["n_gpus"] == 2
+    assert out["n_gpus"] == world
     assert out["config"]["docs_total"] == n
     assert out["parity"].startswith("bit-exact"), out["parity"]
-    assert out["value"] > 0
-    assert out["config"]["tokens_per_gpu"] in (GOLD["shards"]["0/2"]["tokens"],)
+    assert "C4 shards of %d" % world in out["parity"]
+    return out
+
+
+@pytest.mark.timeout(600)
+def test_bench_two_ranks_share_one_gpu(c4):
+    out = _bench_ranks(c4, 2)
+    assert out["value"] > 0 and out["config"]["tokens_per_gpu"] == GOLD["shards"]["0/2"]["tokens"]
+
+
+@pytest.mark.timeout(600)
+def test_bench_eight_ranks_share_one_gpu(c4):
+    """Rehearsal of the driver's 8-GPU scaling run (bench.py --gpus 8) with the 8 ranks on device 0:
+    every rank's shard of the 8-way split bit-exact against its golden digest (one vote per rank)."""
+    out = _bench_ranks(c4, 8, ["--no-user-facing"])
+    assert out["config"]["parallelism"] == "doc-sharded x8, no collectives"
+    assert out["value"] > 0 and out["config"]["tokens_per_gpu"] == GOLD["shards"]["0/8"]["tokens"]

@@ -233,10 +233,23 @@ def test_window_rounds_non_monotone(seed):
             docs.append(b"x " + "".join(rng.choice(chars, size=max(1, n // len(chars[0].encode())))).encode() + b" y")
     rng.shuffle(docs)
     text, off = corpus.pack(docs)
+    fewer = []
     for o in objs:
         tok, rc = gpu_tok(o), ref_c.RefC(o)
-        ids, toff = tok.encode_packed(text, off)
+        ids, toff = tok.encode_packed(text, off, timing=True)
         assert_same(ids, toff, *rc.encode_packed(text, off))
+        # the window rounds ran: fewer rounds than with them switched off at load
+        rounds = tok.last_stats["long_rounds"]
+        os.environ["CTOK_NO_WINDOW"] = "1"
+        try:
+            plain = gpu_tok(o)
+        finally:
+            del os.environ["CTOK_NO_WINDOW"]
+        ids2, toff2 = plain.encode_packed(text, off, timing=True)
+        assert_same(ids2, toff2, ids, toff)
+        assert 0 < rounds <= plain.last_stats["long_rounds"], (rounds, plain.last_stats["long_rounds"])
+        fewer.append(rounds < plain.last_stats["long_rounds"])
+    assert any(fewer), "window rounds never fired"
 
 
 def test_c3_full_corpus(llama3_path):

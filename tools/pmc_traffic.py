@@ -42,7 +42,13 @@ def main():
     workload = sys.argv[4] if len(sys.argv) > 4 else None
     f = load(fetch_dir, "FETCH_SIZE")
     w = load(write_dir, "WRITE_SIZE")
+    import hashlib
+    lib = os.environ.get("CTOK_LIB") or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                     "complexity-tokenizer_amd", "complexity_tokenizer", "libctok.so")
+    with open(lib, "rb") as fh:
+        lib_sha = hashlib.sha256(fh.read()).hexdigest()
     res = {"unit": "bytes per launch", "fetch_correction": 2.0, "workload": workload,
+           "lib_sha256": lib_sha,  # the profiled library: bench.py reports `traffic` only for this build
            "note": "FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE, KiB -> bytes",
            "fetch_kib": f, "write_kib": w, "hbm_bytes_per_launch": {}}
     for k in sorted(set(f) | set(w)):

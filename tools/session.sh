@@ -84,6 +84,12 @@ for step in "$@"; do
       (cd /tmp && timeout -s KILL 240 rocprofv3 --pmc $(echo "$ctrs" | tr , ' ') --output-format csv -d "$d" -o run -- \
         python3 "$ROOT/tools/probe.py" "$cfg" "$fx" 2 > "$d.log" 2>&1) || { tail -20 "$d.log"; exit 1; }
       python3 tools/pmc_sum.py "$d" | tee "$d.txt" ;;
+    corpus:*)  # build full-size corpora into the per-box cache (outside any profiler: worker processes)
+      timeout -k 10 600 python -u -c "import sys; sys.path.insert(0, '.'); from datagen import cache; cache.build(cache.default_dir(), sys.argv[1].split(','))" \
+        "${step#corpus:}" 2>&1 | tee "$OUT/corpus.log" ;;
+    avail)  # the PMC counters of this GPU
+      (cd /tmp && timeout -k 10 120 rocprofv3 --list-avail > "$OUT/avail.txt" 2>&1) || true
+      grep -c . "$OUT/avail.txt" ;;
     probe:*)
       IFS=: read -r _ cfg fx <<< "$step"
       timeout -k 10 300 python -u tools/probe.py "$cfg" "$fx" 5 2>&1 | tee -a "$OUT/probe_${cfg}_${fx}.txt" ;;
