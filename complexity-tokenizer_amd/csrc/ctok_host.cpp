@@ -242,6 +242,7 @@ struct DeviceState {
   DevBuf<uint32_t> docbits, pbits, tile_np, tile_tok, tile_doc, tcls, list0, list1, list2, list3, tcnt, scratch, counters;
   DevBuf<uint32_t> lids, lw, long_pos, lw_pos, lwn, rend, cps;
   DevBuf<uint64_t> tregion;
+  DevBuf<uint64_t> stamps;  // diagnostic builds (CTOK_SEG_STAMPS) with CTOK_STAMPS=1
   DevBuf<uint16_t> wpref;
   DevBuf<uint32_t> long_cnt, long_ord, long_hist;
   DevBuf<uint64_t> long_list, mid_list, scan_tmp, scan_tmp2;
@@ -1690,6 +1691,12 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   w.counters = ds->counters.p;
   w.scan_tmp = (uint32_t*)ds->scan_tmp.p;
   w.scan_tmp_cap = ds->scan_tmp.cap * 2;
+  static const bool stamps_on = getenv("CTOK_STAMPS") != nullptr;
+  if (stamps_on && nt) {  // (k_segment writes them only in a -DCTOK_SEG_STAMPS build)
+    ds->stamps.ensure(nt * 8 + 8);
+    HIPTRY(hipMemsetAsync(ds->stamps.p, 0, nt * 8 * 8, s));
+    w.stamps = ds->stamps.p;
+  }
 
   // events (main stream s): 0 start | 7 segment start | 1 segment end | 2 <= 16 B merge pass end |
   //   8, 10 around the 17..32 B pass | 9 after the 33..64 B pass (main instance) | 5 side stream joined | 3 dropped-byte pass end | 6 emit end.
@@ -1765,6 +1772,24 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   HIPTRY(hipMemcpyAsync(ds->host + 1, ds->counters.p, kNumCounters * 4, hipMemcpyDeviceToHost, s));
   spin_sync(ds, s);
   uint64_t ntok = ((volatile uint64_t*)ds->host)[0];
+  if (w.stamps) {  // diagnostic: k_segment's mean cycles per phase over the tiles that stamped
+    std::vector<uint64_t> st8((size_t)w.n_tiles * 8);
+    HIPTRY(hipMemcpy(st8.data(), w.stamps, st8.size() * 8, hipMemcpyDeviceToHost));
+    double acc[6] = {0, 0, 0, 0, 0, 0}, np_sum = 0;
+    uint64_t n = 0;
+    for (size_t i = 0; i < w.n_tiles; i++) {
+      const uint64_t* r = &st8[i * 8];
+      if (!r[0] || !r[5]) continue;
+      for (int k = 0; k < 5; k++) acc[k] += (double)(r[k + 1] - r[k]);
+      acc[5] += (double)(r[5] - r[0]);
+      np_sum += (double)r[6];
+      n++;
+    }
+    if (n)
+      fprintf(stderr, "[ctok stamps] k_segment cycles per tile (mean of %llu): loads %.0f  non-ascii %.0f  starts %.0f  "
+              "routing %.0f  tail %.0f  total %.0f  pieces %.1f\n", (unsigned long long)n, acc[0] / n, acc[1] / n,
+              acc[2] / n, acc[3] / n, acc[4] / n, acc[5] / n, np_sum / n);
+  }
   uint32_t cnt[kNumCounters];
   for (int i = 0; i < kNumCounters; i++) cnt[i] = ((volatile uint32_t*)(ds->host + 1))[i];
   if (w.nfc_watch == 1 && cnt[12]) {  // a code point NFC may change: check, normalise, run again

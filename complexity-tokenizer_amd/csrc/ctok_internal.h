@@ -264,6 +264,7 @@ struct Work {              // device pointers, sized by the host for one call
   uint32_t* lw;            // global-memory long-piece state (4 u32 per byte of the pieces > 4 KiB), sized after k_long_len
   uint32_t* scan_tmp;      // scan partials
   uint64_t scan_tmp_cap;
+  uint64_t* stamps;        // diagnostic builds only (CTOK_SEG_STAMPS): 8 u64 per tile, else null
 };
 
 // ---- decode (decode.hip): ids -> UTF-8 text -------------------------------------------

@@ -340,6 +340,21 @@ __device__ __forceinline__ uint32_t select_bit(uint64_t x, uint32_t k) {
 // (amdgpu_waves_per_eu(7): at most 72 VGPRs, 7 waves per SIMD; without it the compiler takes 72-73
 // and this kernel runs at 6-7; C4 k_segment 2.78 -> 2.67 ms, 8 waves spill: 2.96 ms,
 // profiles/r03/v30_ab_seg_waves_per_eu.txt)
+// Diagnostic build only (-DCTOK_SEG_STAMPS): shader-clock stamps at k_segment's phase boundaries,
+// one row of 8 u64 per tile in Work::stamps (read by the host with CTOK_STAMPS=1); the production
+// build executes none.  Read the phases' shares, not the build's run time.
+#ifdef CTOK_SEG_STAMPS
+#define SEG_STAMP(k)                                                                              \
+  do {                                                                                            \
+    __builtin_amdgcn_sched_barrier(0);                                                            \
+    unsigned long long t_;                                                                        \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                     \
+    __builtin_amdgcn_sched_barrier(0);                                                            \
+    if (w.stamps && lane == 0) w.stamps[(size_t)tile * 8 + (k)] = t_;                            \
+  } while (0)
+#else
+#define SEG_STAMP(k) do { } while (0)
+#endif
 __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(7))) void k_segment(Work w, Tables t) {
   __shared__ uint16_t s_pos_all[kSegWaves][64 * kSegUnroll + 8];  // one round's piece starts
   // per wave: 3 spare words, the 4 bytes before the context word, the context word, the tile, the
@@ -352,6 +367,7 @@ __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(
   const uint32_t tile = uni(blockIdx.x * kSegWaves + wid);
   if (tile >= w.n_tiles) return;
   uint16_t* s_pos = s_pos_all[wid];
+  SEG_STAMP(0);
   const uint32_t B = w.n_bytes;
   const uint32_t t0 = tile * kTile;
   const int64_t g = (int64_t)tile * kTileWords - 1 + lane;  // this lane's word
@@ -415,6 +431,7 @@ __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  SEG_STAMP(1);
   if (m.NA) {  // non-ASCII code points: classes and NFC flags from the two-level tables
     constexpr int kSegCp = 4;
     bool nfc_bad = false;
@@ -508,6 +525,7 @@ __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(
       if (w.nfc_watch == 2 && g >= 0) atomicOr(&w.nfc_bits[g >> 5], 1u << (g & 31));  // (splice mode only)
     }
   }
+  SEG_STAMP(2);
   // contraction letters only where an apostrophe could use them (this word's or the previous
   // word's last two bytes)
   // (every lane takes part in each shuffle: a lane that is inactive at a ds_bpermute hands its
@@ -560,6 +578,7 @@ __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(
   const uint32_t prew = inc - c;
   uint32_t wcur = 1;  // the first word lane that can hold the next window's first piece (wave-uniform)
 
+  SEG_STAMP(3);
   // ---- C: thread per piece, kSegUnroll pieces per lane per round with their LDS lookups and
   // table probes issued together (each round is one dependent global round trip)
   const bool generic = t.n_at != 0;  // added tokens can match inside pieces: no whole-piece shortcut
@@ -704,6 +723,7 @@ __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
+  SEG_STAMP(4);
   hits = wave_sum_full_u32(hits);
   by0 = wave_sum_full_u32(by0);
   by1 = wave_sum_full_u32(by1);
@@ -723,6 +743,10 @@ __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(
     w.tcls[(size_t)lane * w.n_tiles + tile] = lane == 0 ? n0 : lane == 1 ? n1 : lane == 2 ? n2 : n3;
   if (lane == 0 && n2) w.counters[kCtrAnyMid] = 1;  // plain stores: every writer stores 1
   if (lane == 0 && n3) w.counters[kCtrAnyC3] = 1;
+  SEG_STAMP(5);
+#ifdef CTOK_SEG_STAMPS
+  if (w.stamps && lane == 0) w.stamps[(size_t)tile * 8 + 6] = np;
+#endif
 }
 
 hipError_t launch_segment(const Work& w, const Tables& t, hipStream_t s) {
@@ -1452,6 +1476,158 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
   __syncthreads();
 }
 
+#ifdef CTOK_SHORT_LG
+// A/B variant (-DCTOK_SHORT_LG): a lane group of G lanes per piece (G = 8 for
+// <= 8 B, 16 for 9..16 B pieces; 64 / G pieces per wave): lane i holds the piece's token at
+// position i (positions fixed, a live mask) and the rank of the pair it starts; a merge is the
+// group's minimum (rank << 4 | position) by DPP, the right token's lane dies, and the two new
+// pairs are looked up by the two lanes that start them (one probe each, in flight together).
+// Narrow compact tables only; semantics of src/bpe.rs:88-153 as merge_slots'.
+template <int G>
+__device__ __forceinline__ uint32_t group_min(uint32_t v) {
+  static_assert(G == 8 || G == 16, "groups of 8 or 16 lanes (within a DPP row)");
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0xB1, 0xF, 0xF, false));   // lane ^ 1
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x4E, 0xF, 0xF, false));   // lane ^ 2
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x141, 0xF, 0xF, false));  // row_half_mirror
+  if constexpr (G == 16)
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x140, 0xF, 0xF, false));  // row_mirror
+  return v;
+}
+
+template <int G, bool COMPACT, uint32_t NT, uint32_t SORTCAP, int KT, typename Load>
+__device__ __forceinline__ void lg_pass(const Work& w, const Tables& t, const PairLds& P, const int32_t* s_b2id,
+                                        PassLds<SORTCAP, KT>& S, bool& loaded, Load&& load) {
+  using LC = LdsClass<G>;
+  constexpr int K = KT;
+  constexpr uint32_t PPW = 64 / G;  // pieces per wave per block
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  const uint32_t li = lane % G, gbase = lane - li, gi = lane / G;
+  constexpr uint32_t gmask = G == 16 ? 0xFFFFu : 0xFFu;
+  uint32_t* err = &w.counters[2];
+  const uint32_t* list = class_list<G>(w);
+  const uint32_t cap = class_cap<G>(w);
+  const uint32_t* counts = w.tcls + (size_t)LC::cls * w.n_tiles;
+  uint32_t st_bytes = 0, st_ids = 0;
+  if (tid < 2) S.stat[tid] = 0;
+  __syncthreads();
+  uint32_t take = 1;
+  const uint32_t U = w.unit;
+  for (;;) {
+    if (tid == 0) {
+      S.chunk = atomicAdd(&w.counters[ctr_chunk(LC::cls)], take);
+      S.take = take;
+      S.next = 0;
+    }
+    __syncthreads();
+    const uint32_t c0 = S.chunk * U;
+    if (c0 >= w.n_tiles) break;
+    const uint32_t tb1 = min(w.n_tiles, c0 + U * S.take);
+    const uint32_t E = tile_share_init<K>(counts, tb1, c0, S.pre, S.tsum, w.tregion, LC::cls, S.tbase);
+    if (E && !loaded) {
+      load();
+      loaded = true;
+      __syncthreads();
+    }
+    for (;;) {  // blocks of PPW entries per wave (wave-uniform)
+      uint32_t b = 0;
+      if (lane == 0) b = atomicAdd(&S.next, PPW);
+      b = uni((uint32_t)__shfl((int)b, 0, 64));
+      if (b >= E) break;
+      const uint32_t q = b + gi;
+      const bool valid = q < E;
+      uint32_t kt = 0, e = 0;
+      if (valid) {
+        kt = tile_of<K>(S.pre, q);
+        e = list[(size_t)(c0 + kt) * cap + (q - S.pre[kt])];
+      }
+      const uint32_t tile = c0 + kt;
+      const uint32_t s = tile * kTile + (e & 0xFFFu);
+      const uint32_t n = valid ? ent_len(e) : 0u;
+      const uint32_t by = li < n ? (uint32_t)w.text[s + li] : 0u;
+      const uint32_t bn = dpp_next(by);  // the next position's byte (lane li + 1 of the group)
+      const int32_t id = s_b2id[by];
+      const uint64_t miss = __ballot(li < n && id < 0);
+      const bool missing = ((miss >> gbase) & gmask) != 0;
+      if (missing && li == 0) {  // a byte char absent from the vocab: the generic pass
+        const uint32_t mi = atomicAdd(&w.counters[4], 1u);
+        if (mi < w.mid_cap)
+          w.mid_list[mi] = (uint64_t)s | ((uint64_t)ent_j(e) << 32) | ((uint64_t)n << 48) | ((e & kEntDoc) ? kMidDoc : 0ull);
+        else
+          atomicOr(&w.counters[kCtrOverflow], 1u);
+      }
+      bool live = !missing && li < n;
+      uint32_t tok = (uint32_t)id & 0xFFFFu;
+      uint32_t rk = kNoRank;
+      if (live && li + 1 < n) {
+        rk = t.pair0[(by << 8) | bn];
+        if (rk != kNoRank && value_panics(t, rk)) {
+          atomicOr(err, kErrPanic);
+          rk = kNoRank;
+        }
+      }
+      for (;;) {
+        const uint32_t key = (live && rk != kNoRank) ? (rk << 4) | li : ~0u;
+        const uint32_t gmin = group_min<G>(key);
+        if (__ballot(gmin != ~0u) == 0) break;  // (wave-uniform)
+        const bool act = gmin != ~0u;
+        const uint32_t bi = gmin & 15u, r = gmin >> 4;
+        const uint32_t nid = (COMPACT ? r : t.rank_newid[r]) & 0xFFFFu;
+        const uint32_t lvm = (uint32_t)(__ballot(live) >> gbase) & gmask;
+        const uint32_t p = bi + 1 + (uint32_t)__builtin_ctz((lvm | (1u << G)) >> (bi + 1));  // the right token
+        const uint32_t qn = p + 1 + (uint32_t)__builtin_ctz((lvm | (1u << G)) >> (p + 1));  // the one after it
+        const bool has_r = qn < (uint32_t)G;
+        const uint32_t lo = lvm & ((1u << bi) - 1u);
+        const uint32_t pv = 31u - (uint32_t)__builtin_clz(lo | 1u);
+        const uint32_t tq = (uint32_t)__shfl((int)tok, (int)(gbase + min(qn, (uint32_t)G - 1)), 64);
+        const bool am_bi = act && li == bi, am_pv = act && lo != 0 && li == pv;
+        Probe<true, true> pr;
+        pr.start(t, P, am_bi ? nid : tok, am_bi ? tq : nid, (am_bi && has_r) || am_pv);
+        const uint32_t rr = pr.finish(t, err);
+        if (am_bi) {
+          tok = nid;
+          rk = has_r ? rr : kNoRank;
+        }
+        if (am_pv) rk = rr;
+        if (act && li == p) live = false;
+      }
+      // the group's ids, in position order, to the tile's region; the record
+      const uint32_t lvm = (uint32_t)(__ballot(live) >> gbase) & gmask;
+      const uint32_t m = (uint32_t)__popc(lvm);
+      uint32_t pos = 0;
+      const bool done = valid && !missing;
+      if (done && li == 0) pos = atomicAdd(&S.tsum[kt], m);
+      pos = (uint32_t)__shfl((int)pos, (int)gbase, 64);
+      if (done && live) w.scratch[(size_t)tile * kTileSlots + pos + __popc(lvm & ((1u << li) - 1u))] = tok;
+      if (done && li == 0) {
+        w.tcnt[(size_t)tile * kTileSlots + ent_j(e)] = rec_short(m, pos) | ((e & kEntDoc) ? kRecDoc : 0u);
+        st_bytes += n;
+        st_ids += m;
+      }
+    }
+    tile_share_flush<K>(w, c0, tb1, S.tsum, S.tbase, LC::cls);
+    const uint32_t units = (w.n_tiles + U - 1) / U, next = S.chunk + S.take;
+    const uint32_t share = next < units ? (units - next) / gridDim.x : 0u;
+    take = min(min((uint32_t)K / U, max(1u, share)), 64u);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    st_bytes += (uint32_t)__shfl_xor((int)st_bytes, o, 64);
+    st_ids += (uint32_t)__shfl_xor((int)st_ids, o, 64);
+  }
+  if ((tid & 63) == 0) {
+    atomicAdd(&S.stat[0], st_bytes);
+    atomicAdd(&S.stat[1], st_ids);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    atomicAdd(&w.counters[ctr_stat(LC::cls)], S.stat[0]);
+    atomicAdd(&w.counters[ctr_stat(LC::cls) + 1], S.stat[1]);
+  }
+  __syncthreads();
+}
+#endif
+
 // Pieces of <= 16 bytes (classes 0 and 1): one workgroup per CU holding the whole LDS image
 // (hot table + Bloom filter); a workgroup moves on to class 1 as soon as class 0 has no chunk
 // left, with no kernel boundary in between.  NARROW (every id < 2^16): 1024 threads, the last
@@ -1493,6 +1669,13 @@ __global__ __launch_bounds__(1024) void k_bpe_short(Work w, Tables t) {
   const PairLds P{(const lds_u64*)s_img, (const lds_u32*)(s_img + kHotBuckets)};
   lds_u32* sk = (lds_u32*)s_key;
   lds_u16* st = (lds_u16*)s_tok;
+#ifdef CTOK_SHORT_LG
+  if constexpr (NARROW) {
+    lg_pass<8, COMPACT, NT, ShortCfg<NARROW>::SORTCAP, kShortKT>(w, t, P, s_b2id, S, loaded, load);
+    lg_pass<16, COMPACT, NT, ShortCfg<NARROW>::SORTCAP, kShortKT>(w, t, P, s_b2id, S, loaded, load);
+    return;
+  }
+#endif
   class_pass<8, COMPACT, true, NT, ShortCfg<NARROW>::SORTCAP, NARROW, kShortKT>(w, t, P, s_b2id, S, loaded, load, sk, st);
   class_pass<16, COMPACT, true, NT, ShortCfg<NARROW>::SORTCAP, NARROW, kShortKT>(w, t, P, s_b2id, S, loaded, load, sk, st);
 }

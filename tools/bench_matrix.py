@@ -2,8 +2,8 @@
 """Measurement matrix of SURVEY.md section 8(d) on one MI355X (bench.py keeps the one-line
 driver contract; this tool reports everything around it).
 
-Per config (C1, C2, C3, C5 of BASELINE.json; C4 is C2's generator sharded by the driver's
-1/2/4/8-GPU bench runs):
+Per config (C1, C2, C3, C5 of BASELINE.json, C3 with the tiktoken-layout merge list (C3TT) and C5
+with NFC-active text (C5-NFC); C4 is C2's generator sharded by the driver's 1/2/4/8-GPU bench runs):
   kernel    device-resident ctok_encode_batch_device, host clock around the call (median of
             >= 10 after 3 warm-ups) and HIP-event device time
   e2e       ctok_encode_batch from host numpy buffers: pinned-staging pipeline, H2D + kernels +
@@ -16,7 +16,7 @@ Per config (C1, C2, C3, C5 of BASELINE.json; C4 is C2's generator sharded by the
   parity    sha256(tok_off, ids) of the whole config vs tests/golden/digests.json
 plus the device-to-device copy rate (a measured HBM stream peak) and the host CPU model.
 
-    python tools/bench_matrix.py [--configs c1,c2,c3,c5] [--out profiles/x.json] [--threads 16]
+    python tools/bench_matrix.py [--configs c1,c2,c3,c3tt,c5,c5nfc] [--out profiles/x.json] [--threads 16]
 """
 import argparse
 import hashlib
@@ -106,7 +106,12 @@ def run_config(name, args, torch, dev):
     os.makedirs(tmp, exist_ok=True)
     path = fixture_path(tok_name, tmp)
     t0 = time.time()
-    text, off = gen()
+    if name == "c1":
+        text, off = gen()
+    else:  # the per-box corpus cache (tools/session.sh corpus:NAME builds it ahead)
+        from datagen import cache
+        key = {"c3tt": "C3"}.get(name, name.upper())
+        text, off = cache.wait_load(cache.default_dir(), key)
     n_docs, n_bytes = len(off) - 1, int(off[-1])
     log("[matrix] %s: %d docs %.1f MB (corpus %.1fs)" % (name, n_docs, n_bytes / 1e6, time.time() - t0))
     tok = Tokenizer.from_file(path)
@@ -246,7 +251,7 @@ def run_config(name, args, torch, dev):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--configs", default="c1,c2,c3,c5")
+    ap.add_argument("--configs", default="c1,c2,c3,c3tt,c5,c5nfc")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "matrix.json"))
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=4.0)

@@ -90,6 +90,11 @@ for step in "$@"; do
     avail)  # the PMC counters of this GPU
       (cd /tmp && timeout -k 10 120 rocprofv3 --list-avail > "$OUT/avail.txt" 2>&1) || true
       grep -c . "$OUT/avail.txt" ;;
+    stamps:*)  # k_segment phase stamps (diagnostic build abl/stamps.so, -DCTOK_SEG_STAMPS): stamps:CFG:FIX
+      IFS=: read -r _ cfg fx <<< "$step"
+      CTOK_LIB=abl/stamps.so CTOK_STAMPS=1 timeout -k 10 300 python -u tools/probe.py "$cfg" "$fx" 2 \
+        > "$OUT/stamps_${cfg}.txt" 2>&1 || { tail -5 "$OUT/stamps_${cfg}.txt"; exit 1; }
+      grep -E "stamps|MB/s" "$OUT/stamps_${cfg}.txt" | tail -3 ;;
     probe:*)
       IFS=: read -r _ cfg fx <<< "$step"
       timeout -k 10 300 python -u tools/probe.py "$cfg" "$fx" 5 2>&1 | tee -a "$OUT/probe_${cfg}_${fx}.txt" ;;
