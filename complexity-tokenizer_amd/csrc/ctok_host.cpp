@@ -233,7 +233,7 @@ struct DeviceState {
   DevBuf<uint32_t> piece_tab;
   DevBuf<uint32_t> rank_newid, eager, wmeta;
   DevBuf<int32_t> byte2id;
-  DevBuf<uint8_t> cls_s1, cls_s2, nfc_s1, alnum, at_bytes, at_flags;
+  DevBuf<uint8_t> cls_s1, cls_s2, nfc_s1, alnum, at_bytes, at_flags, cls_bmp;
   DevBuf<uint16_t> nfc_s2, decomp_off;
   DevBuf<uint32_t> decomp_cp, decomp_data, comp_val, at_off, at_id;
   DevBuf<uint64_t> comp_key;
@@ -1396,6 +1396,18 @@ DeviceState* device_state(ctok* t, int device) {
   upload(ds->cls_s2, ct_cls_stage2, sizeof(ct_cls_stage2), s);
   upload(ds->nfc_s1, ct_nfc_stage1, sizeof(ct_nfc_stage1), s);
   upload(ds->nfc_s2, ct_nfc_stage2, sizeof(ct_nfc_stage2) / 2, s);
+  {  // the BMP's classes and NFC flags as one direct table: a nibble per code point
+    static const std::vector<uint8_t> bmp = [] {
+      std::vector<uint8_t> b(32768, 0);
+      for (uint32_t cp = 0; cp < 0x10000; cp++) {
+        const uint32_t cl = (ct_cls_stage2[ct_cls_stage1[cp >> 8] * 64 + ((cp & 255) >> 2)] >> ((cp & 3) * 2)) & 3;
+        const uint32_t nf = ct_nfc_stage2[ct_nfc_stage1[cp >> 8] * 256 + (cp & 255)] != 0 ? 4u : 0u;
+        b[cp >> 1] |= (uint8_t)((cl | nf) << ((cp & 1) * 4));
+      }
+      return b;
+    }();
+    upload(ds->cls_bmp, bmp.data(), bmp.size(), s);
+  }
   upload(ds->decomp_cp, ct_decomp_cp, CT_DECOMP_N, s);
   upload(ds->decomp_off, ct_decomp_off, CT_DECOMP_N + 1, s);
   upload(ds->decomp_data, ct_decomp_data, CT_DECOMP_DATA_N, s);
@@ -1427,6 +1439,7 @@ DeviceState* device_state(ctok* t, int device) {
   tb.cls_s2 = ds->cls_s2.p;
   tb.nfc_s1 = ds->nfc_s1.p;
   tb.nfc_s2 = ds->nfc_s2.p;
+  tb.cls_bmp = ds->cls_bmp.p;
   tb.cp_fast = cp_fast_ok() ? 1u : 0u;
   tb.decomp_cp = ds->decomp_cp.p;
   tb.decomp_off = ds->decomp_off.p;

@@ -180,6 +180,7 @@ struct Tables {            // device pointers, owned by the host runtime
   const uint8_t* cls_s2;
   const uint8_t* nfc_s1;
   const uint16_t* nfc_s2;
+  const uint8_t* cls_bmp;  // [32768] BMP code point c: nibble c & 1 of byte c >> 1 = class | NFC flag << 2
   uint32_t cp_fast;        // 1: the code point ranges of cp_range_class (kernels.hip) hold the class
                            // it gives and no NFC flag in these tables (checked at upload)
   const uint32_t* decomp_cp;

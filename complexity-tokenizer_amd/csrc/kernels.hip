@@ -361,7 +361,9 @@ __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(
   // look-ahead word, the 4 bytes after it, 3 spare words (rows of 1032 words: every lane's 64-byte
   // word starts 16-byte aligned for its four 16-byte stores)
   __shared__ __attribute__((aligned(16))) uint32_t s_text_all[kSegWaves][(kTileWords + 2) * 16 + 8];
-  __shared__ uint64_t s_D_all[kSegWaves][64];  // doc starts per word (piece records carry kRecDoc)
+  __shared__ uint64_t s_D_all[kSegWaves][64];
+  constexpr uint32_t kSegLongCap = 32;  // long pieces staged per tile (the list entries)
+  __shared__ uint64_t s_long_all[kSegWaves][kSegLongCap];  // doc starts per word (piece records carry kRecDoc)
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wid = uni(threadIdx.x >> 6);
   const uint32_t tile = uni(blockIdx.x * kSegWaves + wid);
@@ -492,13 +494,14 @@ __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(
               : l == 4 ? ((b0 & 0x07u) << 18) | (b1 << 12) | (b2 << 6) | b3 : b0;
       }
       int rc[kSegCp];  // range-test class, -1: look it up
-      uint32_t s1[kSegCp], n1[kSegCp];
+      uint32_t s1[kSegCp];
 #pragma unroll
       for (int k = 0; k < kSegCp; k++) {
         rc[k] = t.cp_fast ? cp_range_class(cp[k]) : -1;
         const bool in = pos[k] < 64 && cp[k] < 0x110000 && rc[k] < 0;
-        s1[k] = in ? t.cls_s1[cp[k] >> 8] : 0u;
-        n1[k] = in ? t.nfc_s1[cp[k] >> 8] : 0u;
+        // BMP code points: class and NFC flag in one load from the direct table (cls_bmp); the
+        // rare supplementary ones outside the fast ranges: two-level lookups in the branch below
+        s1[k] = in && cp[k] < 0x10000 ? (uint32_t)t.cls_bmp[cp[k] >> 1] : 0u;
       }
 #pragma unroll
       for (int k = 0; k < kSegCp; k++) {
@@ -510,9 +513,13 @@ __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(
           cl = rc[k];
         } else if (c < 0x80) {
           cl = cls_ascii(c);
+        } else if (c < 0x10000) {
+          const uint32_t v = s1[k] >> ((c & 1u) * 4);
+          cl = (int)(v & 3u);
+          nf = (v & 4u) != 0;
         } else if (c < 0x110000) {
-          cl = (t.cls_s2[s1[k] * 64 + ((c & 255) >> 2)] >> ((c & 3) * 2)) & 3;
-          nf = t.nfc_s2[n1[k] * 256 + (c & 255)] != 0;
+          cl = cls_of(c, t);
+          nf = nfc16(t, c) != 0;
         }
         nfc_bad |= nf;
         const uint32_t p = pos[k];
@@ -585,6 +592,7 @@ __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(
   uint32_t* tcnt = w.tcnt + (size_t)tile * kTileSlots;
   uint32_t hits = 0;
   uint32_t n0 = 0, n1 = 0, n2 = 0, n3 = 0;  // class-list lengths (wave-uniform)
+  uint32_t nlong = 0;  // long pieces staged in s_long_all (wave-uniform)
   uint32_t by0 = 0, by1 = 0, by2 = 0;        // this lane's bytes in class lists 0..2 (id regions)
   constexpr int U = kSegUnroll;
   constexpr uint32_t W = 64 * U;  // pieces per round
@@ -702,7 +710,17 @@ __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(
         n3 += __popcll(m3);
       }
       const uint64_t lm = __ballot(cls[u] == 3);
-      if (lm) {  // rare: one global atomic per wave
+      // long pieces staged in LDS; one global atomic for the tile's whole batch at the end (a
+      // returned atomic per round on the shared counter stalled the wave for its round trip)
+      if (lm && nlong + (uint32_t)__popcll(lm) <= kSegLongCap) {
+        if (cls[u] == 3) {
+          const uint32_t el = s_pos[64 * u + lane + 1];
+          const uint32_t ln = el == 0xFFFFu ? 0u : min(el - sl[u], 0x7FFFFu);
+          s_long_all[wid][nlong + __popcll(lm & lanemask_lt())] =
+              (uint64_t)(t0 + sl[u]) | ((uint64_t)j << 32) | ((uint64_t)ln << 44) | (doc[u] ? kLongDoc : 0ull);
+        }
+        nlong += (uint32_t)__popcll(lm);
+      } else if (lm) {  // (past kSegLongCap long pieces in the tile: one global atomic per wave)
         const uint32_t leader = __ffsll((unsigned long long)lm) - 1;
         uint32_t b = 0;
         if (lane == leader) b = atomicAdd(&w.counters[0], (uint32_t)__popcll(lm));
@@ -722,6 +740,16 @@ __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  if (nlong) {  // the tile's staged long pieces: one reservation, coalesced entry stores
+    uint32_t b = 0;
+    if (lane == 0) b = atomicAdd(&w.counters[0], nlong);
+    b = __builtin_amdgcn_readfirstlane(b);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (lane < nlong && b + lane < w.long_cap) w.long_list[b + lane] = s_long_all[wid][lane];
+    if (lane == 0 && b + nlong > w.long_cap) atomicOr(&w.counters[kCtrOverflow], 1u);
   }
   SEG_STAMP(4);
   hits = wave_sum_full_u32(hits);
@@ -2100,7 +2128,7 @@ __device__ __forceinline__ uint32_t rank_pair(const Tables& t, const PairLds& P,
 template <int K, bool HOT>
 __device__ uint32_t bpe_wave_dense(const Tables& t, const PairLds& P, const int32_t* s_b2id, const uint8_t* bytes,
                                    uint32_t n, const WaveSlice<K>& S, uint32_t* out, uint32_t* err, uint32_t* sink,
-                                 uint32_t* rounds = nullptr) {
+                                 uint32_t* rounds = nullptr /* += this piece's rounds (per-wave register) */) {
   const uint32_t lane = threadIdx.x & 63;
   lds_u32* tok = S.tok();
   lds_u32* rk = S.rk();
@@ -2269,7 +2297,7 @@ __device__ uint32_t bpe_wave_dense(const Tables& t, const PairLds& P, const int3
   }
 #pragma unroll 4
   for (uint32_t p = lane; p < m; p += 64) out[p] = tok[p];
-  if (rounds && lane == 0) atomicAdd(rounds, nr);
+  if (rounds) *rounds += nr;
   return m;
 }
 
@@ -2302,7 +2330,7 @@ constexpr uint32_t kNoPos = 0xFFFFu;
 template <int K, bool HOT>
 __device__ uint32_t bpe_wave_seg(const Tables& t, const PairLds& P, const int32_t* s_b2id, const uint8_t* bytes,
                                  uint32_t n, const SegSlice<K>& S, uint32_t* out, uint32_t* err, uint32_t* sink,
-                                 uint32_t* rounds = nullptr) {
+                                 uint32_t* rounds = nullptr /* += this piece's rounds (per-wave register) */) {
   static_assert(K % 16 == 0 && K <= 64, "segment width: a multiple of 16, at most 64");
   constexpr uint32_t R = K / 4;  // registers per group
   const uint32_t lane = threadIdx.x & 63;
@@ -2754,7 +2782,7 @@ __device__ uint32_t bpe_wave_seg(const Tables& t, const PairLds& P, const int32_
       c = uni(c + __popcll(bal));
     }
   }
-  if (rounds && lane == 0) atomicAdd(rounds, nr);
+  if (rounds) *rounds += nr;
   return c;
 }
 
@@ -2870,6 +2898,7 @@ __global__ __launch_bounds__(64 * NW) void k_bpe_wave(Work w, Tables t) {
                         : PairLds{nullptr, (const lds_u32*)s_dyn, NOB};
   lds_u32* slice = (lds_u32*)((__attribute__((address_space(3))) uint8_t*)(s_dyn + kImg) + (size_t)wid * kSlice);
   uint32_t* err = &w.counters[2];
+  uint32_t rounds = 0;  // this wave's rounds over its pieces (statistics; one atomic at the end)
   for (uint32_t step = uni(blockIdx.x * NW + wid);; step += gridDim.x * NW) {
     uint32_t li;
     if constexpr (SEG) {
@@ -2891,9 +2920,8 @@ __global__ __launch_bounds__(64 * NW) void k_bpe_wave(Work w, Tables t) {
     uint32_t cnt;
     uint32_t* sink = &w.counters[kCtrSink];
     uint32_t* out = w.lids + w.long_pos[li];
-    uint32_t* rounds = &w.counters[kCtrRounds];
-    if constexpr (SEG) cnt = bpe_wave_seg<K, HOT>(t, P, s_b2id, w.text + s, n, SegSlice<K>{slice}, out, err, sink, rounds);
-    else cnt = bpe_wave_dense<K, HOT>(t, P, s_b2id, w.text + s, n, WaveSlice<K>{slice}, out, err, sink, rounds);
+    if constexpr (SEG) cnt = bpe_wave_seg<K, HOT>(t, P, s_b2id, w.text + s, n, SegSlice<K>{slice}, out, err, sink, &rounds);
+    else cnt = bpe_wave_dense<K, HOT>(t, P, s_b2id, w.text + s, n, WaveSlice<K>{slice}, out, err, sink, &rounds);
     if (lane == 0) {
       const uint32_t tile = s / kTile;
       w.long_cnt[li] = cnt;
@@ -2901,6 +2929,7 @@ __global__ __launch_bounds__(64 * NW) void k_bpe_wave(Work w, Tables t) {
       atomicAdd(&w.tile_tok[tile], cnt);
     }
   }
+  if (lane == 0 && rounds) atomicAdd(&w.counters[kCtrRounds], rounds);
 }
 
 template <int K, uint32_t LO, int NW, bool HOT, bool SEG, bool NOB = false>
