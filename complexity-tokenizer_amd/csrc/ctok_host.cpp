@@ -240,6 +240,8 @@ struct DeviceState {
   Tables t{};
   // workspace
   DevBuf<uint32_t> docbits, pbits, tile_np, tile_tok, tile_doc, tcls, list0, list1, list2, list3, tcnt, scratch, counters;
+  DevBuf<uint16_t> prec;  // piece records (u16, or pairs of them as u32)
+  DevBuf<uint32_t> mrec, pdoc;
   DevBuf<uint32_t> lids, lw, long_pos, lw_pos, lwn, rend, cps;
   DevBuf<uint64_t> tregion;
   DevBuf<uint64_t> stamps;  // diagnostic builds (CTOK_SEG_STAMPS) with CTOK_STAMPS=1
@@ -277,7 +279,7 @@ struct DeviceState {
     uint64_t b = 0;
     auto add = [&](const auto& x) { b += (uint64_t)x.cap * sizeof(*x.p); };
     add(docbits), add(pbits), add(tile_np), add(tile_tok), add(tile_doc), add(tcls), add(list0), add(list1);
-    add(list2), add(list3), add(tcnt), add(scratch), add(counters), add(lids), add(lw), add(tregion), add(rend);
+    add(list2), add(list3), add(tcnt), add(prec), add(mrec), add(pdoc), add(scratch), add(counters), add(lids), add(lw), add(tregion), add(rend);
     add(wpref), add(long_cnt), add(long_ord), add(long_hist), add(long_pos), add(lw_pos), add(lwn), add(long_list);
     add(mid_list), add(scan_tmp), add(scan_tmp2), add(cps);
     add(doc_flag), add(ncp), add(norm_off), add(norm_text);
@@ -1673,6 +1675,12 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
     ds->list3.ensure(nt * kCap3 + 8);
   }
   ds->tcnt.ensure(nt * kTileSlots + 8);
+  // piece records: u16 when every id a whole-piece probe can return is below 0xFFFF
+  static const bool rec32_env = getenv("CTOK_REC32") != nullptr;
+  w.rec16 = (t->narrow && !rec32_env) ? 1u : 0u;
+  ds->prec.ensure(nt * kTileSlots * (w.rec16 ? 1 : 2) + 16);
+  ds->mrec.ensure(nt * kTileSlots + 8);
+  ds->pdoc.ensure(nt * (kTileSlots / 32) + 8);
   ds->scratch.ensure(nt * kTileSlots + 8);  // per tile: the class regions of the register passes
   ds->tregion.ensure(nt + 8);
   ds->long_list.ensure(w.long_cap + 8);
@@ -1696,6 +1704,9 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   w.long_ord = ds->long_ord.p;
   w.long_hist = ds->long_hist.p;
   w.tcnt = ds->tcnt.p;
+  w.prec = ds->prec.p;
+  w.mrec = ds->mrec.p;
+  w.pdoc = ds->pdoc.p;
   w.scratch = ds->scratch.p;
   w.rend = ds->rend.p;
   w.tregion = (uint2*)ds->tregion.p;

@@ -54,29 +54,29 @@ constexpr int kCtrRounds = 29;     // counters[29]: rounds of the LDS wave tiers
 constexpr int kLhBuckets = 65;
 constexpr int kLhHist = 0, kLhScan = 80, kLhFill = 160, kLhTake = 240, kLhWords = 320;
 __host__ __device__ inline uint32_t long_bucket(uint32_t n) { return n > 4096 ? 0u : 64u - (n - 1) / 64; }
-// List entry (u32): start within the tile [0,12), piece index within the tile [12,24), length [24,31)
-// (<= kMedMax = 64), kEntDoc: the piece starts a document.
-constexpr uint32_t kEntDoc = 1u << 31;
-__host__ __device__ inline uint32_t list_entry(uint32_t sl, uint32_t j, uint32_t n) { return sl | (j << 12) | (n << 24); }
+// List entry (u32): start within the tile [0,12), the piece's ordinal among the tile's merged
+// pieces [12,24) (its slot in mrec), length [24,31) (<= kMedMax = 64).
+__host__ __device__ inline uint32_t list_entry(uint32_t sl, uint32_t o, uint32_t n) { return sl | (o << 12) | (n << 24); }
 __host__ __device__ inline uint32_t ent_len(uint32_t e) { return (e >> 24) & 127u; }
-__host__ __device__ inline uint32_t ent_j(uint32_t e) { return (e >> 12) & 0xFFFu; }
-// long_list entry (u64): start byte | j << 32 | n << 44 | kLongDoc (n: the piece's length when
+__host__ __device__ inline uint32_t ent_ord(uint32_t e) { return (e >> 12) & 0xFFFu; }
+// long_list entry (u64): start byte | ordinal << 32 | n << 44 (n: the piece's length when
 // k_segment knows it -- its end lies within the tile's look-ahead --, else 0); mid_list entry:
-// start | j << 32 | kMidDoc | n << 48.
-constexpr uint64_t kLongDoc = 1ull << 63, kMidDoc = 1ull << 44;
-__host__ __device__ inline uint32_t long_j(uint64_t e) { return (uint32_t)(e >> 32) & 0xFFFu; }
+// start | ordinal << 32 | n << 48.
+__host__ __device__ inline uint32_t long_ord(uint64_t e) { return (uint32_t)(e >> 32) & 0xFFFu; }
 __host__ __device__ inline uint32_t long_len(uint64_t e) { return (uint32_t)(e >> 44) & 0x7FFFFu; }
 
-// Piece record (tcnt[tile][j], u32), written by whichever pass finishes piece j:
-//   kRecHit | id            one id, the whole-piece probe's (no scratch entry)
-//   kRecLong | li           long piece li: count long_cnt[li], ids at lids[long_pos[li] ..]
-//   count | pos << 16       merged piece (<= 64 B: register passes, generic pass): ids at
+// Piece records.  k_segment writes one per piece into prec[tile][j]: the whole-piece probe's id,
+// or kRecMerged (all ones) when a later pass produces the piece's ids -- u16 when every id the
+// tokenizer emits is below 0xFFFF (Work::rec16), else u32 -- and the piece's doc-start bit into
+// pdoc.  The merged pieces of a tile are numbered in piece order (their ordinal, carried by the
+// list entries); the pass that finishes the tile's k-th merged piece writes mrec[tile][k] (u32):
+//   count | pos << 16       <= 64 B (register passes, generic pass): ids at
 //                           scratch[tile * kTileSlots + pos ..] (pos: a slot of the tile's region
 //                           for the piece's length class, see tregion)
-// | kRecDoc when the piece starts a document: k_emit then leaves the piece's first id within the
-// tile in its slot (for k_tokoff).
-constexpr uint32_t kRecHit = 0x80000000u, kRecLong = 0x40000000u, kRecDoc = 0x20000000u;
-constexpr uint32_t kRecIdMask = (1u << kIdBits) - 1u, kRecLongMask = kRecDoc - 1u;
+//   kRecLong | li           long piece li: count long_cnt[li], ids at lids[long_pos[li] ..]
+// k_emit reads prec in piece order and mrec in ordinal order: both dense.
+constexpr uint32_t kRecLong = 0x40000000u, kRecLongMask = kRecLong - 1u;
+constexpr uint32_t kRecMerged32 = 0xFFFFFFFFu, kRecMerged16 = 0xFFFFu;
 // Per-tile id regions of the register merge passes in scratch (kTileSlots u32 per tile): class c
 // (c = 0..3) starts at the total bytes of the tile's class lists < c (ids <= bytes), packed as
 // tregion[tile] = {R1 | R2 << 16, R3}.
@@ -241,8 +241,12 @@ struct Work {              // device pointers, sized by the host for one call
   uint32_t* list1;         // [n_tiles * kCap1]
   uint32_t* list2;         // [n_tiles * kCap2]
   uint32_t* list3;         // [n_tiles * kCap3]
-  uint32_t* tcnt;          // [n_tiles * kTileSlots] record of piece j (see kRecHit), then (k_emit) its
-                           // first id within the tile
+  void* prec;              // [n_tiles * kTileSlots] piece record (u16 when rec16, else u32; see kRecLong)
+  uint32_t rec16;
+  uint32_t* mrec;          // [n_tiles * kTileSlots] merged piece records by ordinal
+  uint32_t* pdoc;          // [n_tiles * kTileSlots / 32] bit j: piece j of the tile starts a document
+  uint32_t* tcnt;          // [n_tiles * kTileSlots] (k_emit, without direct tok_off or with keep_first)
+                           // piece j's first id within the tile
   uint32_t* long_cnt;      // ids of long piece li (its length in bytes until a tier has run it)
   uint32_t* long_ord;      // long-list indices in descending length buckets (k_long_order)
   uint32_t* long_hist;     // [kLhWords] bucket counts | their exclusive scan | fill cursors | per-tier take counters

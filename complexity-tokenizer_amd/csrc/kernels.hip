@@ -11,11 +11,11 @@
 // Data layout in HBM (all offsets u32: one call covers < 4 GiB of text):
 //   text[B] u8, doc_off[D+1] u64 (input) ->
 //   docbits / pbits: 1 bit per byte (doc start / piece start), 4 KiB tiles of 64 64-byte words ->
-//   per tile: wpref (pieces before each word), three class lists of pieces still to merge,
-//   tile_np, tile_tok ->
-//   scratch[B] u32: the ids of a merged piece starting at byte s at scratch[s ...] ->
-//   tcnt[tile][j] record of piece j (a whole-piece hit carries its id), tile_tok scanned to each
-//   tile's first id ->
+//   per tile: wpref (pieces before each word), class lists of pieces still to merge, prec[j]
+//   (record of piece j: a whole-piece hit's id, u16 on narrow vocabularies), pdoc, tile_np,
+//   tile_tok ->
+//   per tile: scratch (the merged pieces' ids, by length-class region), mrec[k] (count and place
+//   of the tile's k-th merged piece), tile_tok scanned to each tile's first id ->
 //   ids[T] u32 + tok_off[D+1] u64 (output).
 // No array is indexed by a global piece number, so no pass has to wait for a global piece count.
 //
@@ -363,7 +363,7 @@ __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(
   __shared__ __attribute__((aligned(16))) uint32_t s_text_all[kSegWaves][(kTileWords + 2) * 16 + 8];
   __shared__ uint64_t s_D_all[kSegWaves][64];
   constexpr uint32_t kSegLongCap = 32;  // long pieces staged per tile (the list entries)
-  __shared__ uint64_t s_long_all[kSegWaves][kSegLongCap];  // doc starts per word (piece records carry kRecDoc)
+  __shared__ uint64_t s_long_all[kSegWaves][kSegLongCap];
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wid = uni(threadIdx.x >> 6);
   const uint32_t tile = uni(blockIdx.x * kSegWaves + wid);
@@ -589,8 +589,12 @@ __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(
   // ---- C: thread per piece, kSegUnroll pieces per lane per round with their LDS lookups and
   // table probes issued together (each round is one dependent global round trip)
   const bool generic = t.n_at != 0;  // added tokens can match inside pieces: no whole-piece shortcut
-  uint32_t* tcnt = w.tcnt + (size_t)tile * kTileSlots;
+  const bool rec16 = w.rec16 != 0;
+  uint16_t* prec16 = (uint16_t*)w.prec + (size_t)tile * kTileSlots;
+  uint32_t* prec32 = (uint32_t*)w.prec + (size_t)tile * kTileSlots;
+  uint32_t* pdoc = w.pdoc + (size_t)tile * (kTileSlots / 32);
   uint32_t hits = 0;
+  uint32_t nm = 0;  // merged pieces so far (wave-uniform): the next ordinal
   uint32_t n0 = 0, n1 = 0, n2 = 0, n3 = 0;  // class-list lengths (wave-uniform)
   uint32_t nlong = 0;  // long pieces staged in s_long_all (wave-uniform)
   uint32_t by0 = 0, by1 = 0, by2 = 0;        // this lane's bytes in class lists 0..2 (id regions)
@@ -662,16 +666,23 @@ __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const uint32_t j = j0 + 64 * u + lane;
-      uint32_t rec = 0;  // placeholder, rewritten by the pass that merges the piece
+      uint32_t rec = kRecMerged32;  // a later pass produces the piece's ids (its mrec slot)
       // (written as flag arithmetic: an if / else-if chain assigning cls[u] in each arm was
       // miscompiled by this hipcc in the unrolled loop)
       if (cls[u] == 5) {
         const bool hit = hitv[u] != kNone;
-        rec = hit ? kRecHit | hitv[u] | (doc[u] ? kRecDoc : 0u) : 0u;
+        rec = hit ? hitv[u] : kRecMerged32;
         hits += hit ? 1u : 0u;
         cls[u] = hit ? 4u : 0u;
       }
-      if (j < np) tcnt[j] = rec;  // every piece's slot: whole coalesced lines
+      // every piece's record: whole coalesced lines (u16 on narrow vocabularies)
+      if (j < np) {
+        if (rec16) prec16[j] = (uint16_t)rec;
+        else prec32[j] = rec;
+      }
+      const uint64_t dm = __ballot(j < np && doc[u]);  // doc-start bits of the 64 pieces
+      if (lane == 0 && j0 + 64 * u < np)
+        *reinterpret_cast<uint2*>(pdoc + ((j0 + 64 * u) >> 5)) = make_uint2((uint32_t)dm, (uint32_t)(dm >> 32));
     }
     {  // the tile's class-0 list is full: the rest of its class-0 pieces go to the long list (one
        // uniform test per round; the per-piece fix-up only in the rare round that crosses w.k0)
@@ -690,13 +701,16 @@ __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(
     }
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      const uint32_t j = j0 + 64 * u + lane;
-      const uint32_t e = list_entry(sl[u], j, n[u]) | (doc[u] ? kEntDoc : 0u);
+      const uint64_t below = lanemask_lt();
+      // the piece's ordinal among the tile's merged pieces (inactive lanes have class 4)
+      const uint64_t mm = __ballot(cls[u] != 4);
+      const uint32_t ord = nm + (uint32_t)__popcll(mm & below);
+      nm += (uint32_t)__popcll(mm);
+      const uint32_t e = list_entry(sl[u], ord, n[u]);
       {  // the wave owns its tile's lists: running counts in scalar registers, no atomics
         const uint64_t m0 = __ballot(cls[u] == 0);
         const uint64_t m1 = __ballot(cls[u] == 1), m2 = __ballot(cls[u] == 2);
         const uint64_t m3 = __ballot(cls[u] == 6);
-        const uint64_t below = lanemask_lt();
         if (cls[u] == 0) w.list0[(size_t)tile * w.k0 + n0 + __popcll(m0 & below)] = e;
         if (cls[u] == 1) w.list1[(size_t)tile * kCap1 + n1 + __popcll(m1 & below)] = e;
         if (cls[u] == 2) w.list2[(size_t)tile * kCap2 + n2 + __popcll(m2 & below)] = e;
@@ -717,7 +731,7 @@ __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(
           const uint32_t el = s_pos[64 * u + lane + 1];
           const uint32_t ln = el == 0xFFFFu ? 0u : min(el - sl[u], 0x7FFFFu);
           s_long_all[wid][nlong + __popcll(lm & lanemask_lt())] =
-              (uint64_t)(t0 + sl[u]) | ((uint64_t)j << 32) | ((uint64_t)ln << 44) | (doc[u] ? kLongDoc : 0ull);
+              (uint64_t)(t0 + sl[u]) | ((uint64_t)ord << 32) | ((uint64_t)ln << 44);
         }
         nlong += (uint32_t)__popcll(lm);
       } else if (lm) {  // (past kSegLongCap long pieces in the tile: one global atomic per wave)
@@ -731,7 +745,7 @@ __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(
           // the length when the piece ends within the look-ahead (0: k_long_len finds its end)
           const uint32_t el = s_pos[64 * u + lane + 1];
           const uint32_t ln = el == 0xFFFFu ? 0u : min(el - sl[u], 0x7FFFFu);
-          w.long_list[li] = (uint64_t)(t0 + sl[u]) | ((uint64_t)j << 32) | ((uint64_t)ln << 44) | (doc[u] ? kLongDoc : 0ull);
+          w.long_list[li] = (uint64_t)(t0 + sl[u]) | ((uint64_t)ord << 32) | ((uint64_t)ln << 44);
         }
         if (lane == leader && b + __popcll(lm) > w.long_cap) atomicOr(&w.counters[kCtrOverflow], 1u);
       }
@@ -950,22 +964,20 @@ __global__ __launch_bounds__(MID ? 128 : 256) void k_bpe_generic(Work w, Tables 
   }
   const uint32_t stride = MID ? gridDim.x * NT : NT;
   for (uint32_t q = (MID ? blockIdx.x * NT : 0) + tid; q < E; q += stride) {
-    uint32_t s, j, n, tile, kt = 0, doc;
+    uint32_t s, o, n, tile, kt = 0;  // o: the piece's ordinal (its mrec slot)
     if (MID) {
       const uint64_t e = w.mid_list[q];
       s = (uint32_t)e;
-      j = (uint32_t)(e >> 32) & 0xFFFu;
+      o = (uint32_t)(e >> 32) & 0xFFFu;
       n = (uint32_t)(e >> 48);
-      doc = (e & kMidDoc) ? kRecDoc : 0u;
       tile = s / kTile;
     } else {
       kt = tile_of<kTilesGeneric>(s_pre, q);
       tile = t0 + kt;
       const uint32_t e = w.list0[(size_t)tile * w.k0 + (q - s_pre[kt])];
       s = tile * kTile + (e & 0xFFFu);
-      j = ent_j(e);
+      o = ent_ord(e);
       n = ent_len(e);
-      doc = (e & kEntDoc) ? kRecDoc : 0u;
     }
     const uint8_t* bytes = w.text + s;
     // ids go to the tile's region of the piece's length class, after what the merge passes used
@@ -996,7 +1008,7 @@ __global__ __launch_bounds__(MID ? 128 : 256) void k_bpe_generic(Work w, Tables 
         pos += nxt;
       }
     }
-    w.tcnt[(size_t)tile * kTileSlots + j] = rec_short(cnt, pos) | doc;
+    w.mrec[(size_t)tile * kTileSlots + o] = rec_short(cnt, pos);
     if (MID) atomicAdd(&w.tile_tok[tile], cnt);
     else atomicAdd(&s_tsum[kt], cnt);
   }
@@ -1360,10 +1372,12 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
     };
     auto start_of = [&](uint32_t e, uint32_t kt) { return (c0 + kt) * kTile + (e & 0xFFFu); };
     // one piece: list entry e of chunk tile kt, its first N bytes in wv
-    auto body = [&](uint32_t e, uint32_t kt, const uint32_t* wv) {
+    // `hook` runs before the piece's first store (the pipeline below waits there for its
+    // look-ahead loads, not behind the stores at its next step)
+    auto body = [&](uint32_t e, uint32_t kt, const uint32_t* wv, auto&& hook) {
         const uint32_t tile = c0 + kt;
         const uint32_t s = tile * kTile + (e & 0xFFFu);
-        const uint32_t j = ent_j(e);
+        const uint32_t o = ent_ord(e);
         const uint32_t n = ent_len(e);
         uint32_t tk[N], rk[N];
         bool missing = false;
@@ -1376,9 +1390,10 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
           }
         }
         if (missing) {  // a byte char absent from the vocab is dropped: generic path
+          hook();
           const uint32_t mi = atomicAdd(&w.counters[4], 1u);
           if (mi < w.mid_cap)
-            w.mid_list[mi] = (uint64_t)s | ((uint64_t)j << 32) | ((uint64_t)n << 48) | ((e & kEntDoc) ? kMidDoc : 0ull);
+            w.mid_list[mi] = (uint64_t)s | ((uint64_t)o << 32) | ((uint64_t)n << 48);
           else
             atomicOr(&w.counters[kCtrOverflow], 1u);
           return;
@@ -1411,6 +1426,7 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
         }
         // ids go to the next free slots of the tile's region for this class (dense: a wave's
         // stores fill whole lines), the record points at them
+        hook();
         uint32_t pos = 0;
         auto out_of = [&](uint32_t mm) {
           pos = atomicAdd(&S.tsum[kt], mm);
@@ -1425,7 +1441,7 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
           for (int k = 0; k < N; k++)
             if ((uint32_t)k < m) out[k] = tk[k];
         }
-        w.tcnt[(size_t)tile * kTileSlots + j] = rec_short(m, pos) | ((e & kEntDoc) ? kRecDoc : 0u);
+        w.mrec[(size_t)tile * kTileSlots + o] = rec_short(m, pos);
         st_bytes += n;
         st_ids += m;
     };
@@ -1436,15 +1452,19 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
         const uint32_t e = entry(i, kt);
         uint32_t wv[N / 4];
         load_words<N / 4>(w.text, start_of(e, kt), w.n_bytes, wv);
-        body(e, kt, wv);
+        body(e, kt, wv, [] {});
       }
     } else {
       // Each wavefront takes blocks of 64 entries from S.next (one LDS atomic per block): a wave
       // whose pieces merge quickly takes more blocks, so the chunk's waves finish together
       // instead of each owning a fixed stride of the chunk (which cost 8% (<= 8 B) .. 15%
       // (9..16 B) of the pass at the chunk barrier).  Software pipeline over a wave's blocks b0,
-      // b1, b2: the list entry is loaded two blocks ahead and the piece's text words one block
-      // ahead, so the merges of one piece hide the two dependent global loads of the next.
+      // b1, b2: the list entry is loaded two blocks ahead and the piece's text dwords one block
+      // ahead, so the merges of one piece hide the two dependent global loads of the next.  The
+      // look-ahead registers are only loaded here (aligned at their use) and are waited for
+      // inside the piece's body before its stores (`hook`): vmcnt counts loads and stores
+      // together in issue order, so a wait for them at the top of the next step would also wait
+      // for the stores.
       const uint32_t lane = tid & 63;
       auto take = [&]() -> uint32_t {
         uint32_t b = 0;
@@ -1453,28 +1473,48 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
       };
       constexpr int kPw = N / 4;
       uint32_t e0 = 0, kt0 = 0, e1 = 0, kt1 = 0;
-      uint32_t wv0[kPw];
+      uint32_t d0[kPw + 1], sh0 = 0;  // the next piece's text dwords (unaligned) and its byte shift
+#pragma unroll
+      for (int k = 0; k <= kPw; k++) d0[k] = 0;
+      const uint32_t last = (w.n_bytes - 1) & ~3u;
+      auto issue_words = [&](uint32_t s) {
+        const uint32_t a0 = s & ~3u;
+#pragma unroll
+        for (int k = 0; k <= kPw; k++) d0[k] = *reinterpret_cast<const uint32_t*>(w.text + min(a0 + 4 * k, last));
+        sh0 = s & 3u;
+      };
+      auto hook = [&]() {
+        static_assert(kPw <= 8, "hook operands");
+        if constexpr (kPw == 2) asm volatile("" ::"v"(d0[0]), "v"(d0[1]), "v"(d0[2]), "v"(e1));
+        else if constexpr (kPw == 4)
+          asm volatile("" ::"v"(d0[0]), "v"(d0[1]), "v"(d0[2]), "v"(d0[3]), "v"(d0[4]), "v"(e1));
+        else
+          asm volatile("" ::"v"(d0[0]), "v"(d0[1]), "v"(d0[2]), "v"(d0[3]), "v"(d0[4]), "v"(d0[5]), "v"(d0[6]),
+                       "v"(d0[7]), "v"(d0[8]), "v"(e1));
+      };
       uint32_t b0 = take();
       uint32_t b1 = b0 < E ? take() : E;
       if (b0 + lane < E) {
         e0 = entry(b0 + lane, kt0);
-        load_words<kPw>(w.text, start_of(e0, kt0), w.n_bytes, wv0);
+        issue_words(start_of(e0, kt0));
       }
       if (b1 + lane < E) e1 = entry(b1 + lane, kt1);
+      hook();
       while (b0 < E) {  // wave-uniform
         const uint32_t i = b0 + lane;
         const uint32_t b2 = b1 < E ? take() : E;
         const uint32_t e = e0, kt = kt0;
-        uint32_t wv[N / 4];
+        uint32_t wv[kPw];
 #pragma unroll
-        for (int k = 0; k < N / 4; k++) wv[k] = wv0[k];
+        for (int k = 0; k < kPw; k++) wv[k] = __builtin_amdgcn_alignbyte(d0[k + 1], d0[k], sh0);
         e0 = e1;
         kt0 = kt1;
-        if (b1 + lane < E) load_words<kPw>(w.text, start_of(e0, kt0), w.n_bytes, wv0);
+        if (b1 + lane < E) issue_words(start_of(e0, kt0));
         if (b2 + lane < E) e1 = entry(b2 + lane, kt1);
         b0 = b1;
         b1 = b2;
-        if (i < E) body(e, kt, wv);
+        if (i < E) body(e, kt, wv, hook);
+        else hook();
       }
     }
     tile_share_flush<K>(w, c0, tb1, S.tsum, S.tbase, LC::cls);
@@ -1579,7 +1619,7 @@ __device__ __forceinline__ void lg_pass(const Work& w, const Tables& t, const Pa
       if (missing && li == 0) {  // a byte char absent from the vocab: the generic pass
         const uint32_t mi = atomicAdd(&w.counters[4], 1u);
         if (mi < w.mid_cap)
-          w.mid_list[mi] = (uint64_t)s | ((uint64_t)ent_j(e) << 32) | ((uint64_t)n << 48) | ((e & kEntDoc) ? kMidDoc : 0ull);
+          w.mid_list[mi] = (uint64_t)s | ((uint64_t)ent_ord(e) << 32) | ((uint64_t)n << 48);
         else
           atomicOr(&w.counters[kCtrOverflow], 1u);
       }
@@ -1627,7 +1667,7 @@ __device__ __forceinline__ void lg_pass(const Work& w, const Tables& t, const Pa
       pos = (uint32_t)__shfl((int)pos, (int)gbase, 64);
       if (done && live) w.scratch[(size_t)tile * kTileSlots + pos + __popc(lvm & ((1u << li) - 1u))] = tok;
       if (done && li == 0) {
-        w.tcnt[(size_t)tile * kTileSlots + ent_j(e)] = rec_short(m, pos) | ((e & kEntDoc) ? kRecDoc : 0u);
+        w.mrec[(size_t)tile * kTileSlots + ent_ord(e)] = rec_short(m, pos);
         st_bytes += n;
         st_ids += m;
       }
@@ -2049,8 +2089,7 @@ __global__ __launch_bounds__(256) void k_bpe_long(Work w, Tables t) {
   for (uint32_t li = uni(blockIdx.x * (blockDim.x >> 6) + wid); li < n_long; li += n_waves) {
     const uint64_t e = w.long_list[li];
     const uint32_t s = uni((uint32_t)e);
-    const uint32_t j = uni(long_j(e));
-    const uint32_t doc = (e & kLongDoc) ? kRecDoc : 0u;
+    const uint32_t o = uni(long_ord(e));
     const uint32_t n = uni(piece_end(w, s) - s);
     // tiers: LDS up to kLdsPos positions, global memory beyond (only beyond the dense wave tiers
     // when those run, i.e. without added tokens)
@@ -2071,7 +2110,7 @@ __global__ __launch_bounds__(256) void k_bpe_long(Work w, Tables t) {
     if (lane == 0) {
       const uint32_t tile = s / kTile;
       w.long_cnt[li] = cnt;
-      w.tcnt[(size_t)tile * kTileSlots + j] = kRecLong | li | doc;
+      w.mrec[(size_t)tile * kTileSlots + o] = kRecLong | li;
       atomicAdd(&w.tile_tok[tile], cnt);
     }
   }
@@ -2915,8 +2954,7 @@ __global__ __launch_bounds__(64 * NW) void k_bpe_wave(Work w, Tables t) {
     if (!SEG && n > HI) continue;
     const uint64_t e = w.long_list[li];
     const uint32_t s = uni((uint32_t)e);
-    const uint32_t j = uni(long_j(e));
-    const uint32_t doc = (e & kLongDoc) ? kRecDoc : 0u;
+    const uint32_t o = uni(long_ord(e));
     uint32_t cnt;
     uint32_t* sink = &w.counters[kCtrSink];
     uint32_t* out = w.lids + w.long_pos[li];
@@ -2925,7 +2963,7 @@ __global__ __launch_bounds__(64 * NW) void k_bpe_wave(Work w, Tables t) {
     if (lane == 0) {
       const uint32_t tile = s / kTile;
       w.long_cnt[li] = cnt;
-      w.tcnt[(size_t)tile * kTileSlots + j] = kRecLong | li | doc;
+      w.mrec[(size_t)tile * kTileSlots + o] = kRecLong | li;
       atomicAdd(&w.tile_tok[tile], cnt);
     }
   }
@@ -3019,26 +3057,39 @@ hipError_t launch_bpe_long(const Work& w, const Tables& t, hipStream_t s, uint32
 
 // ------------------------------------------------------------------------------------------
 // emission.  tile_tok is scanned to each tile's first id (tile_doc to its first document); then
-// one wavefront per tile walks the
-// tile's piece records in rounds of 256 pieces: lane l takes pieces 256 r + 4 l .. + 3 (one
-// 16-byte record load; the next round's loads are issued before this round's stores), a wave
-// scan gives each piece's first id within the tile, and the lane writes the ids itself: a
-// whole-piece hit carries its id in the record, a merged piece's ids are copied from scratch.
-// Consecutive lanes write consecutive id runs, so every cache line of the output is written
-// whole within a few store instructions.  A doc-start piece (kRecDoc) leaves its first id
-// within the tile in its record slot for k_tokoff.  No LDS, no barrier: occupancy is set by
-// VGPRs alone and the record -> scratch chains of 8 waves per SIMD overlap.
+// one wavefront per tile walks the tile's piece records in rounds of 256 pieces: lane l takes
+// pieces 256 r + 4 l .. + 3 (one 8- or 16-byte prec load and their pdoc bits), a wave scan
+// numbers the round's merged pieces (their mrec slots: consecutive, so the mrec loads are dense
+// too), a second scan gives each piece's first id within the tile, and the ids are staged in LDS
+// and stored as whole lines: a whole-piece hit's id is its record, a merged piece's ids are
+// copied from scratch (or lids).  Loads run ahead: the records two rounds ahead, the merged
+// records one round ahead.  A doc-start piece writes tok_off directly when no document is empty,
+// else leaves its first id within the tile in tcnt for k_tokoff.
 
 constexpr int kEmitWaves = 4;  // tiles per k_emit workgroup
 constexpr uint32_t kEmitStage = 1024;  // ids of one round staged in LDS (4 KiB per wave)
 
-__device__ __forceinline__ uint32_t rec_count(const Work& w, uint32_t v) {
-  return (v & kRecHit) ? 1u : (v & kRecLong) ? w.long_cnt[v & kRecLongMask] : (v & 0xFFFFu);
-}
+// one lane's four piece records of a round (u16 or u32) and their doc-start bits
+template <typename RT>
+struct EmitRecs {
+  using V = typename std::conditional<sizeof(RT) == 2, uint2, uint4>::type;
+  V v;
+  uint32_t d;
+  __device__ uint32_t rec(int k) const {
+    if constexpr (sizeof(RT) == 2) {
+      const uint32_t x = k < 2 ? v.x : v.y;
+      return (k & 1) ? x >> 16 : x & 0xFFFFu;
+    } else {
+      return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w;
+    }
+  }
+};
 
+template <typename RT>
 __global__ __launch_bounds__(64 * kEmitWaves) void k_emit(Work w, uint32_t* __restrict__ ids, uint64_t ids_cap,
                                                          uint64_t* __restrict__ tok_off) {
   if (spec_failed(w)) return;
+  constexpr uint32_t kMerged = sizeof(RT) == 2 ? kRecMerged16 : kRecMerged32;
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t tile = uni(blockIdx.x * kEmitWaves + (threadIdx.x >> 6));
   if (tile >= w.n_tiles) return;
@@ -3047,64 +3098,144 @@ __global__ __launch_bounds__(64 * kEmitWaves) void k_emit(Work w, uint32_t* __re
   // no empty documents: the n-th doc-start piece of the tile starts document tile_doc[tile] + n,
   // so tok_off is written here (k_tokoff then only writes tok_off[n_docs])
   const bool direct = uni(w.counters[kCtrEmptyDocs]) == 0;
-  uint32_t drun = uni(w.tile_doc[tile]);
+  const RT* prec = (const RT*)w.prec + (size_t)tile * kTileSlots;
+  const uint32_t* mrec = w.mrec + (size_t)tile * kTileSlots;
+  const uint32_t* pdoc = w.pdoc + (size_t)tile * (kTileSlots / 32);
   uint32_t* tcnt = w.tcnt + (size_t)tile * kTileSlots;
   const uint32_t* src0 = w.scratch + (size_t)tile * kTileSlots;
+  using Recs = EmitRecs<RT>;
+  // (no arithmetic on the loaded values here: a use right after the load would wait for it)
   auto load = [&](uint32_t j0) {
-    return j0 < np ? *reinterpret_cast<const uint4*>(tcnt + j0) : make_uint4(0, 0, 0, 0);
+    Recs x;
+    if (j0 < np) {
+      x.v = *reinterpret_cast<const typename Recs::V*>(prec + j0);
+      x.d = pdoc[j0 >> 5];
+    } else {
+      x.v = {};
+      x.d = 0;
+    }
+    return x;
+  };
+  // the doc-start bits of pieces j0 .. j0 + 3 (j0 % 4 == 0: they share a word)
+  auto docs = [&](const Recs& x, uint32_t j0) {
+    const uint32_t d = (x.d >> (j0 & 31)) & 15u;
+    return j0 + 4 > np ? (j0 < np ? d & ((1u << (np - j0)) - 1u) : 0u) : d;
+  };
+  __shared__ uint32_t s_stage[kEmitWaves][kEmitStage];
+  __shared__ uint32_t s_mrec[kEmitWaves][256];
+  lds_u32* stage = (lds_u32*)s_stage[threadIdx.x >> 6];
+  lds_u32* smr = (lds_u32*)s_mrec[threadIdx.x >> 6];
+  // A round's numbering: one scan of (doc starts << 16 | merged pieces) gives this lane's first
+  // merged ordinal and first document; the round's merged records (consecutive in mrec) are
+  // loaded by the whole wave, 64 per instruction: the first 64 a round ahead of their use, more
+  // (rare on English text) when they are used.
+  uint32_t mrun = 0, dnext = uni(w.tile_doc[tile]);  // (wave-uniform)
+  struct Ahead {
+    uint32_t o, d, nm;  // this lane's first ordinal (within the round) and document; the round's merged pieces
+    uint32_t m0;        // the round's first merged ordinal (wave-uniform)
+    uint32_t q;         // mrec[m0 + lane]
+  };
+  auto number = [&](const Recs& x, uint32_t j0) {
+    Ahead a;
+    uint32_t nm = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) nm += (j0 + k < np && x.rec(k) == kMerged) ? 1u : 0u;
+    const uint32_t nd = (uint32_t)__popc(docs(x, j0));
+    const uint32_t v = nm | (nd << 16);
+    const uint32_t inc = wave_incl_scan(v);
+    const uint32_t tot = uni(lane63(inc));
+    a.o = (inc - v) & 0xFFFFu;
+    a.d = dnext + ((inc - v) >> 16);
+    a.nm = tot & 0xFFFFu;
+    dnext = uni(dnext + (tot >> 16));
+    a.m0 = mrun;
+    a.q = lane < a.nm ? mrec[mrun + lane] : 0u;
+    mrun = uni(mrun + a.nm);
+    return a;
   };
   uint32_t run = 0;  // ids of the earlier rounds (wave-uniform)
   uint32_t r_first = 0;  // the current round's first id within the tile (wave-uniform)
-  __shared__ uint32_t s_stage[kEmitWaves][kEmitStage];
-  lds_u32* stage = (lds_u32*)s_stage[threadIdx.x >> 6];
-  uint4 nx = load(4 * lane);
+  // (an empty asm reading loaded registers: the compiler waits for those loads there, not at a
+  // later use behind the round's stores)
+  auto touch = [](const Recs& x) {
+    if constexpr (sizeof(RT) == 2) asm volatile("" ::"v"(x.v.x), "v"(x.v.y), "v"(x.d));
+    else asm volatile("" ::"v"(x.v.x), "v"(x.v.y), "v"(x.v.z), "v"(x.v.w), "v"(x.d));
+  };
+  Recs cur = load(4 * lane);
+  Ahead acur = number(cur, 4 * lane);
+  Recs nx = load(256 + 4 * lane);
+  touch(nx);
+  if (acur.nm > 0) smr[lane] = acur.q;  // (the first round's; each round writes the next one's)
   for (uint32_t r0 = 0; r0 < np; r0 += 256) {
     const uint32_t j0 = r0 + 4 * lane;
-    const uint32_t rec[4] = {nx.x, nx.y, nx.z, nx.w};
-    if (r0 + 256 < np) nx = load(j0 + 256);
-    uint32_t c[4], sum = 0;
+    // this round's merged records into LDS, each lane's four from there
+    // Waits: every load of the round is issued before the first wait (the scratch ids), which
+    // then also covers the look-ahead loads; the look-ahead values are consumed before the
+    // round's stores, so the next round starts without waiting for those stores (vmcnt counts
+    // loads and stores together, in issue order).
+    if (acur.nm > 64)  // (the round's merged records past the first 64: loaded now)
+      for (uint32_t i = 64 + lane; i < acur.nm; i += 64) smr[i] = mrec[acur.m0 + i];
+    if (acur.nm > 0) wave_sync_lds();
+    uint32_t mv[4];
+    {
+      uint32_t o = acur.o;
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const bool m = j0 + k < np && cur.rec(k) == kMerged;
+        mv[k] = m ? smr[o] : 0u;
+        o += m ? 1u : 0u;
+      }
+    }
+    // the next round's numbering and merged records, the records of the round after it
+    Ahead anx{};
+    if (r0 + 256 < np) anx = number(nx, j0 + 256);
+    const Recs nx2 = load(j0 + 512);
+    // id counts and where the ids are; long pieces' from long_cnt / long_pos, in a wave-uniform
+    // branch that waits for those loads itself
+    uint32_t c[4];
+    const uint32_t* sp[4];
+    bool lng = false;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-      c[k] = j0 + k < np ? rec_count(w, rec[k]) : 0u;
-      sum += c[k];
+      const uint32_t r = cur.rec(k), v = mv[k];
+      const bool merged = j0 + k < np && r == kMerged;
+      c[k] = j0 + k >= np ? 0u : !merged ? 1u : (v & 0xFFFFu);
+      sp[k] = src0 + (merged ? (v >> 16) & 0xFFFu : 0u);
+      lng |= merged && (v & kRecLong);
     }
-    const uint32_t inc = wave_incl_scan(sum);
-    uint32_t o = run + inc - sum;
-    run = uni(run + lane63(inc));
-    uint32_t dord = 0;  // this lane's first doc-start piece's document (direct mode)
-    if (direct) {
-      uint32_t nd = 0;
+    if (__ballot(lng)) {
 #pragma unroll
-      for (int k = 0; k < 4; k++) nd += (j0 + k < np && (rec[k] & kRecDoc)) ? 1u : 0u;
-      const uint32_t dinc = wave_incl_scan(nd);
-      dord = drun + dinc - nd;
-      drun = uni(drun + lane63(dinc));
+      for (int k = 0; k < 4; k++) {
+        const uint32_t v = mv[k];
+        if (j0 + k < np && cur.rec(k) == kMerged && (v & kRecLong)) {
+          c[k] = w.long_cnt[v & kRecLongMask];
+          sp[k] = w.lids + w.long_pos[v & kRecLongMask];
+        }
+      }
+      asm volatile("" ::"v"(c[0]), "v"(c[1]), "v"(c[2]), "v"(c[3]), "v"(sp[0]), "v"(sp[1]), "v"(sp[2]), "v"(sp[3]));
     }
+    const uint32_t sum = c[0] + c[1] + c[2] + c[3];
+    const uint32_t inc = wave_incl_scan(sum);
+    const uint32_t o0 = run + inc - sum;  // this lane's first id within the tile
+    run = uni(run + lane63(inc));
     // first ids: all loads of this lane's pieces in flight together
-    // (records past np are stale: c[k] == 0 keeps them from being followed)
-    const uint32_t* sp[4];
     uint32_t v0[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-      const uint32_t r = rec[k];
-      const bool follow = c[k] != 0 && !(r & kRecHit);
-      sp[k] = !follow ? src0
-              : (r & kRecLong) ? w.lids + w.long_pos[r & kRecLongMask]
-              : src0 + ((r >> 16) & 0xFFFu);
-      v0[k] = (r & kRecHit) ? (r & kRecIdMask) : (follow ? sp[k][0] : 0u);
+      const uint32_t r = cur.rec(k);
+      v0[k] = r != kMerged ? r : (c[k] != 0 ? sp[k][0] : 0u);
     }
     // the round's ids: staged in LDS when they fit, then written out by the whole wave as 64
     // consecutive dwords per store (whole lines; the lanes' own runs are ~5 ids apart, so direct
     // stores touch a dozen partial lines each); else each lane stores its runs itself
     const uint32_t r_ids = run - r_first;
     const bool staged = r_ids <= kEmitStage;
+    if (staged) {
+      uint32_t o = o0 - r_first;
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const uint32_t r = rec[k], cj = c[k];
-      const uint64_t dst = base + o;
-      if (staged) {
-        const uint32_t so = o - r_first;
-        if (cj > 0) stage[so] = v0[k];
+      for (int k = 0; k < 4; k++) {
+        const uint32_t cj = c[k];
+        if (cj > 0) stage[o] = v0[k];
         if (cj > 1) {
           const uint32_t* spk = sp[k];
           for (uint32_t m = 1; m < cj; m += 4) {
@@ -3113,10 +3244,27 @@ __global__ __launch_bounds__(64 * kEmitWaves) void k_emit(Work w, uint32_t* __re
             for (int i = 0; i < 4; i++) x[i] = m + i < cj ? spk[m + i] : 0u;
 #pragma unroll
             for (int i = 0; i < 4; i++)
-              if (m + i < cj) stage[so + m + i] = x[i];
+              if (m + i < cj) stage[o + m + i] = x[i];
           }
         }
-      } else {
+        o += cj;
+      }
+    }
+    // the look-ahead values in place before any store: the next round's merged records to LDS
+    // (this round's were read above), the records it uses waited for here
+    if (anx.nm > 0) smr[lane] = anx.q;
+    touch(nx2);
+    if (staged) {
+      wave_sync_lds();
+      const uint64_t d0 = base + r_first;
+      for (uint32_t i = lane; i < r_ids; i += 64)
+        if (d0 + i < ids_cap) ids[d0 + i] = stage[i];
+    } else {
+      uint32_t o = o0;
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const uint32_t cj = c[k];
+        const uint64_t dst = base + o;
         if (cj > 0 && dst < ids_cap) ids[dst] = v0[k];
         if (cj > 1) {  // merged / long piece: the rest of its ids, four loads in flight at a time
           const uint32_t* spk = sp[k];
@@ -3129,22 +3277,29 @@ __global__ __launch_bounds__(64 * kEmitWaves) void k_emit(Work w, uint32_t* __re
               if (m + i < cj && dst + m + i < ids_cap) ids[dst + m + i] = x[i];  // the host reports CTOK_E_CAPACITY when short
           }
         }
+        o += cj;
       }
-      if ((r & kRecDoc) && j0 + k < np) {
-        if (direct) tok_off[dord++] = base + o;
-        else tcnt[j0 + k] = o;  // read by k_tokoff
-      }
-      if (w.keep_first && j0 + k < np) tcnt[j0 + k] = o;  // ctok_encode_offsets
-      o += cj;
     }
-    if (staged) {
-      wave_sync_lds();
-      const uint64_t d0 = base + r_first;
-      for (uint32_t i = lane; i < r_ids; i += 64)
-        if (d0 + i < ids_cap) ids[d0 + i] = stage[i];
-      wave_sync_lds();  // (the next round's staging overwrites the buffer)
+    // document starts / first ids (after the id stores: no load waits behind them)
+    {
+      const uint32_t dcur = docs(cur, j0);
+      uint32_t dord = acur.d;  // this lane's first doc-start piece's document (direct mode)
+      uint32_t o = o0;
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        if ((dcur >> k) & 1u) {
+          if (direct) tok_off[dord++] = base + o;
+          else tcnt[j0 + k] = o;  // read by k_tokoff
+        }
+        if (w.keep_first && j0 + k < np) tcnt[j0 + k] = o;  // ctok_encode_offsets
+        o += c[k];
+      }
     }
     r_first = run;
+    wave_sync_lds();  // (the next round's staging overwrites the buffer; its smr reads follow)
+    cur = nx;
+    nx = nx2;
+    acur = anx;
   }
 }
 
@@ -3179,8 +3334,11 @@ __global__ void k_tokoff(Work w, uint64_t* __restrict__ tok_off) {
 hipError_t launch_emit(const Work& w, uint32_t* ids, uint64_t ids_cap, uint64_t* tok_off, hipStream_t s) {
   HIPCHK(scan_u32(w.tile_tok, w.tile_tok, (uint64_t)w.n_tiles, nullptr, w.scan_tmp, w.scan_tmp_cap, s));
   HIPCHK(scan_u32(w.tile_doc, w.tile_doc, (uint64_t)w.n_tiles, nullptr, w.scan_tmp, w.scan_tmp_cap, s));
-  if (w.n_tiles)
-    k_emit<<<(w.n_tiles + kEmitWaves - 1) / kEmitWaves, 64 * kEmitWaves, 0, s>>>(w, ids, ids_cap, tok_off);
+  if (w.n_tiles) {
+    const uint32_t nb = (w.n_tiles + kEmitWaves - 1) / kEmitWaves;
+    if (w.rec16) k_emit<uint16_t><<<nb, 64 * kEmitWaves, 0, s>>>(w, ids, ids_cap, tok_off);
+    else k_emit<uint32_t><<<nb, 64 * kEmitWaves, 0, s>>>(w, ids, ids_cap, tok_off);
+  }
   // (grid-stride: with no empty document only tok_off[n_docs] is left to write)
   k_tokoff<<<std::min<uint32_t>((w.n_docs + 1 + 255) / 256, 4096), 256, 0, s>>>(w, tok_off);
   return hipGetLastError();

@@ -7,7 +7,7 @@
 #   matrix  tools/bench_matrix.py (every config)  probe:CFG:FIX  one probe of the working tree
 #   ptest:FILE[,FILE]  a subset of the GPU tests    pmcp:CFG:FIX:CTR,CTR  a PMC pass over probe.py (per-kernel)
 #   abenv:VAR=VAL   bench.py A/B (tools/ab.sh) without / with VAR=VAL     ablib:LIB_A:LIB_B   the same for two libraries
-#   usage: TAG=name bash tools/session.sh STEP [STEP ...]
+#   usage: TAG=name [STRICT=1] bash tools/session.sh STEP [STEP ...]   (STRICT: a failing test ends the session)
 set -e
 TAG=${TAG:-run}
 ROOT=$(pwd)
@@ -22,14 +22,16 @@ for step in "$@"; do
         > "$OUT/gpu_tests.log" 2>&1 || rc=$?
       tail -3 "$OUT/gpu_tests.log"
       if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "tests: exit $rc"; exit 1; fi
-      grep -E "^(FAILED|ERROR)" "$OUT/gpu_tests.log" || true ;;
+      grep -E "^(FAILED|ERROR)" "$OUT/gpu_tests.log" || true
+      if [ -n "$STRICT" ] && [ $rc -ne 0 ]; then echo "tests: failures (STRICT): session ends"; exit 1; fi ;;
     ptest:*)  # a subset of the GPU tests: ptest:FILE[,FILE...] (paths under tests/)
       rc=0; files=$(echo "${step#ptest:}" | tr , ' ' | sed 's|\([^ ]*\)|tests/\1|g')
       timeout -k 10 900 python -u -m pytest $files -m gpu -v --maxfail=5 --timeout 600 --timeout-method thread \
         > "$OUT/ptest.log" 2>&1 || rc=$?
       tail -3 "$OUT/ptest.log"
       if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "ptest: exit $rc"; exit 1; fi
-      grep -E "^(FAILED|ERROR)" "$OUT/ptest.log" || true ;;
+      grep -E "^(FAILED|ERROR)" "$OUT/ptest.log" || true
+      if [ -n "$STRICT" ] && [ $rc -ne 0 ]; then echo "ptest: failures (STRICT): session ends"; exit 1; fi ;;
     bench)
       timeout -k 10 500 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.log" || { tail -20 "$OUT/bench.log"; exit 1; }
       cat "$OUT/bench.json" ;;
