@@ -602,20 +602,35 @@ __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(
   constexpr uint32_t W = 64 * U;  // pieces per round
   for (uint32_t j0 = 0; j0 < np; j0 += W) {
     // expansion of this round's window [j0, j0 + W]: s_pos[j - j0] = start of piece j (the
-    // entry past the window is the next round's first piece, peeked, not consumed).  One word
-    // at a time over the whole wave: lane b writes the start at bit b of the word, its piece
-    // index from the word's prefix and the set bits below b (mbcnt) -- about ten instructions
-    // per word, against a per-lane loop over its own word's starts whose trip count is the
-    // busiest word's (~20 per round).
-    for (uint32_t wl = wcur; wl <= (uint32_t)kTileWords; wl++) {  // (wave-uniform)
-      const uint32_t pw = uni(__builtin_amdgcn_readlane(prew, wl));
-      if (pw > j0 + W) break;  // this word and the later ones start no piece of the window
-      wcur = wl;
-      const uint64_t mk = ((uint64_t)uni(__builtin_amdgcn_readlane((uint32_t)(stw >> 32), wl)) << 32) |
-                          uni(__builtin_amdgcn_readlane((uint32_t)stw, wl));
-      const uint32_t k = pw + __builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u));
-      if (((mk >> lane) & 1ull) && k >= j0 && k <= j0 + W) s_pos[k - j0] = (uint16_t)((wl - 1) * 64 + lane);
+    // entry past the window is the next round's first piece, peeked, not consumed).
+    // Half-words over the lanes: lane l takes half (l & 1) of word wb + (l >> 1), 32 words per
+    // pass (a window of 256 pieces spans ~18 words of English text: one pass), and walks its
+    // half's set bits -- a trip count of the busiest half (~10), against ten VALU per word of
+    // the round-3 word-serial walk (C4 k_segment 2.72 -> 2.66 ms, profiles/r05/v16_*).
+    for (uint32_t wb = wcur;; wb += 32) {  // (wave-uniform)
+      const uint32_t wl = wb + (lane >> 1), src = min(wl, 63u);
+      const uint32_t lo32 = (uint32_t)__shfl((int)(uint32_t)stw, (int)src, 64);
+      const uint32_t hi32 = (uint32_t)__shfl((int)(uint32_t)(stw >> 32), (int)src, 64);
+      const uint32_t pw = (uint32_t)__shfl((int)prew, (int)src, 64);
+      const bool hi = (lane & 1) != 0;
+      uint32_t bits = wl <= (uint32_t)kTileWords ? (hi ? hi32 : lo32) : 0u;
+      uint32_t k = pw + (hi ? (uint32_t)__popc(lo32) : 0u);  // piece index of the half's first start
+      if (k > j0 + W || k + (uint32_t)__popc(bits) <= j0) bits = 0;  // no piece of the window
+      const uint32_t pos0 = (wl - 1) * 64 + (hi ? 32u : 0u);
+      while (bits) {
+        const uint32_t b = (uint32_t)__builtin_ctz(bits);
+        if (k >= j0 && k <= j0 + W) s_pos[k - j0] = (uint16_t)(pos0 + b);
+        bits &= bits - 1u;
+        k++;
+      }
+      const uint32_t wn = wb + 32;  // the next pass's first word: needed when it starts a piece of the window
+      if (wn > (uint32_t)kTileWords || uni(__builtin_amdgcn_readlane(prew, wn)) > j0 + W) break;
     }
+    {  // the last word whose first piece index is within the window (the next window starts there)
+      const uint64_t inw = __ballot(lane >= wcur && lane <= (uint32_t)kTileWords && prew <= j0 + W);
+      if (inw) wcur = 63u - (uint32_t)__builtin_clzll(inw);
+    }
+
     if (lane == 0 && np <= j0 + W) s_pos[np - j0] = (uint16_t)tile_end;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
