@@ -3,6 +3,7 @@
 # failure ends the session, each under its own time limit:
 #   tests   pytest -m gpu (whole suite)          bench   bench.py default line (C4, CPU baseline)
 #   prof    rocprofv3 kernel trace of bench.py   pmc     FETCH_SIZE / WRITE_SIZE passes -> traffic
+#   pmccopy the session's traffic record to profiles/pmc_traffic.json (bench.py reads it)
 #   ab:CFG:FIX:LIB_A:LIB_B   alternating kernel-only probes (tools/probe.py) of two libraries
 #   matrix  tools/bench_matrix.py (every config)  probe:CFG:FIX  one probe of the working tree
 #   ptest:FILE[,FILE]  a subset of the GPU tests    pmcp:CFG:FIX:CTR,CTR  a PMC pass over probe.py (per-kernel)
@@ -48,6 +49,8 @@ for step in "$@"; do
         python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-parity --no-user-facing --corpus-workers 1 \
         > "$OUT/pmc_write.log" 2>&1) || { tail -20 "$OUT/pmc_write.log"; exit 1; }
       python3 "$ROOT/tools/pmc_traffic.py" "$OUT/pmc_fetch" "$OUT/pmc_write" "$OUT/pmc_traffic.json" c4/10000000 ;;
+    pmccopy)  # this session's PMC traffic as the record bench.py reads (hash-matched to libctok.so)
+      cp "$OUT/pmc_traffic.json" "$ROOT/profiles/pmc_traffic.json" && echo "pmccopy: profiles/pmc_traffic.json" ;;
     ab:*)
       IFS=: read -r _ cfg fx la lb <<< "$step"
       for i in 1 2 3; do
