@@ -1734,7 +1734,7 @@ template <bool NARROW> struct ShortCfg {
 constexpr int kShortKT = 64;
 
 template <bool COMPACT, bool NARROW>
-__global__ __launch_bounds__(1024) void k_bpe_short(Work w, Tables t) {
+__global__ __launch_bounds__(1024) void k_bpe_short(Work w, Tables t, uint32_t passes) {
   if (spec_failed(w)) return;
   constexpr uint32_t NT = ShortCfg<NARROW>::NT;
   extern __shared__ __attribute__((aligned(16))) uint4 s_img[];
@@ -1759,8 +1759,12 @@ __global__ __launch_bounds__(1024) void k_bpe_short(Work w, Tables t) {
     return;
   }
 #endif
-  class_pass<8, COMPACT, true, NT, ShortCfg<NARROW>::SORTCAP, NARROW, kShortKT>(w, t, P, s_b2id, S, loaded, load, sk, st);
-  class_pass<16, COMPACT, true, NT, ShortCfg<NARROW>::SORTCAP, NARROW, kShortKT>(w, t, P, s_b2id, S, loaded, load, sk, st);
+  // passes: bit 0 the <= 8 B class, bit 1 the 9..16 B class (both, except in the timing A/B
+  // CTOK_DBG_MODE=30, which launches them as two kernels to time them apart)
+  if (passes & 1u)
+    class_pass<8, COMPACT, true, NT, ShortCfg<NARROW>::SORTCAP, NARROW, kShortKT>(w, t, P, s_b2id, S, loaded, load, sk, st);
+  if (passes & 2u)
+    class_pass<16, COMPACT, true, NT, ShortCfg<NARROW>::SORTCAP, NARROW, kShortKT>(w, t, P, s_b2id, S, loaded, load, sk, st);
 }
 
 // Pieces of 17..32 bytes (CLS = 2, on the main stream after k_bpe_short) or 33..64 bytes (CLS = 3,
@@ -1840,7 +1844,13 @@ static hipError_t launch_short_t(const Work& w, const Tables& t, hipStream_t s) 
   static LdsAttr attr;
   HIPCHK(lds_attr_once(attr, (const void*)k_bpe_short<C, NW>, kLdsImageBytes));
   if (!w.n_tiles) return hipSuccess;
-  k_bpe_short<C, NW><<<min((w.n_tiles + w.unit - 1) / w.unit, w.n_cus), ShortCfg<NW>::NT, kLdsImageBytes, s>>>(w, t);
+  const uint32_t grid = min((w.n_tiles + w.unit - 1) / w.unit, w.n_cus);
+  if (t.dbg == 30) {
+    k_bpe_short<C, NW><<<grid, ShortCfg<NW>::NT, kLdsImageBytes, s>>>(w, t, 1u);
+    k_bpe_short<C, NW><<<grid, ShortCfg<NW>::NT, kLdsImageBytes, s>>>(w, t, 2u);
+  } else {
+    k_bpe_short<C, NW><<<grid, ShortCfg<NW>::NT, kLdsImageBytes, s>>>(w, t, 3u);
+  }
   return hipGetLastError();
 }
 template <bool C>
