@@ -3256,12 +3256,28 @@ __global__ __launch_bounds__(64 * kEmitWaves) void k_emit(Work w, uint32_t* __re
     const uint32_t r_ids = run - r_first;
     const bool staged = r_ids <= kEmitStage;
     if (staged) {
+      // first ids into the stage; a merged piece's further ids are copied by the whole wave from a
+      // list of (scratch place, count, stage place) descriptors in smr (this round's merged
+      // records were read above): one round trip for the round's copies instead of one per piece
+      // position k, and the lanes share them evenly (a long piece's ids: its own lane)
+      bool sk[4];
+      uint32_t nd = 0;
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        sk[k] = c[k] > 1 && !(mv[k] & kRecLong);
+        nd += sk[k] ? 1u : 0u;
+      }
+      const uint32_t dinc = wave_incl_scan(nd);
+      uint32_t di = dinc - nd;
+      const uint32_t n_desc = uni(lane63(dinc));
       uint32_t o = o0 - r_first;
 #pragma unroll
       for (int k = 0; k < 4; k++) {
         const uint32_t cj = c[k];
         if (cj > 0) stage[o] = v0[k];
-        if (cj > 1) {
+        if (sk[k]) {
+          smr[di++] = ((mv[k] >> 16) & 0xFFFu) | (cj << 12) | (o << 19);
+        } else if (cj > 1) {
           const uint32_t* spk = sp[k];
           for (uint32_t m = 1; m < cj; m += 4) {
             uint32_t x[4];
@@ -3273,6 +3289,22 @@ __global__ __launch_bounds__(64 * kEmitWaves) void k_emit(Work w, uint32_t* __re
           }
         }
         o += cj;
+      }
+      if (n_desc) {
+        wave_sync_lds();
+        for (uint32_t q = lane; q < n_desc; q += 64) {
+          const uint32_t d = smr[q];
+          const uint32_t* spk = src0 + (d & 0xFFFu);
+          const uint32_t cj = (d >> 12) & 0x7Fu, so = d >> 19;
+          for (uint32_t m = 1; m < cj; m += 4) {
+            uint32_t x[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) x[i] = m + i < cj ? spk[m + i] : 0u;
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+              if (m + i < cj) stage[so + m + i] = x[i];
+          }
+        }
       }
     }
     // the look-ahead values in place before any store: the next round's merged records to LDS
