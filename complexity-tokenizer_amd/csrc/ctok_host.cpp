@@ -1749,16 +1749,19 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   HIPTRY(hipEventRecord(ds->ev_cnt, ds->side));
   STEP("bpe_short", launch_bpe_class(w, tb, 0, s));
   if (timing) HIPTRY(hipEventRecord(ds->ev[2], s));
-  if (timing) HIPTRY(hipEventRecord(ds->ev[8], s));
-  STEP("bpe_mid", launch_bpe_class(w, tb, 2, s));
-  if (timing) HIPTRY(hipEventRecord(ds->ev[10], s));
-  STEP("bpe_c3", launch_bpe_class(w, tb, 4, s));
-  if (timing) HIPTRY(hipEventRecord(ds->ev[9], s));
+  // k_segment's counters (they arrive while the <= 16 B pass runs, long before it ends): the
+  // 17..32 B pass takes 768 threads per workgroup when there are no long pieces
   for (;;) {
     const hipError_t e = hipEventQuery(ds->ev_cnt);
     if (e == hipSuccess) break;
     if (e != hipErrorNotReady) throw_err(CTOK_E_DEVICE, std::string("hipEventQuery: ") + hipGetErrorString(e));
   }
+  w.mid_wide = (seg_cnt[0] == 0 && !getenv("CTOK_MID512")) ? 1u : 0u;
+  if (timing) HIPTRY(hipEventRecord(ds->ev[8], s));
+  STEP("bpe_mid", launch_bpe_class(w, tb, 2, s));
+  if (timing) HIPTRY(hipEventRecord(ds->ev[10], s));
+  STEP("bpe_c3", launch_bpe_class(w, tb, 4, s));
+  if (timing) HIPTRY(hipEventRecord(ds->ev[9], s));
   if (!(w.nfc_watch == 1 && seg_cnt[12])) {  // (a failed NFC speculation discards this pass: nothing to launch)
     const uint32_t n_long = std::min<uint32_t>((uint32_t)seg_cnt[0], w.long_cap);
     bool any_gmem = false;  // a long piece for the global-memory tier (its state words reserved)

@@ -229,6 +229,7 @@ struct Work {              // device pointers, sized by the host for one call
                            // runs again normalised), 2: they finish (the flagged docs are spliced)
   uint32_t* nfc_bits;      // nfc_watch: bit g set when 64-byte word g holds the start of a code point
                            // NFC might change (zeroed by the host; nfc_splice flags docs from it)
+  uint32_t mid_wide;       // 1: the 17..32 B pass at 768 threads per workgroup (the call has no long pieces)
   uint32_t keep_first;     // 1: k_emit leaves every piece's first id within its tile in tcnt (not
                            // only doc-start pieces'), for ctok_encode_offsets
   uint16_t* wpref;         // [n_tiles * 64] pieces of the tile before each 64-byte word

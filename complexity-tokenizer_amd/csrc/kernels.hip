@@ -1777,17 +1777,21 @@ __global__ __launch_bounds__(1024) void k_bpe_short(Work w, Tables t, uint32_t p
 // stream's passes, and a large class 3 (multilingual text) is shared by both as CUs free up.
 // Most tiles per chunk of the 17..32 B / 33..64 B passes: these classes can be sparse (C4: ~5
 // class-2 pieces per tile), where 64 tiles left most of a 512-thread workgroup idle per chunk.
+// NT: threads per workgroup.  The 17..32 B pass runs at 768 (three waves per SIMD at 168 VGPRs,
+// 152 KiB of LDS) when the call has no long pieces -- on C4 0.60 -> 0.55 ms --, else at 512: with
+// long pieces the side stream's tiers share the CUs, and 768 made C5 slower (+0.12 ms,
+// profiles/r05/v17_ab_mid768_c4_c5.txt).
 template <int CLS> struct MidCfg { static constexpr int KT = 256; };
 
-template <bool COMPACT, int CLS, bool NARROW>
-__global__ __launch_bounds__(512) void k_bpe_mid(Work w, Tables t) {
+template <bool COMPACT, int CLS, bool NARROW, uint32_t NT = 512>
+__global__ __launch_bounds__(NT) void k_bpe_mid(Work w, Tables t) {
   if (spec_failed(w)) return;
   constexpr int KT = MidCfg<CLS>::KT;
   extern __shared__ __attribute__((aligned(16))) uint4 s_img[];
   __shared__ int32_t s_b2id[256];
   __shared__ PassLds<kSortCap, KT> S;
-  __shared__ uint32_t s_key[NARROW ? 8 * 512 : 1];
-  __shared__ uint16_t s_tok[NARROW ? 8 * 512 : 1];
+  __shared__ uint32_t s_key[NARROW ? 8 * NT : 1];
+  __shared__ uint16_t s_tok[NARROW ? 8 * NT : 1];
   // (the image is loaded up front: a lazy load pushes the 64-slot pass into scratch; the kernel
   // returns at once when k_segment found no piece of its class)
   if (w.counters[CLS == 2 ? kCtrAnyMid : kCtrAnyC3] == 0) return;
@@ -1800,11 +1804,11 @@ __global__ __launch_bounds__(512) void k_bpe_mid(Work w, Tables t) {
   if (!s_left) return;
   const uint32_t tid = threadIdx.x;
   const uint4* img = NARROW ? t.lds16_image : t.lds_image;
-  for (uint32_t i = tid; i < kLdsImageBytes / 16; i += 512) s_img[i] = img[i];
-  for (uint32_t i = tid; i < 256; i += 512) s_b2id[i] = t.byte2id[i];
+  for (uint32_t i = tid; i < kLdsImageBytes / 16; i += NT) s_img[i] = img[i];
+  for (uint32_t i = tid; i < 256; i += NT) s_b2id[i] = t.byte2id[i];
   bool loaded = true;
   const PairLds P{(const lds_u64*)s_img, (const lds_u32*)(s_img + kHotBuckets)};
-  class_pass<CLS == 2 ? 32 : 64, COMPACT, true, 512, kSortCap, NARROW, KT>(w, t, P, s_b2id, S, loaded, [] {},
+  class_pass<CLS == 2 ? 32 : 64, COMPACT, true, NT, kSortCap, NARROW, KT>(w, t, P, s_b2id, S, loaded, [] {},
                                                                          (lds_u32*)s_key, (lds_u16*)s_tok);
 }
 
@@ -1831,7 +1835,16 @@ static hipError_t launch_mid_t(const Work& w, const Tables& t, hipStream_t s) {
   static LdsAttr attr;
   HIPCHK(lds_attr_once(attr, (const void*)k_bpe_mid<C, CLS, NW>, kLdsImageBytes));
   if (!w.n_tiles) return hipSuccess;
-  k_bpe_mid<C, CLS, NW><<<min((w.n_tiles + w.unit - 1) / w.unit, w.n_cus), 512, kLdsImageBytes, s>>>(w, t);
+  const uint32_t grid = min((w.n_tiles + w.unit - 1) / w.unit, w.n_cus);
+  if constexpr (CLS == 2) {
+    if (w.mid_wide) {
+      static LdsAttr attr768;
+      HIPCHK(lds_attr_once(attr768, (const void*)k_bpe_mid<C, CLS, NW, 768>, kLdsImageBytes));
+      k_bpe_mid<C, CLS, NW, 768><<<grid, 768, kLdsImageBytes, s>>>(w, t);
+      return hipGetLastError();
+    }
+  }
+  k_bpe_mid<C, CLS, NW><<<grid, 512, kLdsImageBytes, s>>>(w, t);
   return hipGetLastError();
 }
 template <bool C, int CLS>
