@@ -355,6 +355,9 @@ __device__ __forceinline__ uint32_t select_bit(uint64_t x, uint32_t k) {
 #else
 #define SEG_STAMP(k) do { } while (0)
 #endif
+// R16: u16 piece records (Work::rec16); a template parameter, not a branch on the flag: both store
+// paths in one kernel cost 18 more spilled SGPRs
+template <bool R16>
 __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(7))) void k_segment(Work w, Tables t) {
   __shared__ uint16_t s_pos_all[kSegWaves][64 * kSegUnroll + 8];  // one round's piece starts
   // per wave: 3 spare words, the 4 bytes before the context word, the context word, the tile, the
@@ -589,9 +592,8 @@ __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(
   // ---- C: thread per piece, kSegUnroll pieces per lane per round with their LDS lookups and
   // table probes issued together (each round is one dependent global round trip)
   const bool generic = t.n_at != 0;  // added tokens can match inside pieces: no whole-piece shortcut
-  const bool rec16 = w.rec16 != 0;
-  uint16_t* prec16 = (uint16_t*)w.prec + (size_t)tile * kTileSlots;
-  uint32_t* prec32 = (uint32_t*)w.prec + (size_t)tile * kTileSlots;
+  using RecT = typename std::conditional<R16, uint16_t, uint32_t>::type;
+  RecT* prec = (RecT*)w.prec + (size_t)tile * kTileSlots;
   uint32_t* pdoc = w.pdoc + (size_t)tile * (kTileSlots / 32);
   uint32_t hits = 0;
   uint32_t nm = 0;  // merged pieces so far (wave-uniform): the next ordinal
@@ -692,8 +694,7 @@ __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(
       }
       // every piece's record: whole coalesced lines (u16 on narrow vocabularies)
       if (j < np) {
-        if (rec16) prec16[j] = (uint16_t)rec;
-        else prec32[j] = rec;
+        prec[j] = (RecT)rec;
       }
       const uint64_t dm = __ballot(j < np && doc[u]);  // doc-start bits of the 64 pieces
       if (lane == 0 && j0 + 64 * u < np)
@@ -807,7 +808,9 @@ __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(
 }
 
 hipError_t launch_segment(const Work& w, const Tables& t, hipStream_t s) {
-  if (w.n_tiles) k_segment<<<(w.n_tiles + kSegWaves - 1) / kSegWaves, 64 * kSegWaves, 0, s>>>(w, t);
+  const uint32_t grid = (w.n_tiles + kSegWaves - 1) / kSegWaves;
+  if (w.n_tiles && w.rec16) k_segment<true><<<grid, 64 * kSegWaves, 0, s>>>(w, t);
+  else if (w.n_tiles) k_segment<false><<<grid, 64 * kSegWaves, 0, s>>>(w, t);
   return hipGetLastError();
 }
 
