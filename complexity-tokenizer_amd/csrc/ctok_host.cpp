@@ -1581,7 +1581,7 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   if (timing) HIPTRY(hipEventRecord(ds->ev[0], s));
 
   ds->counters.ensure(kNumCounters);
-  HIPTRY(hipMemsetAsync(ds->counters.p, 0, kNumCounters * 4, s));
+  bool ctr_zeroed = false;  // (else launch_docstart zeroes them, in the bitmap's clearing launch)
   const uint8_t* text = d_text;
   const uint64_t* off = d_off;
   uint64_t B = n_bytes;
@@ -1595,6 +1595,8 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   } else if (t->nfc && n_bytes && !speculate) {
     ds->doc_flag.ensure(n_docs + 1);
     HIPTRY(hipMemsetAsync(ds->doc_flag.p, 0, (n_docs + 1) * 4, s));
+    HIPTRY(hipMemsetAsync(ds->counters.p, 0, kNumCounters * 4, s));
+    ctr_zeroed = true;
     STEP("nfc_check", launch_nfc_check(d_text, n_bytes, d_off, (uint32_t)n_docs, tb, ds->doc_flag.p, ds->counters.p + 3, s));
     HIPTRY(hipMemcpyAsync(ds->host, ds->counters.p + 3, 4, hipMemcpyDeviceToHost, s));
     spin_sync(ds, s);
@@ -1726,7 +1728,7 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   //   8, 10 around the 17..32 B pass | 9 after the 33..64 B pass (main instance) | 5 side stream joined | 3 dropped-byte pass end | 6 emit end.
   //   The side stream runs the long-piece pass, forked after k_segment (it reads only its output)
   //   and joined before the dropped-byte pass (fed by all merge passes) and k_emit.
-  STEP("docstart", launch_docstart(w, s));
+  STEP("docstart", launch_docstart(w, s, !ctr_zeroed));
   if (timing) HIPTRY(hipEventRecord(ds->ev[7], s));
   STEP("segment", launch_segment(w, tb, s));
   if (timing) HIPTRY(hipEventRecord(ds->ev[1], s));

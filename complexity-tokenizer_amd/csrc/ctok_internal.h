@@ -347,7 +347,8 @@ hipError_t launch_pad_rows(const PadWork& w, hipStream_t s);
 
 // ---- launchers (kernels.hip) -----------------------------------------------------------
 void upload_done();
-hipError_t launch_docstart(const Work& w, hipStream_t s);
+hipError_t launch_docstart(const Work& w, hipStream_t s, bool zero_counters);  // also zeroes the counters
+hipError_t scan_tiles(const Work& w, hipStream_t s);  // tile_tok, tile_doc: exclusive scans + totals at n_tiles
 hipError_t launch_nfc_check(const uint8_t* text, uint64_t n_bytes, const uint64_t* doc_off, uint32_t n_docs,
                             const Tables& t, uint32_t* doc_flag, uint32_t* counter, hipStream_t s);
 hipError_t launch_norm(const uint8_t* text, const uint64_t* doc_off, uint32_t n_docs, const uint32_t* doc_flag,
