@@ -1639,9 +1639,7 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   w.n_cus = ds->n_cus;
   w.nfc_watch = speculate ? (splice ? 2u : 1u) : 0u;
   if (w.nfc_watch == 2) {
-    const uint64_t nw32 = (B + 2047) / 2048 + 8;
-    ds->nfc_bits.ensure(nw32);
-    HIPTRY(hipMemsetAsync(ds->nfc_bits.p, 0, nw32 * 4, s));
+    ds->nfc_bits.ensure(nfc_bits_words(B));  // (zeroed by launch_docstart)
     w.nfc_bits = ds->nfc_bits.p;
   }
   w.keep_first = keep_first ? 1u : 0u;
@@ -1794,9 +1792,8 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   if (timing) HIPTRY(hipEventRecord(ds->ev[5], s));
   STEP("bpe_dropped", launch_bpe_class(w, tb, 3, s));
   if (timing) HIPTRY(hipEventRecord(ds->ev[3], s));
-  STEP("emit", launch_emit(w, d_ids, ids_cap, d_tok_off, s));
+  STEP("emit", launch_emit(w, d_ids, ids_cap, d_tok_off, s, st != nullptr));
   if (timing) HIPTRY(hipEventRecord(ds->ev[6], s));
-  if (st && w.n_tiles) STEP("count", launch_count_pieces(w, s));
   HIPTRY(hipMemcpyAsync(ds->host, d_tok_off + n_docs, 8, hipMemcpyDeviceToHost, s));
   HIPTRY(hipMemcpyAsync(ds->host + 1, ds->counters.p, kNumCounters * 4, hipMemcpyDeviceToHost, s));
   spin_sync(ds, s);

@@ -347,15 +347,16 @@ hipError_t launch_pad_rows(const PadWork& w, hipStream_t s);
 
 // ---- launchers (kernels.hip) -----------------------------------------------------------
 void upload_done();
-hipError_t launch_docstart(const Work& w, hipStream_t s, bool zero_counters);  // also zeroes the counters
-hipError_t scan_tiles(const Work& w, hipStream_t s);  // tile_tok, tile_doc: exclusive scans + totals at n_tiles
+hipError_t launch_docstart(const Work& w, hipStream_t s, bool zero_counters);  // also zeroes the counters and nfc_bits
+uint64_t nfc_bits_words(uint64_t n_bytes);  // nfc_bits size (u32 words)
+hipError_t scan_tiles(const Work& w, hipStream_t s, bool count);  // tile_tok, tile_doc: exclusive scans + totals
+                                                                  // at n_tiles; count: pieces into counters[5]
 hipError_t launch_nfc_check(const uint8_t* text, uint64_t n_bytes, const uint64_t* doc_off, uint32_t n_docs,
                             const Tables& t, uint32_t* doc_flag, uint32_t* counter, hipStream_t s);
 hipError_t launch_norm(const uint8_t* text, const uint64_t* doc_off, uint32_t n_docs, const uint32_t* doc_flag,
                        int add_prefix, int nfc, const Tables& t, uint32_t* cp_scratch, uint32_t* ncp,
                        uint64_t* new_len_then_off, uint8_t* out_text, int phase, hipStream_t s);
 hipError_t launch_segment(const Work& w, const Tables& t, hipStream_t s);
-hipError_t launch_count_pieces(const Work& w, hipStream_t s);
 // cls 0: classes 0 and 1; 2: classes 2 and 3; 3: dropped-byte pieces (mid_list)
 hipError_t launch_bpe_class(const Work& w, const Tables& t, int cls, hipStream_t s);
 // long-piece preparation (side stream): lengths, order, id places (long_pos) and global-memory
@@ -365,7 +366,8 @@ hipError_t launch_long_prep(const Work& w, const Tables& t, hipStream_t s, uint3
 // long-piece tiers (side stream): n_long = k_segment's long-list length, any_c3 = a class-3
 // piece exists (the side instance of the 33..64 B pass); grids sized for them, nothing when empty
 hipError_t launch_bpe_long(const Work& w, const Tables& t, hipStream_t s, uint32_t n_long, bool any_c3, bool any_gmem);
-hipError_t launch_emit(const Work& w, uint32_t* ids, uint64_t ids_cap, uint64_t* tok_off, hipStream_t s);
+hipError_t launch_emit(const Work& w, uint32_t* ids, uint64_t ids_cap, uint64_t* tok_off, hipStream_t s,
+                       bool count_pieces);  // count_pieces: counters[5] = pieces (statistics)
 // exclusive scan of n u32 (n read from *n_dev when non-null, else n_max); out[n] = total
 hipError_t scan_u32(const uint32_t* in, uint32_t* out, uint64_t n_max, const uint32_t* n_dev,
                     uint32_t* tmp, uint64_t tmp_cap, hipStream_t s);

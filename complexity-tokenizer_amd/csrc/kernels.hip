@@ -242,23 +242,31 @@ __global__ __launch_bounds__(256) void k_docstart(const uint64_t* __restrict__ o
     atomicAdd(&counters[kCtrEmptyDocs], (uint32_t)__popcll(me));
 }
 
-// Zeroes the doc-start bitmap and, when asked, the call's counters in one launch (the two
-// hipMemsetAsync calls it replaces were five fill launches per C4 call, ~39 us).
-__global__ __launch_bounds__(256) void k_clear(uint32_t* __restrict__ bits, uint64_t n, uint32_t* __restrict__ counters) {
+// Zeroes the doc-start bitmap, the NFC watch bitmap (nfc_watch 2) and, when asked, the call's
+// counters in one launch (the hipMemsetAsync calls it replaces were five fill launches per C4
+// call, ~39 us).
+__device__ __forceinline__ void clear_words(uint32_t* __restrict__ p, uint64_t n) {
   const uint64_t n4 = n / 4;
-  uint4* b4 = reinterpret_cast<uint4*>(bits);  // (hipMalloc'd: 256-byte aligned)
+  uint4* p4 = reinterpret_cast<uint4*>(p);  // (hipMalloc'd: 256-byte aligned)
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (uint64_t)gridDim.x * 256)
-    b4[i] = make_uint4(0u, 0u, 0u, 0u);
-  if (blockIdx.x == 0) {
-    if (threadIdx.x < n - 4 * n4) bits[4 * n4 + threadIdx.x] = 0u;
-    if (counters && threadIdx.x < (uint32_t)kNumCounters) counters[threadIdx.x] = 0u;
-  }
+    p4[i] = make_uint4(0u, 0u, 0u, 0u);
+  if (blockIdx.x == 0 && threadIdx.x < n - 4 * n4) p[4 * n4 + threadIdx.x] = 0u;
 }
+
+__global__ __launch_bounds__(256) void k_clear(uint32_t* __restrict__ bits, uint64_t n, uint32_t* __restrict__ bits2,
+                                               uint64_t n2, uint32_t* __restrict__ counters) {
+  clear_words(bits, n);
+  if (bits2) clear_words(bits2, n2);
+  if (blockIdx.x == 0 && counters && threadIdx.x < (uint32_t)kNumCounters) counters[threadIdx.x] = 0u;
+}
+
+uint64_t nfc_bits_words(uint64_t n_bytes) { return (n_bytes + 2047) / 2048 + 8; }
 
 hipError_t launch_docstart(const Work& w, hipStream_t s, bool zero_counters) {
   const uint64_t n = (uint64_t)w.n_words + 2;
+  const bool nfc = w.nfc_watch == 2;
   k_clear<<<(unsigned)std::min<uint64_t>((n / 4 + 255) / 256 + 1, 8ull * w.n_cus), 256, 0, s>>>(
-      w.docbits, n, zero_counters ? w.counters : nullptr);
+      w.docbits, n, nfc ? w.nfc_bits : nullptr, nfc ? nfc_bits_words(w.n_bytes) : 0, zero_counters ? w.counters : nullptr);
   if (w.n_docs) k_docstart<<<(w.n_docs + 255) / 256, 256, 0, s>>>(w.doc_off, w.n_docs, w.docbits, w.counters);
   return hipGetLastError();
 }
@@ -826,20 +834,6 @@ hipError_t launch_segment(const Work& w, const Tables& t, hipStream_t s) {
   const uint32_t grid = (w.n_tiles + kSegWaves - 1) / kSegWaves;
   if (w.n_tiles && w.rec16) k_segment<true><<<grid, 64 * kSegWaves, 0, s>>>(w, t);
   else if (w.n_tiles) k_segment<false><<<grid, 64 * kSegWaves, 0, s>>>(w, t);
-  return hipGetLastError();
-}
-
-// pieces in the batch (statistics only): one workgroup sums tile_np into counters[5]
-__global__ __launch_bounds__(256) void k_count_pieces(Work w) {
-  if (spec_failed(w)) return;
-  uint32_t c = 0;
-  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < w.n_tiles; i += gridDim.x * 256) c += w.tile_np[i];
-  c = wave_sum_full_u32(c);
-  if ((threadIdx.x & 63) == 0 && c) atomicAdd(&w.counters[5], c);  // (counters are zeroed per call)
-}
-
-hipError_t launch_count_pieces(const Work& w, hipStream_t s) {
-  k_count_pieces<<<std::min<uint32_t>((w.n_tiles + 1023) / 1024, 256), 256, 0, s>>>(w);
   return hipGetLastError();
 }
 
@@ -3419,8 +3413,9 @@ __global__ void k_tokoff(Work w, uint64_t* __restrict__ tok_off) {
     tokoff_one(w, tok_off, d);
 }
 
-hipError_t launch_emit(const Work& w, uint32_t* ids, uint64_t ids_cap, uint64_t* tok_off, hipStream_t s) {
-  HIPCHK(scan_tiles(w, s));
+hipError_t launch_emit(const Work& w, uint32_t* ids, uint64_t ids_cap, uint64_t* tok_off, hipStream_t s,
+                       bool count_pieces) {
+  HIPCHK(scan_tiles(w, s, count_pieces));
   if (w.n_tiles) {
     const uint32_t nb = (w.n_tiles + kEmitWaves - 1) / kEmitWaves;
     if (w.rec16) k_emit<uint16_t><<<nb, 64 * kEmitWaves, 0, s>>>(w, ids, ids_cap, tok_off);
@@ -3522,7 +3517,8 @@ uint64_t scan_tmp_elems(uint64_t n_max) {
 // Both per-tile scans (tile_tok: the tiles' first ids, tile_doc: their first documents) as ONE
 // scan of packed u64 values tok | doc << 32: every partial sum of either array is below 2^32 (ids
 // and documents of a call are < 2^32), so the low half never carries into the high one.
-// Reduce, scan of the block partials, apply: 3 launches (1 for <= 4096 tiles) instead of 8.
+// Reduce, scan of the block partials, apply: 3 launches (1 for <= 4096 tiles) instead of 8 (and
+// the apply sums the pieces for the statistics, which took a launch of its own).
 __device__ __forceinline__ uint64_t tile_pair(const Work& w, uint64_t i) {
   return i < w.n_tiles ? (uint64_t)w.tile_tok[i] | ((uint64_t)w.tile_doc[i] << 32) : 0ull;
 }
@@ -3538,7 +3534,8 @@ __global__ __launch_bounds__(256) void k_tiles_reduce(Work w, uint64_t* __restri
   if (threadIdx.x == 0) part[blockIdx.x] = total;
 }
 
-__global__ __launch_bounds__(256) void k_tiles_apply(Work w, const uint64_t* __restrict__ part_scanned) {
+// count: also the batch's pieces (statistics only): the sum of tile_np into counters[5]
+__global__ __launch_bounds__(256) void k_tiles_apply(Work w, const uint64_t* __restrict__ part_scanned, uint32_t count) {
   __shared__ uint64_t s_scan[17];
   const uint64_t n = w.n_tiles;
   const uint64_t b0 = (uint64_t)blockIdx.x * kScanBlock + threadIdx.x * kScanPer;
@@ -3562,16 +3559,24 @@ __global__ __launch_bounds__(256) void k_tiles_apply(Work w, const uint64_t* __r
     }
     ex += v[k];
   }
+  if (count) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int k = 0; k < kScanPer; k++)
+      if (b0 + k < n) c += w.tile_np[b0 + k];
+    c = wave_sum_full_u32(c);
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(&w.counters[5], c);  // (counters are zeroed per call)
+  }
   if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {  // the totals at index n
     w.tile_tok[n] = (uint32_t)(base + total);
     w.tile_doc[n] = (uint32_t)((base + total) >> 32);
   }
 }
 
-hipError_t scan_tiles(const Work& w, hipStream_t s) {
+hipError_t scan_tiles(const Work& w, hipStream_t s, bool count) {
   const uint64_t nb = ((uint64_t)w.n_tiles + kScanBlock - 1) / kScanBlock;
   if (nb <= 1) {
-    k_tiles_apply<<<1, 256, 0, s>>>(w, nullptr);
+    k_tiles_apply<<<1, 256, 0, s>>>(w, nullptr, count ? 1u : 0u);
     return hipGetLastError();
   }
   uint64_t* part = reinterpret_cast<uint64_t*>(w.scan_tmp);
@@ -3580,7 +3585,7 @@ hipError_t scan_tiles(const Work& w, hipStream_t s) {
   k_tiles_reduce<<<(unsigned)nb, 256, 0, s>>>(w, part);
   HIPCHK(hipGetLastError());
   HIPCHK(scan_u64(part, nb, part + nb + 1, cap - nb - 1, s));
-  k_tiles_apply<<<(unsigned)nb, 256, 0, s>>>(w, part);
+  k_tiles_apply<<<(unsigned)nb, 256, 0, s>>>(w, part, count ? 1u : 0u);
   return hipGetLastError();
 }
 

@@ -71,6 +71,18 @@ def test_c2_sample_vs_c_oracle(gpt2):
     assert_same(ids, toff, *rc.encode_packed(text, off))
 
 
+@pytest.mark.parametrize("which", ["c1", "c2"])
+def test_stats_pieces(gpt2, which):
+    """last_stats["pieces"] (the tile scan's sum of k_segment's per-tile piece counts) equals the
+    C oracle's pre-tokenizer piece count; C2's first 200k docs span two scan blocks (> 4096 tiles)."""
+    _, tok, rc = gpt2
+    text, off = corpus.corpus_c1() if which == "c1" else corpus.corpus_c2(200_000)
+    ids, toff = tok.encode_packed(text, off)
+    assert_same(ids, toff, *rc.encode_packed(text, off))
+    want = sum(len(ref_c.pieces(d)) for d in corpus.unpack(text, off))
+    assert tok.last_stats["pieces"] == want
+
+
 def test_long_pieces(gpt2):
     obj, tok, rc = gpt2
     docs = edge_cases.long_docs()
