@@ -343,12 +343,12 @@ def main():
     P, T, B, D = st["pieces"], st["tokens"], st["bytes_norm"], st["docs"]
     # Per-kernel rooflines (HIP events on the encode stream, averaged over the timed steps).
     # Algorithmic bytes per launch:
-    #   k_segment:      text read (B) + doc-start bitmap read (B/8) + piece-start bitmap written (B/8)
+    #   k_segment:      text read (B) + piece-start bitmap written (B/8) + document offsets read (8 B per doc)
     #   k_bpe_short:    text bytes of the <= 16 B pieces left to merge + 4 B per id written
     #   k_bpe_mid<2>:   the same for the 17..32 B pieces (33..64 B: k_bpe_mid<3>, main + side stream)
     cb, ci = st["class_bytes"], st["class_ids"]
     kernels = {
-        "k_segment": (avg("ms_segment"), 1.25 * B),
+        "k_segment": (avg("ms_segment"), 1.125 * B + 8 * D),
         "k_bpe_short": (avg("ms_bpe_lo"), cb[0] + cb[1] + 4 * (ci[0] + ci[1])),
         "k_bpe_mid": (avg("ms_bpe_hi"), cb[2] + 4 * ci[2]),
         "k_emit": (avg("ms_emit"), 8 * T + 16 * (D + 1)),  # + tile scan, k_tokoff: ids read + written, offsets

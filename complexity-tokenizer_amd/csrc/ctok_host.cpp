@@ -239,7 +239,7 @@ struct DeviceState {
   DevBuf<uint64_t> comp_key;
   Tables t{};
   // workspace
-  DevBuf<uint32_t> docbits, pbits, tile_np, tile_tok, tile_doc, tcls, list0, list1, list2, list3, tcnt, scratch, counters;
+  DevBuf<uint32_t> tfirst, pbits, tile_np, tile_tok, tile_doc, tcls, list0, list1, list2, list3, tcnt, scratch, counters;
   DevBuf<uint16_t> prec;  // piece records (u16, or pairs of them as u32)
   DevBuf<uint32_t> mrec, pdoc;
   DevBuf<uint32_t> lids, lw, long_pos, lw_pos, lwn, rend, cps;
@@ -278,7 +278,7 @@ struct DeviceState {
   uint64_t workspace_bytes() const {
     uint64_t b = 0;
     auto add = [&](const auto& x) { b += (uint64_t)x.cap * sizeof(*x.p); };
-    add(docbits), add(pbits), add(tile_np), add(tile_tok), add(tile_doc), add(tcls), add(list0), add(list1);
+    add(tfirst), add(pbits), add(tile_np), add(tile_tok), add(tile_doc), add(tcls), add(list0), add(list1);
     add(list2), add(list3), add(tcnt), add(prec), add(mrec), add(pdoc), add(scratch), add(counters), add(lids), add(lw), add(tregion), add(rend);
     add(wpref), add(long_cnt), add(long_ord), add(long_hist), add(long_pos), add(lw_pos), add(lwn), add(long_list);
     add(mid_list), add(scan_tmp), add(scan_tmp2), add(cps);
@@ -1644,7 +1644,7 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   }
   w.keep_first = keep_first ? 1u : 0u;
   const size_t nt = w.n_tiles;
-  ds->docbits.ensure(w.n_words + 8);
+  ds->tfirst.ensure(nt + 8);
   ds->pbits.ensure(w.n_words + 8);
   ds->wpref.ensure(nt * 64 + 8);
   ds->tile_np.ensure(nt + 8);
@@ -1689,7 +1689,7 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   ds->long_hist.ensure(kLhWords);
   ds->mid_list.ensure(w.mid_cap + 8);
   ds->scan_tmp.ensure(scan_tmp_elems(std::max<uint64_t>(nt + 1, n_docs + 1)) + 64);
-  w.docbits = ds->docbits.p;
+  w.tfirst = ds->tfirst.p;
   w.pbits = ds->pbits.p;
   w.wpref = ds->wpref.p;
   w.tile_np = ds->tile_np.p;

@@ -219,7 +219,7 @@ struct Work {              // device pointers, sized by the host for one call
   uint32_t n_bytes;
   const uint64_t* doc_off; // (normalised) offsets, n_docs + 1
   uint32_t n_docs;
-  uint32_t* docbits;       // doc-start bitmap (u32 words), n_words + 8
+  uint32_t* tfirst;        // [n_tiles] each tile's first document: the first with doc_off >= its context word
   uint32_t* pbits;         // piece-start bitmap (u32 words), n_words + 8
   uint32_t n_words;
   uint32_t n_tiles;

@@ -10,7 +10,8 @@
 //
 // Data layout in HBM (all offsets u32: one call covers < 4 GiB of text):
 //   text[B] u8, doc_off[D+1] u64 (input) ->
-//   docbits / pbits: 1 bit per byte (doc start / piece start), 4 KiB tiles of 64 64-byte words ->
+//   tfirst (each tile's first document) ->
+//   pbits: 1 bit per byte (piece start), 4 KiB tiles of 64 64-byte words ->
 //   per tile: wpref (pieces before each word), class lists of pieces still to merge, prec[j]
 //   (record of piece j: a whole-piece hit's id, u16 on narrow vocabularies), pdoc, tile_np,
 //   tile_tok ->
@@ -220,31 +221,45 @@ __device__ __forceinline__ uint32_t rank_of(const Tables& t, uint32_t a, uint32_
 // ------------------------------------------------------------------------------------------
 // doc-start bitmap
 
-// (empty documents set no bit and are counted into counters[kCtrEmptyDocs], one atomic per wave)
-// Doc-start bitmap (zeroed first).  Offsets are sorted: a doc whose start word holds no other
-// doc's start (the previous doc's start and the next one's lie in other words) sets its bit with a
-// plain store, the rest with an atomic OR (no other doc can share a word stored plainly).
-__global__ __launch_bounds__(256) void k_docstart(const uint64_t* __restrict__ off, uint32_t n_docs,
-                                                  uint32_t* __restrict__ bits, uint32_t* __restrict__ counters) {
+// Each tile's first document (k_segment finds the doc starts of its 64 words from it): tfirst[t] =
+// the first doc d with doc_off[d] >= the tile's context word (t * kTile - 64), written by thread d
+// for the tiles whose context word lies in (doc_off[d - 1], doc_off[d]] -- at most 64 of them
+// (a document over ~250 KB leaves the rest at ~0 from k_clear, and k_segment searches for those);
+// and the empty documents, counted into counters[kCtrEmptyDocs] (one atomic per wave).  It
+// replaces a doc-start bitmap of n_bytes / 8 bytes, zeroed, written and read back every call.
+__global__ __launch_bounds__(256) void k_tilefirst(const uint64_t* __restrict__ off, uint32_t n_docs, uint32_t n_tiles,
+                                                   uint32_t* __restrict__ tfirst, uint32_t* __restrict__ counters) {
   const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
   bool empty = false;
-  if (d < n_docs) {
-    const uint64_t x = off[d], y = off[d + 1], p = d ? off[d - 1] : ~0ull;
-    empty = x == y;
-    if (!empty) {
-      const uint64_t wd = x >> 5;
-      if ((p >> 5) != wd && (y >> 5) != wd) bits[wd] = 1u << (x & 31);
-      else atomicOr(&bits[wd], 1u << (x & 31));
-    }
+  if (d <= n_docs && n_tiles) {
+    const uint64_t y = off[d];
+    empty = d < n_docs && y == off[d + 1];
+    // tiles t with off[d - 1] < t * kTile - 64 <= y (d = 0: every t with t * kTile - 64 <= y)
+    const uint64_t t_lo = d ? (off[d - 1] + 64) / kTile + 1 : 0ull;
+    const uint64_t t_hi = min((y + 64) / kTile, (uint64_t)n_tiles - 1);
+    for (uint64_t t = t_lo; t <= t_hi && t < t_lo + 64; t++) tfirst[t] = d;
+  } else if (d < n_docs) {
+    empty = off[d] == off[d + 1];
   }
   const uint64_t me = __ballot(empty);
   if (me && (threadIdx.x & 63) == (uint32_t)__ffsll((unsigned long long)me) - 1)
     atomicAdd(&counters[kCtrEmptyDocs], (uint32_t)__popcll(me));
 }
 
-// Zeroes the doc-start bitmap, the NFC watch bitmap (nfc_watch 2) and, when asked, the call's
-// counters in one launch (the hipMemsetAsync calls it replaces were five fill launches per C4
-// call, ~39 us).
+// The same for one tile, by bisection (k_segment: a tile whose context word lies inside a document
+// longer than k_tilefirst's 64 tiles).  Wave-uniform.
+__device__ uint32_t tile_first_search(const uint64_t* off, uint32_t n_docs, uint32_t tile) {
+  const uint64_t key = tile ? (uint64_t)tile * kTile - 64 : 0ull;
+  uint32_t lo = 0, hi = n_docs;
+  while (lo < hi) {
+    const uint32_t mid = lo + (hi - lo) / 2;
+    if (__builtin_amdgcn_readfirstlane((uint32_t)(off[mid] < key))) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// Zeroes the call's counters (when asked) and the NFC watch bitmap (nfc_watch 2) in one launch.
 __device__ __forceinline__ void clear_words(uint32_t* __restrict__ p, uint64_t n) {
   const uint64_t n4 = n / 4;
   uint4* p4 = reinterpret_cast<uint4*>(p);  // (hipMalloc'd: 256-byte aligned)
@@ -253,21 +268,24 @@ __device__ __forceinline__ void clear_words(uint32_t* __restrict__ p, uint64_t n
   if (blockIdx.x == 0 && threadIdx.x < n - 4 * n4) p[4 * n4 + threadIdx.x] = 0u;
 }
 
-__global__ __launch_bounds__(256) void k_clear(uint32_t* __restrict__ bits, uint64_t n, uint32_t* __restrict__ bits2,
-                                               uint64_t n2, uint32_t* __restrict__ counters) {
-  clear_words(bits, n);
-  if (bits2) clear_words(bits2, n2);
+__global__ __launch_bounds__(256) void k_clear(uint32_t* __restrict__ bits, uint64_t n, uint32_t* __restrict__ counters,
+                                               uint32_t* __restrict__ tfirst, uint32_t n_tiles) {
+  if (bits) clear_words(bits, n);
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n_tiles; i += gridDim.x * 256) tfirst[i] = ~0u;
   if (blockIdx.x == 0 && counters && threadIdx.x < (uint32_t)kNumCounters) counters[threadIdx.x] = 0u;
 }
 
 uint64_t nfc_bits_words(uint64_t n_bytes) { return (n_bytes + 2047) / 2048 + 8; }
 
 hipError_t launch_docstart(const Work& w, hipStream_t s, bool zero_counters) {
-  const uint64_t n = (uint64_t)w.n_words + 2;
   const bool nfc = w.nfc_watch == 2;
-  k_clear<<<(unsigned)std::min<uint64_t>((n / 4 + 255) / 256 + 1, 8ull * w.n_cus), 256, 0, s>>>(
-      w.docbits, n, nfc ? w.nfc_bits : nullptr, nfc ? nfc_bits_words(w.n_bytes) : 0, zero_counters ? w.counters : nullptr);
-  if (w.n_docs) k_docstart<<<(w.n_docs + 255) / 256, 256, 0, s>>>(w.doc_off, w.n_docs, w.docbits, w.counters);
+  const uint64_t n = nfc ? nfc_bits_words(w.n_bytes) : 0;
+  const uint64_t work = std::max<uint64_t>(n / 4, w.n_tiles);
+  k_clear<<<(unsigned)std::min<uint64_t>((work + 255) / 256 + 1, 8ull * w.n_cus), 256, 0, s>>>(
+      nfc ? w.nfc_bits : nullptr, n, zero_counters ? w.counters : nullptr, w.tfirst, w.n_tiles);
+  if (w.n_tiles) k_tilefirst<<<(w.n_docs + 1 + 255) / 256, 256, 0, s>>>(w.doc_off, w.n_docs, w.n_tiles, w.tfirst, w.counters);
+  else if (w.n_docs)  // (no text: only the empty-document count)
+    k_tilefirst<<<(w.n_docs + 255) / 256, 256, 0, s>>>(w.doc_off, w.n_docs, 0, w.tfirst, w.counters);
   return hipGetLastError();
 }
 
@@ -424,15 +442,52 @@ __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(
         for (uint32_t i = 0; i < n; i++) x[i >> 2] |= (uint32_t)w.text[x0 + i] << (8 * (i & 3));
       }
     }
-    if (x0 < 0) D = 0;
-    else if (x0 >= (int64_t)B) D = ~0ull;
-    else {
-      const uint32_t wi = (uint32_t)(x0 >> 5);
-      D = (uint64_t)w.docbits[wi] | ((uint64_t)w.docbits[wi + 1] << 32);
-      D |= ~valid;
-    }
+  }
+  // the first 64 documents from the tile's first (k_tilefirst), loaded right behind the text
+  // (their starts give the doc-start bits below; the mask work on the text runs meanwhile)
+  uint32_t dfirst = uni(w.tfirst[tile]);
+  if (dfirst == ~0u) dfirst = tile_first_search(w.doc_off, w.n_docs, tile);  // (inside a document > 250 KB)
+  uint64_t xs0 = ~0ull, ys0 = ~0ull;
+  if (dfirst + lane < w.n_docs) {
+    xs0 = w.doc_off[dfirst + lane];
+    ys0 = w.doc_off[dfirst + lane + 1];
   }
   seg::Masks m = seg::ascii_masks(x);
+  {  // doc-start bits of the 64 words [base, base + 4096): the non-empty documents starting there,
+     // from the tile's first document on (k_tilefirst), 64 at a time (C4: one round)
+    uint64_t* s_D = s_D_all[wid];
+    s_D[lane] = 0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const uint64_t base = (uint64_t)t0 - 64;  // (tile 0: -64, wrapping; the sums below wrap back)
+    const uint64_t lim = (uint64_t)t0 + 4032;  // the window's end
+    auto mark = [&](uint64_t xs, uint64_t ys) {  // (xs = ~0: no document)
+      const bool in = xs < lim;
+      if (in && xs != ys) {
+        const uint64_t r = xs - base;
+        atomicOr((unsigned long long*)&s_D[r >> 6], 1ull << (r & 63));
+      }
+      return in;
+    };
+    if (__ballot(mark(xs0, ys0)) == ~0ull) {  // every lane's doc started inside: look further (rare)
+      for (uint32_t d = dfirst + 64;; d += 64) {
+        const uint32_t i = d + lane;
+        uint64_t xs = ~0ull, ys = ~0ull;
+        if (i < w.n_docs) {
+          xs = w.doc_off[i];
+          ys = w.doc_off[i + 1];
+        }
+        if (__ballot(mark(xs, ys)) != ~0ull) break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int64_t x0 = g * 64;
+    if (x0 < 0) D = 0;
+    else if (x0 >= (int64_t)B) D = ~0ull;
+    else D = s_D[lane] | ~valid;
+  }
   s_D_all[wid][lane] = D;
   // every lane's word in LDS: the tile's bytes (and the look-ahead word) for the whole-piece
   // probes (s_text: the tile's first byte), the context word too for the code point decoding below

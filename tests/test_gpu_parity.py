@@ -83,6 +83,21 @@ def test_stats_pieces(gpt2, which):
     assert tok.last_stats["pieces"] == want
 
 
+def test_megabyte_documents(gpt2):
+    """Documents of 1.3 MB and 2.6 MB (C2 text joined) among small ones: tiles whose context word
+    lies more than 64 tiles inside a document get their first document from k_segment's own
+    search (k_tilefirst writes 64 tiles per document)."""
+    _, tok, rc = gpt2
+    text, off = corpus.corpus_c2(30_000)
+    small = corpus.unpack(text, off)
+    big1 = b" ".join(small[:10_000])
+    big2 = b"\n".join(small[10_000:30_000])
+    docs = small[:50] + [big1] + small[50:60] + [b"", big2, b""] + small[60:100]
+    t2, o2 = corpus.pack(docs)
+    ids, toff = tok.encode_packed(t2, o2)
+    assert_same(ids, toff, *rc.encode_packed(t2, o2))
+
+
 def test_long_pieces(gpt2):
     obj, tok, rc = gpt2
     docs = edge_cases.long_docs()
