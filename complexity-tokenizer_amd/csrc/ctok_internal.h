@@ -42,7 +42,7 @@ __host__ __device__ constexpr int ctr_stat(int c) { return c < 3 ? 6 + 2 * c : 1
 __host__ __device__ constexpr int ctr_chunk(int c) { return c < 3 ? 13 + c : 18; }
 constexpr int kCtrAnyMid = 19;  // counters[19] != 0: some tile has a class-2 piece
 constexpr int kCtrAnyC3 = 20;   // counters[20] != 0: some tile has a class-3 piece
-constexpr int kCtrEmptyDocs = 21;  // counters[21]: empty documents (k_docstart); 0: k_emit writes tok_off
+constexpr int kCtrEmptyDocs = 21;  // counters[21]: empty documents (k_tilefirst); 0: k_emit writes tok_off
 constexpr int kCtrSink = 31;       // counters[31]: panic bits of lookups whose pairs need not exist (discarded)
 constexpr int kCtrOverflow = 25;   // counters[25] != 0: a list outgrew its lean capacity (the host reruns the call safe)
 constexpr int kCtrLongIds = 26;    // counters[26]: long-piece id slots reserved (k_long_len: a piece's bytes)

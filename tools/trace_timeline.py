@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Timeline of the last encode call in a rocprofv3 kernel trace (profiling helper, not product code):
-the kernels from the last k_docstart on, with start / end relative to it and their queue (the main
+the kernels from the last k_clear on, with start / end relative to it and their queue (the main
 and the side stream of the call).   usage: trace_timeline.py DIR_OR_CSV [min_us]"""
 import csv
 import glob
@@ -13,7 +13,7 @@ if os.path.isdir(path):
     path = sorted(glob.glob(os.path.join(path, "**", "*kernel_trace.csv"), recursive=True))[-1]
 rows = list(csv.DictReader(open(path)))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-starts = [i for i, r in enumerate(rows) if "k_docstart" in r["Kernel_Name"]]
+starts = [i for i, r in enumerate(rows) if "k_clear" in r["Kernel_Name"]]
 last = rows[starts[-1]:] if starts else rows
 t0 = int(last[0]["Start_Timestamp"])
 qkey = "Queue_Id" if "Queue_Id" in last[0] else "Stream_Id"
