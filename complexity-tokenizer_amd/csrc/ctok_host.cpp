@@ -227,6 +227,7 @@ struct DeviceState {
   hipStream_t side = nullptr;     // long-piece pass, overlapped with the short merge passes
   hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_cnt = nullptr;
   uint64_t* host = nullptr;       // pinned host words for small device->host readbacks
+  uint64_t* host_dev = nullptr;   // the same words as a device pointer (k_tokoff writes the results there)
   // tables
   DevBuf<uint64_t> merge_tab, lds_image, lds16_image, merge16;
   DevBuf<uint32_t> pair0;
@@ -246,7 +247,7 @@ struct DeviceState {
   DevBuf<uint64_t> tregion;
   DevBuf<uint64_t> stamps;  // diagnostic builds (CTOK_SEG_STAMPS) with CTOK_STAMPS=1
   DevBuf<uint16_t> wpref;
-  DevBuf<uint32_t> long_cnt, long_ord, long_hist;
+  DevBuf<uint32_t> long_cnt, long_ord, long_hist, c3q;
   DevBuf<uint64_t> long_list, mid_list, scan_tmp, scan_tmp2;
   DevBuf<uint32_t> doc_flag, ncp;
   // NFC splice (nfc_splice): flagged-doc ranks / sub-batch positions, the speculative pass's
@@ -280,7 +281,7 @@ struct DeviceState {
     auto add = [&](const auto& x) { b += (uint64_t)x.cap * sizeof(*x.p); };
     add(tfirst), add(pbits), add(tile_np), add(tile_tok), add(tile_doc), add(tcls), add(list0), add(list1);
     add(list2), add(list3), add(tcnt), add(prec), add(mrec), add(pdoc), add(scratch), add(counters), add(lids), add(lw), add(tregion), add(rend);
-    add(wpref), add(long_cnt), add(long_ord), add(long_hist), add(long_pos), add(lw_pos), add(lwn), add(long_list);
+    add(wpref), add(long_cnt), add(long_ord), add(long_hist), add(long_pos), add(lw_pos), add(lwn), add(long_list), add(c3q);
     add(mid_list), add(scan_tmp), add(scan_tmp2), add(cps);
     add(doc_flag), add(ncp), add(norm_off), add(norm_text);
     add(nfc_bits), add(spl_rank), add(spl_ids), add(sub_ids), add(spl_pos), add(spl_toff), add(sub_off), add(sub_toff), add(sub_text);
@@ -1381,6 +1382,7 @@ DeviceState* device_state(ctok* t, int device) {
   HIPTRY(hipEventCreateWithFlags(&ds->ev_cnt, hipEventDisableTiming));
   HIPTRY(hipStreamCreateWithFlags(&ds->side, hipStreamNonBlocking));
   HIPTRY(hipHostMalloc((void**)&ds->host, 4096, hipHostMallocDefault));
+  HIPTRY(hipHostGetDevicePointer((void**)&ds->host_dev, ds->host, 0));
   hipStream_t s = ds->stream;
   upload(ds->merge_tab, t->merge_tab.data(), t->merge_tab.size(), s);
   upload(ds->lds_image, t->lds_image.data(), t->lds_image.size(), s);
@@ -1715,6 +1717,16 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   w.counters = ds->counters.p;
   w.scan_tmp = (uint32_t*)ds->scan_tmp.p;
   w.scan_tmp_cap = ds->scan_tmp.cap * 2;
+  // sparse class 3 (k_c3_list / k_bpe_sparse): at most c3_max pieces of 33..64 B are merged a
+  // wavefront each instead of by the register pass (CTOK_C3_SPARSE=n sets the bound, 0 disables)
+  // (read per call: the GPU tests switch it within one process)
+  const char* c3_var = getenv("CTOK_C3_SPARSE");
+  const uint64_t c3_env = c3_var ? strtoull(c3_var, nullptr, 10) : kC3SparseDefault;
+  w.c3_max = tb.n_at == 0 ? (uint32_t)std::min<uint64_t>(c3_env, B / 33 + 64) : 0u;
+  if (w.c3_max) {
+    ds->c3q.ensure(w.c3_max + 8);
+    w.c3q = ds->c3q.p;
+  }
   static const bool stamps_on = getenv("CTOK_STAMPS") != nullptr;
   if (stamps_on && nt) {  // (k_segment writes them only in a -DCTOK_SEG_STAMPS build)
     ds->stamps.ensure(nt * 8 + 8);
@@ -1745,6 +1757,7 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   // main stream's merge passes run; the long-piece tiers are then launched with grids sized for
   // the pieces there are, or not at all (no idle workgroups queued behind the merge passes)
   volatile uint32_t* seg_cnt = (volatile uint32_t*)(ds->host + 64);
+  HIPTRY(launch_c3_list(w, ds->side));  // (no LDS: it runs beside k_bpe_short; its count comes back too)
   HIPTRY(hipMemcpyAsync((void*)seg_cnt, ds->counters.p, kNumCounters * 4, hipMemcpyDeviceToHost, ds->side));
   HIPTRY(hipEventRecord(ds->ev_cnt, ds->side));
   STEP("bpe_short", launch_bpe_class(w, tb, 0, s));
@@ -1757,11 +1770,26 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
     if (e != hipErrorNotReady) throw_err(CTOK_E_DEVICE, std::string("hipEventQuery: ") + hipGetErrorString(e));
   }
   w.mid_wide = (seg_cnt[0] == 0 && !getenv("CTOK_MID512")) ? 1u : 0u;
-  if (timing) HIPTRY(hipEventRecord(ds->ev[8], s));
-  STEP("bpe_mid", launch_bpe_class(w, tb, 2, s));
-  if (timing) HIPTRY(hipEventRecord(ds->ev[10], s));
-  STEP("bpe_c3", launch_bpe_class(w, tb, 4, s));
-  if (timing) HIPTRY(hipEventRecord(ds->ev[9], s));
+  const uint32_t c3n = seg_cnt[kCtrC3Count];
+  const bool c3_sparse = c3n != 0 && c3n <= w.c3_max;
+  // Without long pieces the side stream is idle: the 17..32 B pass (overlap >= 1) and the
+  // 33..64 B pass (overlap 2) go there, so their workgroups take the CUs that k_bpe_short's
+  // workgroups free at its end instead of waiting for its last one (the classes' pieces,
+  // regions and records are disjoint; the main stream joins the side stream before k_emit)
+  const char* ov_var = getenv("CTOK_OVERLAP");
+  const int overlap = ov_var ? atoi(ov_var) : kOverlapDefault;
+  const bool mid_side = overlap >= 1 && seg_cnt[0] == 0;
+  hipStream_t s_mid = mid_side ? ds->side : s, s_c3 = (mid_side && overlap >= 2) ? ds->side : s;
+  if (timing) HIPTRY(hipEventRecord(ds->ev[8], s_mid));
+  { hipStream_t s = s_mid; STEP("bpe_mid", launch_bpe_class(w, tb, 2, s)); }
+  if (timing) HIPTRY(hipEventRecord(ds->ev[10], s_mid));
+  if (timing) HIPTRY(hipEventRecord(ds->ev[4], s_c3));
+  {
+    hipStream_t s = s_c3;
+    if (c3_sparse) STEP("bpe_c3_sparse", launch_c3_sparse(w, tb, c3n, s));
+    else STEP("bpe_c3", launch_bpe_class(w, tb, 4, s));
+  }
+  if (timing) HIPTRY(hipEventRecord(ds->ev[9], s_c3));
   if (!(w.nfc_watch == 1 && seg_cnt[12])) {  // (a failed NFC speculation discards this pass: nothing to launch)
     const uint32_t n_long = std::min<uint32_t>((uint32_t)seg_cnt[0], w.long_cap);
     bool any_gmem = false;  // a long piece for the global-memory tier (its state words reserved)
@@ -1785,17 +1813,23 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
       w.lids = ds->lids.p;
       w.lw = ds->lw.p;
     }
-    STEP("bpe_long", launch_bpe_long(w, tb, ds->side, n_long, seg_cnt[kCtrAnyC3] != 0, any_gmem));
+    STEP("bpe_long", launch_bpe_long(w, tb, ds->side, n_long, seg_cnt[kCtrAnyC3] != 0 && !c3_sparse, any_gmem));
   }
   HIPTRY(hipEventRecord(ds->ev_join, ds->side));
   HIPTRY(hipStreamWaitEvent(s, ds->ev_join, 0));
   if (timing) HIPTRY(hipEventRecord(ds->ev[5], s));
   STEP("bpe_dropped", launch_bpe_class(w, tb, 3, s));
   if (timing) HIPTRY(hipEventRecord(ds->ev[3], s));
-  STEP("emit", launch_emit(w, d_ids, ids_cap, d_tok_off, s, st != nullptr));
+  // the token count and the counters: written by k_tokoff straight into the pinned host words
+  // (two copy launches fewer at the end of every call), or copied
+  static const bool copy_res = getenv("CTOK_COPY_RESULTS") != nullptr;
+  w.host_res = copy_res ? nullptr : ds->host_dev;
+  STEP("emit", launch_emit(w, d_ids, ids_cap, d_tok_off, s, st != nullptr, seg_cnt[kCtrEmptyDocs] != 0));
   if (timing) HIPTRY(hipEventRecord(ds->ev[6], s));
-  HIPTRY(hipMemcpyAsync(ds->host, d_tok_off + n_docs, 8, hipMemcpyDeviceToHost, s));
-  HIPTRY(hipMemcpyAsync(ds->host + 1, ds->counters.p, kNumCounters * 4, hipMemcpyDeviceToHost, s));
+  if (!w.host_res) {
+    HIPTRY(hipMemcpyAsync(ds->host, d_tok_off + n_docs, 8, hipMemcpyDeviceToHost, s));
+    HIPTRY(hipMemcpyAsync(ds->host + 1, ds->counters.p, kNumCounters * 4, hipMemcpyDeviceToHost, s));
+  }
   spin_sync(ds, s);
   uint64_t ntok = ((volatile uint64_t*)ds->host)[0];
   if (w.stamps) {  // diagnostic: k_segment's mean cycles per phase over the tiles that stamped
@@ -1868,7 +1902,7 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
       st->ms_segment = el(7, 1);
       st->ms_bpe_lo = el(1, 2);
       st->ms_bpe_hi = el(8, 10);   // class 2
-      st->ms_bpe_med = el(10, 9);  // class 3, main-stream instance (the side instance overlaps)
+      st->ms_bpe_med = el(4, 9);   // class 3, main-stream instance (the side instance overlaps) or sparse path
       st->ms_bpe_short = el(1, 9);
       st->ms_bpe_long = el(9, 5);
       st->ms_emit = el(3, 6);

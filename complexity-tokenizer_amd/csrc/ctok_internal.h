@@ -43,6 +43,10 @@ __host__ __device__ constexpr int ctr_chunk(int c) { return c < 3 ? 13 + c : 18;
 constexpr int kCtrAnyMid = 19;  // counters[19] != 0: some tile has a class-2 piece
 constexpr int kCtrAnyC3 = 20;   // counters[20] != 0: some tile has a class-3 piece
 constexpr int kCtrEmptyDocs = 21;  // counters[21]: empty documents (k_tilefirst); 0: k_emit writes tok_off
+constexpr int kCtrC3Count = 22;    // counters[22]: class-3 pieces (k_c3_list; the sparse path's list length)
+constexpr int kCtrC3Take = 23;     // counters[23]: next entry of that list (k_bpe_sparse's waves)
+constexpr uint32_t kC3SparseDefault = 65536;  // Work::c3_max unless CTOK_C3_SPARSE says otherwise
+constexpr int kOverlapDefault = 1;             // merge passes on the side stream without long pieces (CTOK_OVERLAP)
 constexpr int kCtrSink = 31;       // counters[31]: panic bits of lookups whose pairs need not exist (discarded)
 constexpr int kCtrOverflow = 25;   // counters[25] != 0: a list outgrew its lean capacity (the host reruns the call safe)
 constexpr int kCtrLongIds = 26;    // counters[26]: long-piece id slots reserved (k_long_len: a piece's bytes)
@@ -271,6 +275,10 @@ struct Work {              // device pointers, sized by the host for one call
   uint32_t* scan_tmp;      // scan partials
   uint64_t scan_tmp_cap;
   uint64_t* stamps;        // diagnostic builds only (CTOK_SEG_STAMPS): 8 u64 per tile, else null
+  uint32_t* c3q;           // [c3_max] class-3 pieces as tile << 7 | list index (k_c3_list), for the sparse path
+  uint32_t c3_max;         // the sparse path takes class 3 when it holds at most this many pieces (0: never)
+  uint64_t* host_res;      // pinned host words (device pointer): k_tokoff writes the token count to [0] and
+                           // the counters to [1 ..] (null: the host copies them)
 };
 
 // ---- decode (decode.hip): ids -> UTF-8 text -------------------------------------------
@@ -359,6 +367,11 @@ hipError_t launch_norm(const uint8_t* text, const uint64_t* doc_off, uint32_t n_
 hipError_t launch_segment(const Work& w, const Tables& t, hipStream_t s);
 // cls 0: classes 0 and 1; 2: classes 2 and 3; 3: dropped-byte pieces (mid_list)
 hipError_t launch_bpe_class(const Work& w, const Tables& t, int cls, hipStream_t s);
+// sparse class 3: k_c3_list gathers the class-3 pieces (count into counters[kCtrC3Count]);
+// launch_c3_sparse merges them a wavefront per piece (the host launches it instead of the
+// 33..64 B register pass when the count is at most Work::c3_max)
+hipError_t launch_c3_list(const Work& w, hipStream_t s);
+hipError_t launch_c3_sparse(const Work& w, const Tables& t, uint32_t n_pieces, hipStream_t s);
 // long-piece preparation (side stream): lengths, order, id places (long_pos) and global-memory
 // state places (lw_pos); long_pos[n_long] / lw_pos[n_long] = the totals the host sizes lids / lw by
 hipError_t launch_long_prep(const Work& w, const Tables& t, hipStream_t s, uint32_t n_long, uint32_t* lwn,
@@ -366,8 +379,10 @@ hipError_t launch_long_prep(const Work& w, const Tables& t, hipStream_t s, uint3
 // long-piece tiers (side stream): n_long = k_segment's long-list length, any_c3 = a class-3
 // piece exists (the side instance of the 33..64 B pass); grids sized for them, nothing when empty
 hipError_t launch_bpe_long(const Work& w, const Tables& t, hipStream_t s, uint32_t n_long, bool any_c3, bool any_gmem);
+// count_pieces: counters[5] = pieces (statistics); empty_docs: some document is empty (k_tokoff
+// then writes every tok_off entry; else k_emit wrote them and k_tokoff only the total)
 hipError_t launch_emit(const Work& w, uint32_t* ids, uint64_t ids_cap, uint64_t* tok_off, hipStream_t s,
-                       bool count_pieces);  // count_pieces: counters[5] = pieces (statistics)
+                       bool count_pieces, bool empty_docs = true);
 // exclusive scan of n u32 (n read from *n_dev when non-null, else n_max); out[n] = total
 hipError_t scan_u32(const uint32_t* in, uint32_t* out, uint64_t n_max, const uint32_t* n_dev,
                     uint32_t* tmp, uint64_t tmp_cap, hipStream_t s);

@@ -3161,6 +3161,156 @@ hipError_t launch_bpe_long(const Work& w, const Tables& t, hipStream_t s, uint32
 }
 
 // ------------------------------------------------------------------------------------------
+// Sparse 33..64 B class (round 6).  On English-like text class 3 is a few pieces per thousand
+// tiles (C4: ~600 pieces in 322k tiles; C2 or a 1/8 C4 shard: ~70), and the register pass
+// (k_bpe_mid<3>: a thread per piece over 64 slots, ~1,300 VALU per merge) then costs one thread's
+// whole merge chain: 90 us on C2, 190 us on C4 for a few kilobytes.  k_c3_list gathers the
+// class-3 list entries into one list (a wave per 64 tiles of tcls, one atomic per wave that meets
+// any); when the host sees at most Work::c3_max of them it launches k_bpe_sparse instead of the
+// register pass: a wavefront per piece (merge_wave64), its ids into the tile's class-3 region
+// (reserved from rend, as the dropped-byte pass does) and its merged record in mrec -- what the
+// register pass would write.
+__global__ __launch_bounds__(256) void k_c3_list(Work w) {
+  if (spec_failed(w)) return;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t* cnt3 = w.tcls + 3ull * w.n_tiles;
+  for (uint32_t t0 = blockIdx.x * 256 + (threadIdx.x & ~63u); t0 < w.n_tiles; t0 += gridDim.x * 256) {
+    const uint32_t tile = t0 + lane;
+    const uint32_t c = tile < w.n_tiles ? cnt3[tile] : 0u;
+    if (__ballot(c != 0) == 0) continue;  // (wave-uniform)
+    const uint32_t inc = wave_incl_scan(c);
+    uint32_t b = 0;
+    if (lane == 63) b = atomicAdd(&w.counters[kCtrC3Count], inc);
+    b = __builtin_amdgcn_readlane(b, 63) + inc - c;
+    for (uint32_t j = 0; j < c; j++)
+      if (b + j < w.c3_max) w.c3q[b + j] = (tile << 7) | j;
+  }
+}
+
+// The merge loop of one <= 64-token piece on a whole wavefront: lane k holds token k (positions
+// stay put) and the value of the pair its token starts (kNoRank when it starts none); the live
+// mask lv (wave-uniform, in SGPRs) marks the lanes that still hold a token.  A merge is a 64-lane
+// minimum of value << 6 | lane (the lowest value, leftmost on ties: src/bpe.rs:118-149, as
+// merge_slots), its neighbours found with scalar bit scans of lv, the two new pairs looked up at
+// once by lanes 0 and 1, and three selects -- a chain of ~40 instructions and one LDS probe per
+// merge where the register pass spends ~1,300 on one lane.  Returns the token count.
+template <bool COMPACT, bool NARROW>
+__device__ __forceinline__ uint32_t merge_wave64(const Tables& t, const PairLds& P, uint32_t& tok, uint32_t rk,
+                                                 uint64_t& lv, uint32_t* err) {
+  const uint32_t lane = threadIdx.x & 63;
+  for (;;) {
+    const uint32_t best = wave_min_full_u32((rk << 6) | lane);
+    const uint32_t r = best >> 6, bi = best & 63u;
+    if (r == kNoRank) break;
+    const uint32_t nid = COMPACT ? r : uni(t.rank_newid[r]);
+    const uint64_t right = lv & ~((2ull << bi) - 1ull);  // live lanes past bi (bi < 63: it starts a pair)
+    const uint32_t p = (uint32_t)__builtin_ctzll(right);  // the right token
+    const uint64_t after = right & (right - 1ull);
+    const bool has_r = after != 0;
+    const uint32_t q = has_r ? (uint32_t)__builtin_ctzll(after) : 0u;  // the token after it
+    const uint64_t left = lv & ((1ull << bi) - 1ull);
+    const bool has_l = left != 0;
+    const uint32_t pv = has_l ? 63u - (uint32_t)__builtin_clzll(left) : 0u;  // the token before
+    const uint32_t L = __builtin_amdgcn_readlane(tok, pv), R = __builtin_amdgcn_readlane(tok, q);
+    uint32_t v = kNoRank;
+    if (lane < 2) {  // lane 0: (L, nid), lane 1: (nid, R)
+      Probe<NARROW, true> pr;
+      pr.start(t, P, lane == 0 ? L : nid, lane == 0 ? nid : R, lane == 0 ? has_l : has_r);
+      v = pr.finish(t, err);
+    }
+    const uint32_t rl = __builtin_amdgcn_readlane(v, 0), rr = __builtin_amdgcn_readlane(v, 1);
+    tok = lane == bi ? nid : tok;
+    rk = (has_l && lane == pv) ? rl : rk;
+    rk = lane == bi ? (has_r ? rr : kNoRank) : rk;
+    rk = lane == p ? kNoRank : rk;
+    lv &= ~(1ull << p);
+  }
+  return (uint32_t)__popcll(lv);
+}
+
+constexpr int kSparseWaves = 16;  // waves per k_bpe_sparse workgroup (beside the 96 KiB image: one per CU)
+
+template <bool COMPACT, bool NARROW>
+__global__ __launch_bounds__(64 * kSparseWaves) void k_bpe_sparse(Work w, Tables t, uint32_t n) {
+  if (spec_failed(w)) return;
+  extern __shared__ __attribute__((aligned(16))) uint4 s_dyn[];
+  __shared__ int32_t s_b2id[256];
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  const uint4* img = NARROW ? t.lds16_image : t.lds_image;
+  for (uint32_t i = tid; i < kLdsImageBytes / 16; i += 64 * kSparseWaves) s_dyn[i] = img[i];
+  for (uint32_t i = tid; i < 256; i += 64 * kSparseWaves) s_b2id[i] = t.byte2id[i];
+  __syncthreads();
+  const PairLds P{(const lds_u64*)s_dyn, (const lds_u32*)(s_dyn + kHotBuckets)};
+  uint32_t* err = &w.counters[2];
+  uint32_t st_bytes = 0, st_ids = 0;
+  for (;;) {
+    // (every lane takes part, lane 0 adding 1: no divergent branch around the atomic)
+    const uint32_t k = uni(atomicAdd(&w.counters[kCtrC3Take], lane == 0 ? 1u : 0u));
+    if (k >= n) break;
+    const uint32_t qe = uni(w.c3q[k]);
+    const uint32_t tile = qe >> 7;
+    const uint32_t e = uni(w.list3[(size_t)tile * kCap3 + (qe & 127u)]);
+    const uint32_t s = tile * kTile + (e & 0xFFFu), o = ent_ord(e), len = ent_len(e);
+    // lane k: byte k, its token, the value of the byte pair it starts (the 256 x 256 table)
+    const uint32_t b0 = lane < len ? w.text[s + lane] : 0u;
+    const uint32_t b1 = lane + 1 < len ? w.text[s + lane + 1] : 0u;
+    const int32_t id = s_b2id[b0];
+    if (__ballot(lane < len && id < 0)) {  // a byte char absent from the vocab: the generic pass drops it
+      if (lane == 0) {
+        const uint32_t mi = atomicAdd(&w.counters[4], 1u);
+        if (mi < w.mid_cap) w.mid_list[mi] = (uint64_t)s | ((uint64_t)o << 32) | ((uint64_t)len << 48);
+        else atomicOr(&w.counters[kCtrOverflow], 1u);
+      }
+      continue;
+    }
+    uint32_t rk = lane + 1 < len ? t.pair0[(b0 << 8) | b1] : kNoRank;
+    if (rk != kNoRank && value_panics(t, rk)) {
+      atomicOr(err, kErrPanic);
+      rk = kNoRank;
+    }
+    uint32_t tok = (uint32_t)id;
+    uint64_t lv = len >= 64 ? ~0ull : (1ull << len) - 1ull;
+    const uint32_t m = merge_wave64<COMPACT, NARROW>(t, P, tok, rk, lv, err);
+    uint32_t pos = 0;
+    if (lane == 0) pos = atomicAdd(&w.rend[3ull * w.n_tiles + tile], m);
+    pos = uni(pos);
+    if ((lv >> lane) & 1u) w.scratch[(size_t)tile * kTileSlots + pos + __popcll(lv & lanemask_lt())] = tok;
+    if (lane == 0) {
+      w.mrec[(size_t)tile * kTileSlots + o] = rec_short(m, pos);
+      atomicAdd(&w.tile_tok[tile], m);
+    }
+    st_bytes += len;
+    st_ids += m;
+  }
+  if (lane == 0 && st_bytes) {  // statistics: bytes merged / ids produced by class 3
+    atomicAdd(&w.counters[ctr_stat(3)], st_bytes);
+    atomicAdd(&w.counters[ctr_stat(3) + 1], st_ids);
+  }
+}
+
+hipError_t launch_c3_list(const Work& w, hipStream_t s) {
+  if (!w.n_tiles || !w.c3_max) return hipSuccess;
+  const uint32_t grid = std::max(1u, std::min((w.n_tiles + 255) / 256, 4 * w.n_cus));
+  k_c3_list<<<grid, 256, 0, s>>>(w);
+  return hipGetLastError();
+}
+
+template <bool C, bool NW>
+static hipError_t launch_sparse_t(const Work& w, const Tables& t, uint32_t n_pieces, hipStream_t s) {
+  static LdsAttr attr;
+  HIPCHK(lds_attr_once(attr, (const void*)k_bpe_sparse<C, NW>, kLdsImageBytes));
+  const uint32_t grid = std::max(1u, std::min((n_pieces + kSparseWaves - 1) / kSparseWaves, w.n_cus));
+  k_bpe_sparse<C, NW><<<grid, 64 * kSparseWaves, kLdsImageBytes, s>>>(w, t, n_pieces);
+  return hipGetLastError();
+}
+
+hipError_t launch_c3_sparse(const Work& w, const Tables& t, uint32_t n_pieces, hipStream_t s) {
+  if (!n_pieces || n_pieces > w.c3_max) return hipSuccess;
+  if (t.compact) return t.narrow ? launch_sparse_t<true, true>(w, t, n_pieces, s) : launch_sparse_t<true, false>(w, t, n_pieces, s);
+  return t.narrow ? launch_sparse_t<false, true>(w, t, n_pieces, s) : launch_sparse_t<false, false>(w, t, n_pieces, s);
+}
+
+// ------------------------------------------------------------------------------------------
 // emission.  tile_tok is scanned to each tile's first id (tile_doc to its first document); then
 // one wavefront per tile walks the tile's piece records in rounds of 256 pieces: lane l takes
 // pieces 256 r + 4 l .. + 3 (one 8- or 16-byte prec load and their pdoc bits), a wave scan
@@ -3459,6 +3609,11 @@ __device__ __forceinline__ void tokoff_one(const Work& w, uint64_t* __restrict__
 }
 
 __global__ void k_tokoff(Work w, uint64_t* __restrict__ tok_off) {
+  if (w.host_res && blockIdx.x == 0) {  // the call's results into the host's pinned words
+    if (threadIdx.x < (uint32_t)kNumCounters) ((uint32_t*)(w.host_res + 1))[threadIdx.x] = w.counters[threadIdx.x];
+    if (threadIdx.x == 0) w.host_res[0] = w.tile_tok[w.n_tiles];
+    __threadfence_system();
+  }
   if (spec_failed(w)) return;
   if (w.counters[kCtrEmptyDocs] == 0) {  // k_emit wrote tok_off[0 .. n_docs)
     if (blockIdx.x == 0 && threadIdx.x == 0) tok_off[w.n_docs] = w.tile_tok[w.n_tiles];
@@ -3469,7 +3624,7 @@ __global__ void k_tokoff(Work w, uint64_t* __restrict__ tok_off) {
 }
 
 hipError_t launch_emit(const Work& w, uint32_t* ids, uint64_t ids_cap, uint64_t* tok_off, hipStream_t s,
-                       bool count_pieces) {
+                       bool count_pieces, bool empty_docs) {
   HIPCHK(scan_tiles(w, s, count_pieces));
   if (w.n_tiles) {
     const uint32_t nb = (w.n_tiles + kEmitWaves - 1) / kEmitWaves;
@@ -3477,7 +3632,7 @@ hipError_t launch_emit(const Work& w, uint32_t* ids, uint64_t ids_cap, uint64_t*
     else k_emit<uint32_t><<<nb, 64 * kEmitWaves, 0, s>>>(w, ids, ids_cap, tok_off);
   }
   // (grid-stride: with no empty document only tok_off[n_docs] is left to write)
-  k_tokoff<<<std::min<uint32_t>((w.n_docs + 1 + 255) / 256, 4096), 256, 0, s>>>(w, tok_off);
+  k_tokoff<<<empty_docs ? std::min<uint32_t>((w.n_docs + 1 + 255) / 256, 4096) : 1u, 256, 0, s>>>(w, tok_off);
   return hipGetLastError();
 }
 

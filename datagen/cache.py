@@ -52,10 +52,25 @@ def build(outdir: str, names) -> None:
             text, off = corpus.corpus_c5nfc(base=c5)
         elif name == "C4":  # 10M docs: independent 1M-doc blocks on worker processes
             text, off = corpus.corpus_c4(workers=min(16, len(os.sched_getaffinity(0))))
+        elif name.startswith("C4S"):  # C4S<N>: rank 0's shard of the N-way split (bench.py --gpus N)
+            text, off = c4_shard(int(name[3:]), 0)
         else:
             text, off = corpus.CONFIGS[name]()
         _save(outdir, name, text, off)
         print("datagen.cache: %s built in %.1f s" % (name, time.time() - t), file=sys.stderr, flush=True)
+
+
+def c4_shard(world: int, rank: int):
+    """(text, off) of rank `rank`'s byte-balanced shard of C4 cut `world` ways -- the per-GPU work
+    of bench.py --gpus `world` (complexity_tokenizer.parallel.shard_bounds)."""
+    from datagen import corpus
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    pkg = os.path.join(root, "complexity-tokenizer_amd")
+    if pkg not in sys.path:
+        sys.path.insert(0, pkg)
+    from complexity_tokenizer.parallel import shard_bounds
+    d0, d1 = shard_bounds(corpus.c4_offsets(corpus.C4_DOCS), world, rank)
+    return corpus.corpus_c4_range(d0, d1, corpus.C4_DOCS, workers=min(8, len(os.sched_getaffinity(0))))
 
 
 _PROCS: dict = {}  # corpus name -> the background process building it

@@ -6,6 +6,7 @@ letters drawn from a small alphabet (many merges), with (x, x) chains ("aaaa", "
 rounds take every other site), with two-token periods, with multi-byte letters (CJK, 3 bytes
 each) and with a table that is not rank-monotone (one site per round)."""
 import json
+import os
 import random
 
 import pytest
@@ -100,3 +101,57 @@ def test_pieces_across_tile_ends(gpt2, multi_path):
     with open(multi_path) as f:
         obj = json.load(f)
     check(Tokenizer.from_file(multi_path), ref_c.RefC(obj), docs)
+
+
+class _env:
+    """Set an environment variable for the duration of a block (the library reads CTOK_C3_SPARSE
+    on every call)."""
+
+    def __init__(self, k, v):
+        self.k, self.v = k, v
+
+    def __enter__(self):
+        self.old = os.environ.get(self.k)
+        os.environ[self.k] = self.v
+
+    def __exit__(self, *a):
+        if self.old is None:
+            del os.environ[self.k]
+        else:
+            os.environ[self.k] = self.old
+
+
+@pytest.mark.parametrize("bound", ["0", "1", "100000000"])
+def test_c3_register_and_sparse_paths(gpt2, multi_path, bound):
+    """The 33..64 B class by either implementation, against the C oracle: the register pass
+    (k_bpe_mid<3>; CTOK_C3_SPARSE=0 or a bound below the class's size) and the sparse path
+    (k_c3_list + k_bpe_sparse: a wavefront per piece, taken when the class holds at most the
+    bound's pieces; 100000000 forces it on the multilingual sample's dense class 3)."""
+    _, tok, rc = gpt2
+    with open(multi_path) as f:
+        mobj = json.load(f)
+    mtok, mrc = Tokenizer.from_file(multi_path), ref_c.RefC(mobj)
+    text, off = corpus.corpus_c5(20_000, seed=77)
+    c5 = [d.decode() for d in corpus.unpack(text, off)]
+    with _env("CTOK_C3_SPARSE", bound):
+        st = check(tok, rc, tier_docs(5))
+        assert st["class_ids"][3] > 0
+        st5 = check(mtok, mrc, c5 + tier_docs(6))
+        assert st5["class_ids"][3] > 1000  # (a dense class 3: CJK runs)
+    with _env("CTOK_C3_SPARSE", "0"):
+        ref5 = check(mtok, mrc, c5 + tier_docs(6))
+    # both implementations merge the same pieces into the same number of ids
+    assert st5["class_bytes"][3] == ref5["class_bytes"][3] and st5["class_ids"][3] == ref5["class_ids"][3]
+
+
+def test_c3_sparse_improper_and_wide_tables(gpt2, llama3_path):
+    """The sparse path on a table that is not rank-monotone (serial rounds, no window merges) and
+    on a wide (128k-vocabulary) table, against the C oracle."""
+    obj, _, _ = gpt2
+    sh = toys.shuffled_merges(obj, seed=9)
+    with open(llama3_path) as f:
+        lobj = json.load(f)
+    with _env("CTOK_C3_SPARSE", "100000000"):
+        check(Tokenizer.from_str(json.dumps(sh)), ref_c.RefC(sh), tier_docs(7))
+        st = check(Tokenizer.from_file(llama3_path), ref_c.RefC(lobj), tier_docs(8))
+        assert st["class_ids"][3] > 0

@@ -41,7 +41,10 @@ for _ in range(reps):
 st = tok.last_stats
 # the last call's output against the golden digest of the config (tests/golden/digests.json)
 gold = json.load(open(os.path.join(ROOT, "tests", "golden", "digests.json"))).get(cfg)
-if gold is not None and "shards" in gold:  # C4: the digest of the 1-way shard is the whole corpus's
+if cfg.startswith("C4S"):  # C4S<N>: rank 0's shard of the N-way split
+    gold = json.load(open(os.path.join(ROOT, "tests", "golden", "digests.json")))["C4"]
+    gold = dict(gold, sha256=gold["shards"]["0/%d" % int(cfg[3:])]["sha256"])
+elif gold is not None and "shards" in gold:  # C4: the digest of the 1-way shard is the whole corpus's
     gold = dict(gold, sha256=gold["shards"]["0/1"]["sha256"])
 parity = "no golden digest"
 if gold is not None and gold["tokenizer"] == fx:
