@@ -199,11 +199,15 @@ def workload(args, rank, world):
     # shards are cached under /tmp: a profiled rerun (rocprofv3 --pmc initialises the GPU before
     # main) must not fork a corpus pool, so it reads what the unprofiled run built
     cache = os.path.join(os.environ.get("TMPDIR", "/tmp"), "ctok_corpus", "c4_%d_%d_%d.npz" % (n, d0, d1))
+    # under a profiler (rocprofv3 sets ROCPROF_* variables for the program) the corpus is
+    # built without a process pool when no cached shard exists: the profiler would follow the
+    # forked workers
+    profiled = any(k.startswith("ROCPROF") for k in os.environ)
     if os.path.exists(cache):
         z = np.load(cache)
         text, off = z["text"], z["off"]
     else:
-        text, off = corpus.corpus_c4_range(d0, d1, n, workers=1 if args.corpus_workers == 1 else
+        text, off = corpus.corpus_c4_range(d0, d1, n, workers=1 if (args.corpus_workers == 1 or profiled) else
                                            max(1, min(8, cpus // world)))
         try:
             os.makedirs(os.path.dirname(cache), exist_ok=True)

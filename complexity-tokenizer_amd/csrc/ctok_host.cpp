@@ -246,6 +246,7 @@ struct DeviceState {
   DevBuf<uint32_t> lids, lw, long_pos, lw_pos, lwn, rend, cps;
   DevBuf<uint64_t> tregion;
   DevBuf<uint64_t> stamps;  // diagnostic builds (CTOK_SEG_STAMPS) with CTOK_STAMPS=1
+  DevBuf<uint64_t> wgrec;   // diagnostic: CTOK_WGREC=1
   DevBuf<uint16_t> wpref;
   DevBuf<uint32_t> long_cnt, long_ord, long_hist, c3q;
   DevBuf<uint64_t> long_list, mid_list, scan_tmp, scan_tmp2;
@@ -346,6 +347,7 @@ struct ctok {
   bool proper = true;
   bool compact = false;
   bool narrow = false;  // every vocab id < 2^16
+  bool hot1 = false;    // the narrow LDS image in the one-bucket layout (CTOK_HOT1)
   bool ids16 = false;   // every id encode can emit (vocab and added tokens) < 2^16: 16-bit ids on PCIe
   // decode (src/huggingface/mod.rs:710-747): decoder kind, per-id decoded bytes
   int decoder = 1;                  // 1 ByteLevel, 0 raw concatenation (unknown decoder type), -1 unsupported
@@ -633,16 +635,18 @@ std::string rust_regex_rejects(const std::string& p) {
           continue;
         }
         if (d == '[' && j + 1 < n && p[j + 1] == ':') {
+          // [:name:] with a known name is an ASCII class; with any other name regex-syntax
+          // (maybe_parse_ascii_class) backtracks and reads the '[' as a nested class
           const size_t e = p.find(":]", j + 2);
           if (e != std::string::npos) {
             std::string nm = p.substr(j + 2, e - j - 2);
             if (!nm.empty() && nm[0] == '^') nm.erase(0, 1);
             static const char* const kAscii[] = {"alnum", "alpha", "ascii", "blank", "cntrl", "digit", "graph",
                                                  "lower", "print", "punct", "space", "upper", "word", "xdigit"};
-            if (std::find_if(std::begin(kAscii), std::end(kAscii), [&](const char* a) { return nm == a; }) == std::end(kAscii))
-              return "unknown ASCII class [:" + nm + ":]";
-            j = e + 2;
-            continue;
+            if (std::find_if(std::begin(kAscii), std::end(kAscii), [&](const char* a) { return nm == a; }) != std::end(kAscii)) {
+              j = e + 2;
+              continue;
+            }
           }
         }
         if (d == '[') {
@@ -668,7 +672,7 @@ std::string rust_regex_rejects(const std::string& p) {
         if (starts("<=") || starts("<!")) return "look-behind (?" + std::string(rest.substr(0, 2));
         if (starts(">")) return "atomic group (?>";
         if (starts("P=")) return "named backreference (?P=";
-        if (!rest.empty() && (strchr("|#('&R+0", rest[0]) || isdigit((unsigned char)rest[0])))
+        if (!rest.empty() && (strchr("|#('&+0", rest[0]) || isdigit((unsigned char)rest[0])))
           return std::string("unsupported group (?") + rest[0];
         if (starts("P<") || starts("<")) {
           const size_t k = i + 2 + (starts("P<") ? 2 : 1);
@@ -720,9 +724,19 @@ std::string rust_regex_rejects(const std::string& p) {
         const size_t comma = body.find(',');
         const std::string a = body.substr(0, comma), b = comma == std::string::npos ? "" : body.substr(comma + 1);
         auto digits = [](const std::string& s) { return !s.empty() && std::all_of(s.begin(), s.end(), ::isdigit); };
+        // a count is a u32 (regex-syntax parse_decimal): a longer one is an invalid decimal
+        auto count = [](const std::string& s) -> uint64_t {
+          uint64_t v = 0;
+          for (char ch : s) {
+            v = v * 10 + (uint64_t)(ch - '0');
+            if (v > 0xFFFFFFFFull) return ~(uint64_t)0;
+          }
+          return v;
+        };
         if (digits(a) && (comma == std::string::npos || b.empty() || digits(b))) {
           if (empty.back()) return "repetition operator missing expression";
-          if (!b.empty() && std::stoull(b) < std::stoull(a)) return "invalid repetition range {" + body + "}";
+          if (count(a) == ~(uint64_t)0 || (!b.empty() && count(b) == ~(uint64_t)0)) return "repetition count overflows u32 {" + body + "}";
+          if (!b.empty() && count(b) < count(a)) return "invalid repetition range {" + body + "}";
           i = e + 1;
           continue;
         }
@@ -1065,7 +1079,26 @@ void load_root(ctok* t, const ctj::Value& root) {
       uint64_t* hot16 = t->lds16_image.data();
       std::fill(hot16, hot16 + kHotU64, kEmpty);
       uint32_t* bloom16 = reinterpret_cast<uint32_t*>(hot16 + kHotU64);
+      // one-bucket layout (hot1, CTOK_HOT1=1; ctok_internal.h): a pair's 4 candidate slots in one
+      // 32-byte bucket, its two Bloom bits in one word
+      t->hot1 = getenv("CTOK_HOT1") != nullptr;
       for (const auto& re : by_rank) {
+        if (!t->hot1) break;
+        const uint64_t e = re.second;
+        const uint32_t a = (uint32_t)((e >> kIdBits) & ((1u << kIdBits) - 1)), b = (uint32_t)(e & ((1u << kIdBits) - 1));
+        const uint32_t h = hash16_h(a, b), g = hash16_g(a, b);
+        uint64_t* slot = nullptr;
+        if (use_hot && re.first < valid_new.size())
+          for (int k = 0; k < 4 && !slot; k++)
+            if (hot16[hot1_bucket(h) + k] == kEmpty) slot = &hot16[hot1_bucket(h) + k];
+        if (slot) {
+          *slot = ((e >> 42) << 32) | key16(a, b);
+          continue;
+        }
+        bloom16[hot1_word(g)] |= hot1_bits(g);
+      }
+      for (const auto& re : by_rank) {
+        if (t->hot1) break;
         const uint64_t e = re.second;
         const uint32_t a = (uint32_t)((e >> kIdBits) & ((1u << kIdBits) - 1)), b = (uint32_t)(e & ((1u << kIdBits) - 1));
         const uint32_t h = hash16_h(a, b), g = hash16_g(a, b);
@@ -1461,6 +1494,7 @@ DeviceState* device_state(ctok* t, int device) {
   tb.proper = (t->proper && !getenv("CTOK_FORCE_IMPROPER")) ? 1 : 0;
   tb.compact = t->compact ? 1 : 0;
   tb.narrow = (t->narrow && !getenv("CTOK_FORCE_WIDE_SLOTS")) ? 1 : 0;
+  tb.hot1 = t->hot1 ? 1 : 0;
   tb.dbg = getenv("CTOK_DBG_MODE") ? (uint32_t)atoi(getenv("CTOK_DBG_MODE")) : 0;
   DeviceState* r = ds.get();
   t->devs[device] = std::move(ds);
@@ -1645,6 +1679,10 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
     w.nfc_bits = ds->nfc_bits.p;
   }
   w.keep_first = keep_first ? 1u : 0u;
+  {
+    const char* v = getenv("CTOK_SHORT_WGS");
+    w.short_wgs = v ? (uint32_t)atoi(v) : 0u;
+  }
   const size_t nt = w.n_tiles;
   ds->tfirst.ensure(nt + 8);
   ds->pbits.ensure(w.n_words + 8);
@@ -1726,6 +1764,16 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   if (w.c3_max) {
     ds->c3q.ensure(w.c3_max + 8);
     w.c3q = ds->c3q.p;
+  }
+#ifdef CTOK_CHECK
+  // (range-checking build: every merged record starts out of range, so one no pass wrote traps)
+  HIPTRY(hipMemsetAsync(ds->mrec.p, 0xFF, (size_t)nt * kTileSlots * 4, s));
+#endif
+  static const bool wgrec_on = getenv("CTOK_WGREC") != nullptr;
+  if (wgrec_on) {  // diagnostic: per-workgroup records of the merge passes (kernels.hip WgRec)
+    ds->wgrec.ensure(kWgRecWords);
+    HIPTRY(hipMemsetAsync(ds->wgrec.p, 0, kWgRecWords * 8, s));
+    w.wgrec = ds->wgrec.p;
   }
   static const bool stamps_on = getenv("CTOK_STAMPS") != nullptr;
   if (stamps_on && nt) {  // (k_segment writes them only in a -DCTOK_SEG_STAMPS build)
@@ -1832,6 +1880,33 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   }
   spin_sync(ds, s);
   uint64_t ntok = ((volatile uint64_t*)ds->host)[0];
+  if (w.wgrec) {  // per kernel: workgroups, distinct CUs, start / end spread (us from the first start)
+    std::vector<uint64_t> r(kWgRecWords);
+    HIPTRY(hipMemcpy(r.data(), w.wgrec, kWgRecWords * 8, hipMemcpyDeviceToHost));
+    uint64_t t0 = ~0ull;
+    for (size_t i = 0; i < kWgRecWords; i += 4)
+      if (r[i]) t0 = std::min(t0, r[i]);
+    static const char* names[4] = {"k_bpe_short", "k_bpe_mid<2>", "k_bpe_mid<3>", "k_bpe_sparse"};
+    for (int k = 0; k < 4; k++) {
+      std::vector<uint64_t> cus;
+      double s0 = 1e30, s1 = 0, e0 = 1e30, e1 = 0;
+      int n = 0, busy = 0;
+      for (int b = 0; b < 1024; b++) {
+        const uint64_t* q = &r[((size_t)k * 1024 + b) * 4];
+        if (!q[0] || !q[1]) continue;
+        n++;
+        busy += q[3] != 0;
+        cus.push_back(q[2]);
+        const double a = (q[0] - t0) / 100.0, e = (q[1] - t0) / 100.0;  // (100 MHz clock)
+        s0 = std::min(s0, a), s1 = std::max(s1, a), e0 = std::min(e0, e), e1 = std::max(e1, e);
+      }
+      if (!n) continue;
+      std::sort(cus.begin(), cus.end());
+      const size_t ncu = std::unique(cus.begin(), cus.end()) - cus.begin();
+      fprintf(stderr, "[ctok wgrec] %-13s wgs %4d (working %4d) on %3zu CUs  start %8.1f .. %8.1f  end %8.1f .. %8.1f us\n",
+              names[k], n, busy, ncu, s0, s1, e0, e1);
+    }
+  }
   if (w.stamps) {  // diagnostic: k_segment's mean cycles per phase over the tiles that stamped
     std::vector<uint64_t> st8((size_t)w.n_tiles * 8);
     HIPTRY(hipMemcpy(st8.data(), w.stamps, st8.size() * 8, hipMemcpyDeviceToHost));

@@ -46,6 +46,7 @@ constexpr int kCtrEmptyDocs = 21;  // counters[21]: empty documents (k_tilefirst
 constexpr int kCtrC3Count = 22;    // counters[22]: class-3 pieces (k_c3_list; the sparse path's list length)
 constexpr int kCtrC3Take = 23;     // counters[23]: next entry of that list (k_bpe_sparse's waves)
 constexpr uint32_t kC3SparseDefault = 65536;  // Work::c3_max unless CTOK_C3_SPARSE says otherwise
+constexpr uint32_t kWgRecWords = 4 * 1024 * 4;  // Work::wgrec: 4 kernels x 1024 workgroups x 4 words
 constexpr int kOverlapDefault = 1;             // merge passes on the side stream without long pieces (CTOK_OVERLAP)
 constexpr int kCtrSink = 31;       // counters[31]: panic bits of lookups whose pairs need not exist (discarded)
 constexpr int kCtrOverflow = 25;   // counters[25] != 0: a list outgrew its lean capacity (the host reruns the call safe)
@@ -142,6 +143,13 @@ __host__ __device__ inline uint32_t hash16_h(uint32_t a, uint32_t b) {
 __host__ __device__ inline uint32_t hash16_g(uint32_t a, uint32_t b) {
   return mul24(b, 0xC2B2AFu) + mul24(a ^ 0x5A5Au, 0x27D4EBu);
 }
+// One-bucket layout of the narrow image (Tables::hot1, an A/B of round 6): the hot table as 2048
+// buckets of four entries, a pair's bucket hash16_h >> 21 (one 32-byte read instead of two
+// 16-byte buckets); the Bloom filter blocked, both of a pair's bits in word hash16_g >> 19 (one
+// read instead of two).
+__host__ __device__ inline uint32_t hot1_bucket(uint32_t h) { return 4u * (h >> 21); }  // (u64 index)
+__host__ __device__ inline uint32_t hot1_word(uint32_t g) { return g >> 19; }
+__host__ __device__ inline uint32_t hot1_bits(uint32_t g) { return (1u << (g & 31u)) | (1u << ((g >> 5) & 31u)); }
 
 // Whole-piece table: raw byte strings of <= 8 bytes whose BPE is exactly one token (checked at
 // load time by running the merge loop on every vocab entry).  Entry = {lo32, hi32, len, id} of
@@ -216,6 +224,7 @@ struct Tables {            // device pointers, owned by the host runtime
   uint32_t compact;         // 1: entry values are new ids (strictly increasing in rank), else ranks
   uint32_t narrow;          // 1: every vocab id < 2^16 (the merge passes keep the last tier's tokens as u16 in LDS)
   uint32_t dbg;             // debug mode (CTOK_DBG_MODE), 0 in production
+  uint32_t hot1;            // 1: the narrow image in the one-bucket layout (hot1_bucket / hot1_word)
 };
 
 struct Work {              // device pointers, sized by the host for one call
@@ -234,6 +243,7 @@ struct Work {              // device pointers, sized by the host for one call
   uint32_t* nfc_bits;      // nfc_watch: bit g set when 64-byte word g holds the start of a code point
                            // NFC might change (zeroed by the host; nfc_splice flags docs from it)
   uint32_t mid_wide;       // 1: the 17..32 B pass at 768 threads per workgroup (the call has no long pieces)
+  uint32_t short_wgs;      // workgroups of k_bpe_short (0: one per CU)
   uint32_t keep_first;     // 1: k_emit leaves every piece's first id within its tile in tcnt (not
                            // only doc-start pieces'), for ctok_encode_offsets
   uint16_t* wpref;         // [n_tiles * 64] pieces of the tile before each 64-byte word
@@ -279,6 +289,7 @@ struct Work {              // device pointers, sized by the host for one call
   uint32_t c3_max;         // the sparse path takes class 3 when it holds at most this many pieces (0: never)
   uint64_t* host_res;      // pinned host words (device pointer): k_tokoff writes the token count to [0] and
                            // the counters to [1 ..] (null: the host copies them)
+  uint64_t* wgrec;         // diagnostic (CTOK_WGREC=1): per-workgroup start / end / CU of the merge passes, else null
 };
 
 // ---- decode (decode.hip): ids -> UTF-8 text -------------------------------------------

@@ -129,6 +129,43 @@ __device__ T block_excl_scan(T v, T* smem /*[17]*/, T* total) {
 // wave reduces over inactive lanes and never terminates).
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// Range checks of decoded piece records (opt-in build: -DCTOK_CHECK, tools/build_variant.sh):
+// a record out of range prints where it was found and traps, instead of steering a gather
+// through garbage offsets (round 5's r05_v12 fault: unwritten merged records).  The host then
+// also fills mrec with all ones before each call, so a record no pass wrote is out of range too.
+#ifdef CTOK_CHECK
+#define CTOK_CHECK_REC(cond, ...)                                                            \
+  do {                                                                                     \
+    if (!(cond)) {                                                                         \
+      printf(__VA_ARGS__);                                                                 \
+      __builtin_trap();                                                                    \
+    }                                                                                      \
+  } while (0)
+#else
+#define CTOK_CHECK_REC(cond, ...) do { } while (0)
+#endif
+
+// Diagnostic (CTOK_WGREC=1, Work::wgrec non-null): workgroup `blockIdx.x` of kernel slot k records
+// its start and end (wall clock, 100 MHz), its CU (xcc | se | cu) and a count.  The host prints,
+// per kernel, the CUs used and the spread of the workgroups' starts and ends (ctok_host.cpp).
+constexpr uint32_t kWgRecMax = 1024;  // (4 kernel slots: short, mid<2>, mid<3>, sparse)
+struct WgRec {
+  uint64_t* p = nullptr;
+  __device__ __forceinline__ void begin(uint64_t* base, uint32_t k) {
+    if (base && threadIdx.x == 0 && blockIdx.x < kWgRecMax) {
+      p = base + ((size_t)k * kWgRecMax + blockIdx.x) * 4;
+      p[0] = (uint64_t)wall_clock64();
+      p[2] = __smid();
+    }
+  }
+  __device__ __forceinline__ void end(uint32_t count) {
+    if (p) {
+      p[1] = (uint64_t)wall_clock64();
+      p[3] = count;
+    }
+  }
+};
+
 // NFC speculation failed in k_segment (a code point NFC might change): the rest of this pass is
 // discarded (the host checks, normalises and runs the pipeline again), so the kernels after
 // k_segment return at once instead of merging text that will be re-encoded.
@@ -1202,10 +1239,21 @@ struct Probe<true, HOT> {
     k = key16(a, b);
     h = hash16_h(a, b);
     const uint32_t h2 = hash16_g(a, b);
-    const uint32_t b1 = h & (kBloomBits - 1), b2 = h2 >> 14;
-    const uint32_t f = (P.bloom[b1 >> 5] >> (b1 & 31)) & (P.bloom[b2 >> 5] >> (b2 & 31)) & 1u;
-    const uint32_t c1 = 2 * (h >> 20), c2 = 2 * (h2 >> 20);
-    const uint64_t x0 = P.hot[c1], x1 = P.hot[c1 + 1], y0 = P.hot[c2], y1 = P.hot[c2 + 1];
+    uint32_t f;
+    uint64_t x0, x1, y0, y1;
+    if (t.hot1) {  // one-bucket layout (wave-uniform branch)
+      const uint32_t bw = P.bloom[hot1_word(h2)], bm = hot1_bits(h2);
+      f = (bw & bm) == bm ? 1u : 0u;
+      // (the bucket's two 16-byte halves in swapped order for odd buckets: each of the two reads
+      // then spreads its lanes over both halves' banks)
+      const uint32_t c = hot1_bucket(h), sw = (h >> 20) & 2u;
+      x0 = P.hot[c + sw], x1 = P.hot[c + sw + 1], y0 = P.hot[c + (sw ^ 2u)], y1 = P.hot[c + (sw ^ 2u) + 1];
+    } else {
+      const uint32_t b1 = h & (kBloomBits - 1), b2 = h2 >> 14;
+      f = (P.bloom[b1 >> 5] >> (b1 & 31)) & (P.bloom[b2 >> 5] >> (b2 & 31)) & 1u;
+      const uint32_t c1 = 2 * (h >> 20), c2 = 2 * (h2 >> 20);
+      x0 = P.hot[c1], x1 = P.hot[c1 + 1], y0 = P.hot[c2], y1 = P.hot[c2 + 1];
+    }
     uint32_t v = kNoRank;
     bool hit = false;
     auto chk = [&](uint64_t x) {
@@ -1523,6 +1571,8 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
           for (int k = 0; k < N; k++)
             if ((uint32_t)k < m) out[k] = tk[k];
         }
+        CTOK_CHECK_REC(m >= 1 && m <= n && pos + m <= (uint32_t)kTileSlots && o < (uint32_t)kTileSlots,
+                       "[ctok check] class pass N=%d tile %u: record m=%u n=%u pos=%u ordinal=%u\n", N, tile, m, n, pos, o);
         w.mrec[(size_t)tile * kTileSlots + o] = rec_short(m, pos);
         st_bytes += n;
         st_ids += m;
@@ -1626,157 +1676,9 @@ __device__ __forceinline__ void class_pass(const Work& w, const Tables& t, const
   __syncthreads();
 }
 
-#ifdef CTOK_SHORT_LG
-// A/B variant (-DCTOK_SHORT_LG): a lane group of G lanes per piece (G = 8 for
-// <= 8 B, 16 for 9..16 B pieces; 64 / G pieces per wave): lane i holds the piece's token at
-// position i (positions fixed, a live mask) and the rank of the pair it starts; a merge is the
-// group's minimum (rank << 4 | position) by DPP, the right token's lane dies, and the two new
-// pairs are looked up by the two lanes that start them (one probe each, in flight together).
-// Narrow compact tables only; semantics of src/bpe.rs:88-153 as merge_slots'.
-template <int G>
-__device__ __forceinline__ uint32_t group_min(uint32_t v) {
-  static_assert(G == 8 || G == 16, "groups of 8 or 16 lanes (within a DPP row)");
-  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0xB1, 0xF, 0xF, false));   // lane ^ 1
-  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x4E, 0xF, 0xF, false));   // lane ^ 2
-  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x141, 0xF, 0xF, false));  // row_half_mirror
-  if constexpr (G == 16)
-    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x140, 0xF, 0xF, false));  // row_mirror
-  return v;
-}
-
-template <int G, bool COMPACT, uint32_t NT, uint32_t SORTCAP, int KT, typename Load>
-__device__ __forceinline__ void lg_pass(const Work& w, const Tables& t, const PairLds& P, const int32_t* s_b2id,
-                                        PassLds<SORTCAP, KT>& S, bool& loaded, Load&& load) {
-  using LC = LdsClass<G>;
-  constexpr int K = KT;
-  constexpr uint32_t PPW = 64 / G;  // pieces per wave per block
-  const uint32_t tid = threadIdx.x, lane = tid & 63;
-  const uint32_t li = lane % G, gbase = lane - li, gi = lane / G;
-  constexpr uint32_t gmask = G == 16 ? 0xFFFFu : 0xFFu;
-  uint32_t* err = &w.counters[2];
-  const uint32_t* list = class_list<G>(w);
-  const uint32_t cap = class_cap<G>(w);
-  const uint32_t* counts = w.tcls + (size_t)LC::cls * w.n_tiles;
-  uint32_t st_bytes = 0, st_ids = 0;
-  if (tid < 2) S.stat[tid] = 0;
-  __syncthreads();
-  uint32_t take = 1;
-  const uint32_t U = w.unit;
-  for (;;) {
-    if (tid == 0) {
-      S.chunk = atomicAdd(&w.counters[ctr_chunk(LC::cls)], take);
-      S.take = take;
-      S.next = 0;
-    }
-    __syncthreads();
-    const uint32_t c0 = S.chunk * U;
-    if (c0 >= w.n_tiles) break;
-    const uint32_t tb1 = min(w.n_tiles, c0 + U * S.take);
-    const uint32_t E = tile_share_init<K>(counts, tb1, c0, S.pre, S.tsum, w.tregion, LC::cls, S.tbase);
-    if (E && !loaded) {
-      load();
-      loaded = true;
-      __syncthreads();
-    }
-    for (;;) {  // blocks of PPW entries per wave (wave-uniform)
-      uint32_t b = 0;
-      if (lane == 0) b = atomicAdd(&S.next, PPW);
-      b = uni((uint32_t)__shfl((int)b, 0, 64));
-      if (b >= E) break;
-      const uint32_t q = b + gi;
-      const bool valid = q < E;
-      uint32_t kt = 0, e = 0;
-      if (valid) {
-        kt = tile_of<K>(S.pre, q);
-        e = list[(size_t)(c0 + kt) * cap + (q - S.pre[kt])];
-      }
-      const uint32_t tile = c0 + kt;
-      const uint32_t s = tile * kTile + (e & 0xFFFu);
-      const uint32_t n = valid ? ent_len(e) : 0u;
-      const uint32_t by = li < n ? (uint32_t)w.text[s + li] : 0u;
-      const uint32_t bn = dpp_next(by);  // the next position's byte (lane li + 1 of the group)
-      const int32_t id = s_b2id[by];
-      const uint64_t miss = __ballot(li < n && id < 0);
-      const bool missing = ((miss >> gbase) & gmask) != 0;
-      if (missing && li == 0) {  // a byte char absent from the vocab: the generic pass
-        const uint32_t mi = atomicAdd(&w.counters[4], 1u);
-        if (mi < w.mid_cap)
-          w.mid_list[mi] = (uint64_t)s | ((uint64_t)ent_ord(e) << 32) | ((uint64_t)n << 48);
-        else
-          atomicOr(&w.counters[kCtrOverflow], 1u);
-      }
-      bool live = !missing && li < n;
-      uint32_t tok = (uint32_t)id & 0xFFFFu;
-      uint32_t rk = kNoRank;
-      if (live && li + 1 < n) {
-        rk = t.pair0[(by << 8) | bn];
-        if (rk != kNoRank && value_panics(t, rk)) {
-          atomicOr(err, kErrPanic);
-          rk = kNoRank;
-        }
-      }
-      for (;;) {
-        const uint32_t key = (live && rk != kNoRank) ? (rk << 4) | li : ~0u;
-        const uint32_t gmin = group_min<G>(key);
-        if (__ballot(gmin != ~0u) == 0) break;  // (wave-uniform)
-        const bool act = gmin != ~0u;
-        const uint32_t bi = gmin & 15u, r = gmin >> 4;
-        const uint32_t nid = (COMPACT ? r : t.rank_newid[r]) & 0xFFFFu;
-        const uint32_t lvm = (uint32_t)(__ballot(live) >> gbase) & gmask;
-        const uint32_t p = bi + 1 + (uint32_t)__builtin_ctz((lvm | (1u << G)) >> (bi + 1));  // the right token
-        const uint32_t qn = p + 1 + (uint32_t)__builtin_ctz((lvm | (1u << G)) >> (p + 1));  // the one after it
-        const bool has_r = qn < (uint32_t)G;
-        const uint32_t lo = lvm & ((1u << bi) - 1u);
-        const uint32_t pv = 31u - (uint32_t)__builtin_clz(lo | 1u);
-        const uint32_t tq = (uint32_t)__shfl((int)tok, (int)(gbase + min(qn, (uint32_t)G - 1)), 64);
-        const bool am_bi = act && li == bi, am_pv = act && lo != 0 && li == pv;
-        Probe<true, true> pr;
-        pr.start(t, P, am_bi ? nid : tok, am_bi ? tq : nid, (am_bi && has_r) || am_pv);
-        const uint32_t rr = pr.finish(t, err);
-        if (am_bi) {
-          tok = nid;
-          rk = has_r ? rr : kNoRank;
-        }
-        if (am_pv) rk = rr;
-        if (act && li == p) live = false;
-      }
-      // the group's ids, in position order, to the tile's region; the record
-      const uint32_t lvm = (uint32_t)(__ballot(live) >> gbase) & gmask;
-      const uint32_t m = (uint32_t)__popc(lvm);
-      uint32_t pos = 0;
-      const bool done = valid && !missing;
-      if (done && li == 0) pos = atomicAdd(&S.tsum[kt], m);
-      pos = (uint32_t)__shfl((int)pos, (int)gbase, 64);
-      if (done && live) w.scratch[(size_t)tile * kTileSlots + pos + __popc(lvm & ((1u << li) - 1u))] = tok;
-      if (done && li == 0) {
-        w.mrec[(size_t)tile * kTileSlots + ent_ord(e)] = rec_short(m, pos);
-        st_bytes += n;
-        st_ids += m;
-      }
-    }
-    tile_share_flush<K>(w, c0, tb1, S.tsum, S.tbase, LC::cls);
-    const uint32_t units = (w.n_tiles + U - 1) / U, next = S.chunk + S.take;
-    const uint32_t share = next < units ? (units - next) / gridDim.x : 0u;
-    take = min(min((uint32_t)K / U, max(1u, share)), 64u);
-    __syncthreads();
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    st_bytes += (uint32_t)__shfl_xor((int)st_bytes, o, 64);
-    st_ids += (uint32_t)__shfl_xor((int)st_ids, o, 64);
-  }
-  if ((tid & 63) == 0) {
-    atomicAdd(&S.stat[0], st_bytes);
-    atomicAdd(&S.stat[1], st_ids);
-  }
-  __syncthreads();
-  if (tid == 0) {
-    atomicAdd(&w.counters[ctr_stat(LC::cls)], S.stat[0]);
-    atomicAdd(&w.counters[ctr_stat(LC::cls) + 1], S.stat[1]);
-  }
-  __syncthreads();
-}
-#endif
+// (Round 5 also built a lane-group variant of this pass -- 8 / 16 lanes per piece, -DCTOK_SHORT_LG:
+// 4.3x slower, VALU-issue bound; DESIGN.md 4.2.  It is kept out of this file as
+// profiles/r05/patches/short_lane_group.diff.)
 
 // Pieces of <= 16 bytes (classes 0 and 1): one workgroup per CU holding the whole LDS image
 // (hot table + Bloom filter); a workgroup moves on to class 1 as soon as class 0 has no chunk
@@ -1819,19 +1721,15 @@ __global__ __launch_bounds__(1024) void k_bpe_short(Work w, Tables t, uint32_t p
   const PairLds P{(const lds_u64*)s_img, (const lds_u32*)(s_img + kHotBuckets)};
   lds_u32* sk = (lds_u32*)s_key;
   lds_u16* st = (lds_u16*)s_tok;
-#ifdef CTOK_SHORT_LG
-  if constexpr (NARROW) {
-    lg_pass<8, COMPACT, NT, ShortCfg<NARROW>::SORTCAP, kShortKT>(w, t, P, s_b2id, S, loaded, load);
-    lg_pass<16, COMPACT, NT, ShortCfg<NARROW>::SORTCAP, kShortKT>(w, t, P, s_b2id, S, loaded, load);
-    return;
-  }
-#endif
+  WgRec rec;
+  rec.begin(w.wgrec, 0);
   // passes: bit 0 the <= 8 B class, bit 1 the 9..16 B class (both, except in the timing A/B
   // CTOK_DBG_MODE=30, which launches them as two kernels to time them apart)
   if (passes & 1u)
     class_pass<8, COMPACT, true, NT, ShortCfg<NARROW>::SORTCAP, NARROW, kShortKT>(w, t, P, s_b2id, S, loaded, load, sk, st);
   if (passes & 2u)
     class_pass<16, COMPACT, true, NT, ShortCfg<NARROW>::SORTCAP, NARROW, kShortKT>(w, t, P, s_b2id, S, loaded, load, sk, st);
+  rec.end(loaded ? 1u : 0u);
 }
 
 // Pieces of 17..32 bytes (CLS = 2, on the main stream after k_bpe_short) or 33..64 bytes (CLS = 3,
@@ -1861,14 +1759,16 @@ __global__ __launch_bounds__(NT) void k_bpe_mid(Work w, Tables t) {
   __shared__ uint16_t s_tok[NARROW ? 8 * NT : 1];
   // (the image is loaded up front: a lazy load pushes the 64-slot pass into scratch; the kernel
   // returns at once when k_segment found no piece of its class)
-  if (w.counters[CLS == 2 ? kCtrAnyMid : kCtrAnyC3] == 0) return;
+  WgRec rec;
+  rec.begin(w.wgrec, CLS == 2 ? 1 : 2);
+  if (w.counters[CLS == 2 ? kCtrAnyMid : kCtrAnyC3] == 0) { rec.end(0); return; }
   // every chunk already taken (the other instance of class 3 got there first): one read for the
   // whole workgroup, so its waves leave together (a wave that stayed would find thread 0 gone)
   __shared__ uint32_t s_left;
   if (threadIdx.x == 0)
     s_left = (uint64_t)__atomic_load_n(&w.counters[ctr_chunk(CLS)], __ATOMIC_RELAXED) * w.unit < w.n_tiles;
   __syncthreads();
-  if (!s_left) return;
+  if (!s_left) { rec.end(0); return; }
   const uint32_t tid = threadIdx.x;
   const uint4* img = NARROW ? t.lds16_image : t.lds_image;
   for (uint32_t i = tid; i < kLdsImageBytes / 16; i += NT) s_img[i] = img[i];
@@ -1877,6 +1777,7 @@ __global__ __launch_bounds__(NT) void k_bpe_mid(Work w, Tables t) {
   const PairLds P{(const lds_u64*)s_img, (const lds_u32*)(s_img + kHotBuckets)};
   class_pass<CLS == 2 ? 32 : 64, COMPACT, true, NT, kSortCap, NARROW, KT>(w, t, P, s_b2id, S, loaded, [] {},
                                                                          (lds_u32*)s_key, (lds_u16*)s_tok);
+  rec.end(1);
 }
 
 // hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device): the attribute is set
@@ -1924,7 +1825,8 @@ static hipError_t launch_short_t(const Work& w, const Tables& t, hipStream_t s) 
   static LdsAttr attr;
   HIPCHK(lds_attr_once(attr, (const void*)k_bpe_short<C, NW>, kLdsImageBytes));
   if (!w.n_tiles) return hipSuccess;
-  const uint32_t grid = min((w.n_tiles + w.unit - 1) / w.unit, w.n_cus);
+  // (Work::short_wgs: fewer workgroups than CUs leave CUs to the side stream's passes from the start)
+  const uint32_t grid = min((w.n_tiles + w.unit - 1) / w.unit, w.short_wgs ? min(w.short_wgs, w.n_cus) : w.n_cus);
   if (t.dbg == 30) {
     k_bpe_short<C, NW><<<grid, ShortCfg<NW>::NT, kLdsImageBytes, s>>>(w, t, 1u);
     k_bpe_short<C, NW><<<grid, ShortCfg<NW>::NT, kLdsImageBytes, s>>>(w, t, 2u);
@@ -3233,6 +3135,8 @@ constexpr int kSparseWaves = 16;  // waves per k_bpe_sparse workgroup (beside th
 template <bool COMPACT, bool NARROW>
 __global__ __launch_bounds__(64 * kSparseWaves) void k_bpe_sparse(Work w, Tables t, uint32_t n) {
   if (spec_failed(w)) return;
+  WgRec rec;
+  rec.begin(w.wgrec, 3);
   extern __shared__ __attribute__((aligned(16))) uint4 s_dyn[];
   __shared__ int32_t s_b2id[256];
   const uint32_t tid = threadIdx.x, lane = tid & 63;
@@ -3275,6 +3179,8 @@ __global__ __launch_bounds__(64 * kSparseWaves) void k_bpe_sparse(Work w, Tables
     if (lane == 0) pos = atomicAdd(&w.rend[3ull * w.n_tiles + tile], m);
     pos = uni(pos);
     if ((lv >> lane) & 1u) w.scratch[(size_t)tile * kTileSlots + pos + __popcll(lv & lanemask_lt())] = tok;
+    CTOK_CHECK_REC(m >= 1 && m <= len && pos + m <= (uint32_t)kTileSlots,
+                   "[ctok check] k_bpe_sparse tile %u: record m=%u n=%u pos=%u\n", tile, m, len, pos);
     if (lane == 0) {
       w.mrec[(size_t)tile * kTileSlots + o] = rec_short(m, pos);
       atomicAdd(&w.tile_tok[tile], m);
@@ -3286,6 +3192,8 @@ __global__ __launch_bounds__(64 * kSparseWaves) void k_bpe_sparse(Work w, Tables
     atomicAdd(&w.counters[ctr_stat(3)], st_bytes);
     atomicAdd(&w.counters[ctr_stat(3) + 1], st_ids);
   }
+  __syncthreads();
+  rec.end(1);
 }
 
 hipError_t launch_c3_list(const Work& w, hipStream_t s) {
@@ -3458,6 +3366,20 @@ __global__ __launch_bounds__(64 * kEmitWaves) void k_emit(Work w, uint32_t* __re
       sp[k] = src0 + (merged ? (v >> 16) & 0xFFFu : 0u);
       lng |= merged && (v & kRecLong);
     }
+#ifdef CTOK_CHECK
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint32_t v = mv[k];
+      if (j0 + k < np && cur.rec(k) == kMerged) {
+        if (v & kRecLong)
+          CTOK_CHECK_REC((v & kRecLongMask) < long_count(w), "[ctok check] k_emit tile %u piece %u: long record %08x past %u\n",
+                         tile, j0 + k, v, long_count(w));
+        else
+          CTOK_CHECK_REC((v & 0xFFFFu) <= (uint32_t)kMedMax && ((v >> 16) & 0xFFFu) + (v & 0xFFFFu) <= (uint32_t)kTileSlots,
+                         "[ctok check] k_emit tile %u piece %u: merged record %08x out of range\n", tile, j0 + k, v);
+      }
+    }
+#endif
     if (__ballot(lng)) {
 #pragma unroll
       for (int k = 0; k < 4; k++) {

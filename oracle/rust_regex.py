@@ -125,11 +125,10 @@ def rejects(p: str) -> str:
                         return why
                     continue
                 if d == "[" and p[j + 1:j + 2] == ":":
+                    # a known [:name:] is an ASCII class; any other name makes regex-syntax
+                    # (maybe_parse_ascii_class) backtrack and read the '[' as a nested class
                     e = p.find(":]", j + 2)
-                    if e >= 0:
-                        nm = p[j + 2:e].lstrip("^")
-                        if nm not in _ASCII_CLASSES:
-                            return "unknown ASCII class [:%s:]" % nm
+                    if e >= 0 and p[j + 2:e].lstrip("^") in _ASCII_CLASSES:
                         j = e + 2
                         continue
                 if d == "[":
@@ -159,7 +158,7 @@ def rejects(p: str) -> str:
                     return "atomic group (?>"
                 if rest.startswith("P="):
                     return "named backreference (?P="
-                if rest.startswith(("|", "#", "(", "'", "&", "R", "+", "0")) or (rest[:1].isascii() and rest[:1].isdigit()):
+                if rest.startswith(("|", "#", "(", "'", "&", "+", "0")) or (rest[:1].isascii() and rest[:1].isdigit()):
                     return "unsupported group (?" + rest[:1]
                 if rest.startswith(("P<", "<")):
                     k = i + 2 + (2 if rest.startswith("P<") else 1)
@@ -212,6 +211,8 @@ def rejects(p: str) -> str:
             if body is not None and a.isascii() and a.isdigit() and (not b or b.isascii() and b.isdigit()):
                 if empty[-1]:
                     return "repetition operator missing expression"
+                if int(a) > 0xFFFFFFFF or (b and int(b) > 0xFFFFFFFF):  # a u32 (regex-syntax parse_decimal)
+                    return "repetition count overflows u32 {%s}" % body
                 if b and int(b) < int(a):
                     return "invalid repetition range {%s}" % body
                 i = e + 1

@@ -182,7 +182,11 @@ SPLIT_PATTERNS = [
     ("\\p{Foo}+", False), ("\\p{sc=Nope}", False), ("\\p{InBasicLatin}", False),  # unknown \p names
     ("a\\Z", False), ("\\Ga", False),          # escapes the crate does not have
     ("*a", False), ("a|+b", False), ("(?:*)", False), ("a{3,2}", False),  # nothing to repeat, bad range
-    ("[[:foo:]]", False),                    # unknown ASCII class
+    ("[[:foo:]]", True),                     # unknown [:name:]: a nested class of ':', 'f', 'o' (regex-syntax backtracks)
+    ("[[:^bar:]x]", True),
+    ("(?R)a", True), ("(?Rm:a)b", True),      # R: the CRLF-mode flag (regex >= 1.8)
+    ("a{99999999999999999999}", False),      # a count past u32: invalid decimal
+    ("a{2,4294967296}", False),
     ("(ab", False), ("ab)", False), ("[ab", False),  # unbalanced
     ("[(?=]x", True),                        # '(?=' inside a character class is literal
     ("\\(?=x", True),                        # escaped '(' : a literal paren, then an optional '='
