@@ -346,16 +346,19 @@ def main():
     st = stats[-1]
     P, T, B, D = st["pieces"], st["tokens"], st["bytes_norm"], st["docs"]
     # Per-kernel rooflines (HIP events on the encode stream, averaged over the timed steps).
-    # Algorithmic bytes per launch:
-    #   k_segment:      text read (B) + piece-start bitmap written (B/8) + document offsets read (8 B per doc)
-    #   k_bpe_short:    text bytes of the <= 16 B pieces left to merge + 4 B per id written
-    #   k_bpe_mid<2>:   the same for the 17..32 B pieces (33..64 B: k_bpe_mid<3>, main + side stream)
+    # Algorithmic bytes per launch, SURVEY.md 8(d)'s terms only (implementation
+    # traffic -- bitmaps, lists, records, scratch ids, tables -- is not counted):
+    #   k_segment:      the text (B) + the input document offsets (8 B per offset)
+    #   k_bpe_short:    the text bytes of the <= 16 B pieces left to merge + 4 B per id they become
+    #   k_bpe_mid<2>:   the same for the 17..32 B pieces
+    #   k_emit:         the output ids (4 B each) + the output offsets (8 B each; with the tile scan
+    #                   and k_tokoff)
     cb, ci = st["class_bytes"], st["class_ids"]
     kernels = {
-        "k_segment": (avg("ms_segment"), 1.125 * B + 8 * D),
+        "k_segment": (avg("ms_segment"), B + 8 * (D + 1)),
         "k_bpe_short": (avg("ms_bpe_lo"), cb[0] + cb[1] + 4 * (ci[0] + ci[1])),
         "k_bpe_mid": (avg("ms_bpe_hi"), cb[2] + 4 * ci[2]),
-        "k_emit": (avg("ms_emit"), 8 * T + 16 * (D + 1)),  # + tile scan, k_tokoff: ids read + written, offsets
+        "k_emit": (avg("ms_emit"), 4 * T + 8 * (D + 1)),
     }
     dom = max(kernels, key=lambda k: kernels[k][0])
     ms_dom, alg_dom = kernels[dom]
@@ -396,7 +399,9 @@ def main():
                 per = tr.get("hbm_bytes_per_launch", {})
                 hits = [v for k, v in per.items() if k.split("<")[0] == dom]
                 traffic = hits[0] if len(hits) == 1 else None
-                traffic_src = "profiles/pmc_traffic.json (FETCH_SIZE x2 + WRITE_SIZE, libctok.so sha256 %s)" % lib_sha[:12]
+                traffic_src = ("profiles/pmc_traffic.json (FETCH_SIZE x %s + WRITE_SIZE x 1, libctok.so sha256 %s; factors "
+                               "calibrated in %s: reads beyond L2, Infinity-Cache hits included)" % (
+                                   tr.get("fetch_correction"), lib_sha[:12], tr.get("calibration", "uncalibrated")))
         ms_step = elapsed_max / args.steps * 1e3
         cfg = dict(desc)
         cfg.update({"docs_per_gpu": n_docs, "bytes_per_gpu": n_bytes, "tokens_per_gpu": int(T),

@@ -3251,7 +3251,10 @@ struct EmitRecs {
 template <typename RT>
 __global__ __launch_bounds__(64 * kEmitWaves) void k_emit(Work w, uint32_t* __restrict__ ids, uint64_t ids_cap,
                                                          uint64_t* __restrict__ tok_off) {
-  if (spec_failed(w)) return;
+  // (a lean list overflowed: some pieces were never listed, so their merged records were never
+  // written -- the host runs the call again with the safe capacities, and this pass must not
+  // gather through records no pass wrote)
+  if (spec_failed(w) || uni(w.counters[kCtrOverflow]) != 0) return;
   constexpr uint32_t kMerged = sizeof(RT) == 2 ? kRecMerged16 : kRecMerged32;
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t tile = uni(blockIdx.x * kEmitWaves + (threadIdx.x >> 6));

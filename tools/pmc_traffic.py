@@ -8,11 +8,16 @@ Usage: python tools/pmc_traffic.py FETCH_DIR WRITE_DIR OUT.json [WORKLOAD]
   WRITE_DIR: output of `rocprofv3 --pmc WRITE_SIZE ...`
 
 FETCH_SIZE / WRITE_SIZE are rocprofv3's derived counters in KiB per dispatch (TCC_EA0 read /
-write requests x 64 B, memory side of the L2).  MI355X_MICROARCH.md: on gfx950 FETCH_SIZE
-reports exactly half the bytes of a wide (16 B/lane) coalesced streaming read; the correction
-applied here is x2 on FETCH_SIZE (the dominant reads of k_segment are 16 B/lane), WRITE_SIZE
-as reported.  Other access widths are uncalibrated, so `hbm_bytes_per_launch` is an estimate
-with that stated correction; the raw KiB values are kept beside it.
+write requests, memory side of the L2).  Calibrated on known byte counts in this path's own access
+shapes (tools/fetch_calib.hip, tools/pmc_calib.sh -> profiles/r06/fetch_calibration.txt): every L2
+read request moves a 128-B line and is tallied at 64 B -- known bytes / FETCH_SIZE = 2.00 for 16-B
+streaming loads, 2.00 for 4-B gathers of one dword per line, 1.97 for two dwords per line (one
+request per line), 1.92 for the merge passes' text-word loads, 56 B tallied per 8-B probe of a
+32 MiB table (0.875 requests: L2 misses served by the Infinity Cache, which FETCH counts);
+WRITE_SIZE is exact for 16-B and consecutive 4-B stores and tallies 32 B per scattered 4-B store
+(one 32-B write request each).  So `hbm_bytes_per_launch` = 2 x FETCH + WRITE is the bytes moved
+beyond the L2 (Infinity-Cache hits included: an upper bound of the HBM bytes); the raw KiB values
+are kept beside it.
 """
 import csv
 import glob
@@ -49,7 +54,9 @@ def main():
         lib_sha = hashlib.sha256(fh.read()).hexdigest()
     res = {"unit": "bytes per launch", "fetch_correction": 2.0, "workload": workload,
            "lib_sha256": lib_sha,  # the profiled library: bench.py reports `traffic` only for this build
-           "note": "FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE, KiB -> bytes",
+           "calibration": "profiles/r06/fetch_calibration.txt",
+           "note": "FETCH_SIZE x2 (calibrated: 128-B read requests tallied at 64 B) + WRITE_SIZE (exact request "
+                   "bytes), KiB -> bytes; bytes moved beyond the L2, Infinity-Cache hits included",
            "fetch_kib": f, "write_kib": w, "hbm_bytes_per_launch": {}}
     for k in sorted(set(f) | set(w)):
         res["hbm_bytes_per_launch"][k] = int((2.0 * f.get(k, 0.0) + w.get(k, 0.0)) * 1024)
