@@ -88,7 +88,7 @@ def _pin_chunk(docs):
     return _PIN["py"].encode_batch(docs)
 
 
-def ref_py_packed(obj, docs, workers=6):
+def ref_py_packed(obj, docs, workers=7):
     """ref_py over `docs` on a pool of worker processes (the Python restatement is slow: ~1.5 ms per
     C5 document); (ids, tok_off) packed like the C oracle's."""
     import multiprocessing as mp
@@ -106,7 +106,7 @@ def ref_py_packed(obj, docs, workers=6):
 # the first PIN_DOCS documents of each config (>= 100k): ref_py uses the `regex`
 # module and `unicodedata` directly, the C oracle the generated tables of csrc/gen/unicode_data.h,
 # so the pin also covers the tables on the config's text.  Recorded as pin_ref_py in digests.json.
-PIN_DOCS = {"C2": 100_000, "C5": 100_000, "C5NFC": 100_000, "C3": 3000, "C3TT": 3000}
+PIN_DOCS = {"C2": 100_000, "C5": 100_000, "C5NFC": 100_000, "C3": 20_000, "C3TT": 20_000}
 
 
 def big(name):
