@@ -1495,6 +1495,7 @@ DeviceState* device_state(ctok* t, int device) {
   tb.compact = t->compact ? 1 : 0;
   tb.narrow = (t->narrow && !getenv("CTOK_FORCE_WIDE_SLOTS")) ? 1 : 0;
   tb.hot1 = t->hot1 ? 1 : 0;
+  tb.all_bytes = std::all_of(t->byte2id, t->byte2id + 256, [](int32_t v) { return v >= 0; }) ? 1 : 0;
   tb.dbg = getenv("CTOK_DBG_MODE") ? (uint32_t)atoi(getenv("CTOK_DBG_MODE")) : 0;
   DeviceState* r = ds.get();
   t->devs[device] = std::move(ds);
@@ -1728,7 +1729,7 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   ds->long_ord.ensure(w.long_cap + 8);
   ds->long_hist.ensure(kLhWords);
   ds->mid_list.ensure(w.mid_cap + 8);
-  ds->scan_tmp.ensure(scan_tmp_elems(std::max<uint64_t>(nt + 1, n_docs + 1)) + 64);
+  ds->scan_tmp.ensure(std::max(scan_tmp_elems(std::max<uint64_t>(nt + 1, n_docs + 1)), tile_scan_tmp_elems(nt)) + 64);
   w.tfirst = ds->tfirst.p;
   w.pbits = ds->pbits.p;
   w.wpref = ds->wpref.p;

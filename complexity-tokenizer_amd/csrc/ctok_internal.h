@@ -225,6 +225,7 @@ struct Tables {            // device pointers, owned by the host runtime
   uint32_t narrow;          // 1: every vocab id < 2^16 (the merge passes keep the last tier's tokens as u16 in LDS)
   uint32_t dbg;             // debug mode (CTOK_DBG_MODE), 0 in production
   uint32_t hot1;            // 1: the narrow image in the one-bucket layout (hot1_bucket / hot1_word)
+  uint32_t all_bytes;       // 1: every byte's char is in the vocab (no piece can have a dropped byte)
 };
 
 struct Work {              // device pointers, sized by the host for one call
@@ -399,6 +400,7 @@ hipError_t scan_u32(const uint32_t* in, uint32_t* out, uint64_t n_max, const uin
                     uint32_t* tmp, uint64_t tmp_cap, hipStream_t s);
 hipError_t scan_u64(uint64_t* inout, uint64_t n, uint64_t* tmp, uint64_t tmp_cap, hipStream_t s);
 uint64_t scan_tmp_elems(uint64_t n_max);
+uint64_t tile_scan_tmp_elems(uint64_t n_tiles);  // scan_tmp (u64) that scan_tiles needs
 hipError_t shift_u64(uint64_t* p, uint64_t n, uint64_t delta, hipStream_t s);  // p[0, n) += delta
 // NFC splice (see kernels.hip): len[d] = flagged doc d's bytes (else 0); flagged docs' bytes
 // gathered to the sub-batch; the output's counts, offsets (out_off[0..n_docs]) and ids

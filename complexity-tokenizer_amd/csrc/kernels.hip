@@ -1849,7 +1849,8 @@ hipError_t launch_bpe_class(const Work& w, const Tables& t, int cls, hipStream_t
     case 0: return t.compact ? launch_short<true>(w, t, s) : launch_short<false>(w, t, s);  // classes 0 and 1
     case 2: return t.compact ? launch_mid<true, 2>(w, t, s) : launch_mid<false, 2>(w, t, s);
     case 4: return t.compact ? launch_mid<true, 3>(w, t, s) : launch_mid<false, 3>(w, t, s);  // main-stream instance
-    case 3:  // pieces with dropped bytes, found by the merge passes
+    case 3:  // pieces with dropped bytes, found by the merge passes (none when every byte's char is in the vocab)
+      if (t.all_bytes) return hipSuccess;
       k_bpe_generic<true><<<64, 128, 0, s>>>(w, t);
       return hipGetLastError();
     default:
@@ -3654,16 +3655,22 @@ uint64_t scan_tmp_elems(uint64_t n_max) {
 // and documents of a call are < 2^32), so the low half never carries into the high one.
 // Reduce, scan of the block partials, apply: 3 launches (1 for <= 4096 tiles) instead of 8 (and
 // the apply sums the pieces for the statistics, which took a launch of its own).
+// The tile scan's blocks: 1024 tiles (4 per thread), so that a call of a few tens of thousands of
+// tiles (a 160 MB shard: 40k) spreads its reduce and apply over tens of workgroups instead of ten
+// (its 3 launches took 23 us there with 4096-tile blocks)
+constexpr int kTileScanPer = 4;
+constexpr int kTileScanBlock = 256 * kTileScanPer;
+
 __device__ __forceinline__ uint64_t tile_pair(const Work& w, uint64_t i) {
   return i < w.n_tiles ? (uint64_t)w.tile_tok[i] | ((uint64_t)w.tile_doc[i] << 32) : 0ull;
 }
 
 __global__ __launch_bounds__(256) void k_tiles_reduce(Work w, uint64_t* __restrict__ part) {
   __shared__ uint64_t s_scan[17];
-  const uint64_t b0 = (uint64_t)blockIdx.x * kScanBlock + threadIdx.x * kScanPer;
+  const uint64_t b0 = (uint64_t)blockIdx.x * kTileScanBlock + threadIdx.x * kTileScanPer;
   uint64_t v = 0;
 #pragma unroll
-  for (int k = 0; k < kScanPer; k++) v += tile_pair(w, b0 + k);
+  for (int k = 0; k < kTileScanPer; k++) v += tile_pair(w, b0 + k);
   uint64_t total;
   block_excl_scan<uint64_t>(v, s_scan, &total);
   if (threadIdx.x == 0) part[blockIdx.x] = total;
@@ -3673,11 +3680,11 @@ __global__ __launch_bounds__(256) void k_tiles_reduce(Work w, uint64_t* __restri
 __global__ __launch_bounds__(256) void k_tiles_apply(Work w, const uint64_t* __restrict__ part_scanned, uint32_t count) {
   __shared__ uint64_t s_scan[17];
   const uint64_t n = w.n_tiles;
-  const uint64_t b0 = (uint64_t)blockIdx.x * kScanBlock + threadIdx.x * kScanPer;
-  uint64_t v[kScanPer];
+  const uint64_t b0 = (uint64_t)blockIdx.x * kTileScanBlock + threadIdx.x * kTileScanPer;
+  uint64_t v[kTileScanPer];
   uint64_t sum = 0;
 #pragma unroll
-  for (int k = 0; k < kScanPer; k++) {
+  for (int k = 0; k < kTileScanPer; k++) {
     v[k] = tile_pair(w, b0 + k);
     sum += v[k];
   }
@@ -3686,7 +3693,7 @@ __global__ __launch_bounds__(256) void k_tiles_apply(Work w, const uint64_t* __r
   const uint64_t base = part_scanned ? part_scanned[blockIdx.x] : 0ull;
   ex += base;
 #pragma unroll
-  for (int k = 0; k < kScanPer; k++) {
+  for (int k = 0; k < kTileScanPer; k++) {
     const uint64_t i = b0 + k;
     if (i < n) {
       w.tile_tok[i] = (uint32_t)ex;
@@ -3697,7 +3704,7 @@ __global__ __launch_bounds__(256) void k_tiles_apply(Work w, const uint64_t* __r
   if (count) {
     uint32_t c = 0;
 #pragma unroll
-    for (int k = 0; k < kScanPer; k++)
+    for (int k = 0; k < kTileScanPer; k++)
       if (b0 + k < n) c += w.tile_np[b0 + k];
     c = wave_sum_full_u32(c);
     if ((threadIdx.x & 63) == 0 && c) atomicAdd(&w.counters[5], c);  // (counters are zeroed per call)
@@ -3708,8 +3715,13 @@ __global__ __launch_bounds__(256) void k_tiles_apply(Work w, const uint64_t* __r
   }
 }
 
+uint64_t tile_scan_tmp_elems(uint64_t n_tiles) {
+  const uint64_t nb = (n_tiles + kTileScanBlock - 1) / kTileScanBlock;
+  return nb + 1 + scan_tmp_elems(nb + 1);
+}
+
 hipError_t scan_tiles(const Work& w, hipStream_t s, bool count) {
-  const uint64_t nb = ((uint64_t)w.n_tiles + kScanBlock - 1) / kScanBlock;
+  const uint64_t nb = ((uint64_t)w.n_tiles + kTileScanBlock - 1) / kTileScanBlock;
   if (nb <= 1) {
     k_tiles_apply<<<1, 256, 0, s>>>(w, nullptr, count ? 1u : 0u);
     return hipGetLastError();
