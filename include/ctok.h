@@ -133,7 +133,7 @@ typedef struct ctok_stats {
                                                           of those NFC changes: flagged per 64-byte word) */
   double ms_segment;      /* k_segment alone: piece starts + whole-piece probes/routing */
   double ms_bpe_lo;       /* k_bpe_short: pieces of <= 16 bytes (classes 0 and 1)        */
-  double ms_bpe_hi;       /* k_bpe_mid<2>: pieces of 17..32 bytes                        */
+  double ms_bpe_hi;       /* k_bpe_mid<2>: pieces of 17..32 bytes (on the side stream: the time it adds after k_bpe_short) */
   uint64_t class_bytes[4];  /* text bytes merged per length class (<= 8, 9..16, 17..32, 33..64 B) */
   uint64_t class_ids[4];    /* ids produced per length class                             */
   double ms_bpe_med;      /* k_bpe_mid<3>, main-stream instance: pieces of 33..64 bytes    */
