@@ -225,7 +225,7 @@ struct DeviceState {
   hipEvent_t ev[12] = {};
   hipEvent_t ev_sync = nullptr;   // spin-waited completion marker (no blocking-wait wakeup latency)
   hipStream_t side = nullptr;     // long-piece pass, overlapped with the short merge passes
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_cnt = nullptr, ev_done = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_cnt = nullptr;
   uint64_t* host = nullptr;       // pinned host words for small device->host readbacks
   uint64_t* host_dev = nullptr;   // the same words as a device pointer (k_tokoff writes the results there)
   // tables
@@ -308,7 +308,6 @@ struct DeviceState {
       if (ev_sync) (void)hipEventDestroy(ev_sync);
       if (ev_fork) (void)hipEventDestroy(ev_fork);
       if (ev_join) (void)hipEventDestroy(ev_join);
-      if (ev_done) (void)hipEventDestroy(ev_done);
       if (ev_cnt) (void)hipEventDestroy(ev_cnt);
       if (side) (void)hipStreamDestroy(side);
       if (host) (void)hipHostFree(host);
@@ -1414,7 +1413,6 @@ DeviceState* device_state(ctok* t, int device) {
   HIPTRY(hipEventCreateWithFlags(&ds->ev_sync, hipEventDisableTiming));
   HIPTRY(hipEventCreateWithFlags(&ds->ev_fork, hipEventDisableTiming));
   HIPTRY(hipEventCreateWithFlags(&ds->ev_join, hipEventDisableTiming));
-  HIPTRY(hipEventCreateWithFlags(&ds->ev_done, hipEventDisableTiming));
   HIPTRY(hipEventCreateWithFlags(&ds->ev_cnt, hipEventDisableTiming));
   HIPTRY(hipStreamCreateWithFlags(&ds->side, hipStreamNonBlocking));
   HIPTRY(hipHostMalloc((void**)&ds->host, 4096, hipHostMallocDefault));
@@ -1868,40 +1866,22 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
     }
     STEP("bpe_long", launch_bpe_long(w, tb, ds->side, n_long, seg_cnt[kCtrAnyC3] != 0 && !c3_sparse, any_gmem));
   }
-  // The streams meet before the dropped-byte pass and k_emit.  overlap >= 3 (with the 17..32 B
-  // pass on the side stream): the tail runs on the side stream, which usually finishes its merge
-  // pass last, so the stream that waits is the one whose event is already complete; the
-  // caller's stream then waits for the tail's end (the host spins on the side stream itself)
-  const bool tail_side = mid_side && overlap >= 3;
-  hipStream_t s_tail = tail_side ? ds->side : s;
-  if (tail_side) {
-    HIPTRY(hipEventRecord(ds->ev_join, s));
-    HIPTRY(hipStreamWaitEvent(ds->side, ds->ev_join, 0));
-  } else {
-    HIPTRY(hipEventRecord(ds->ev_join, ds->side));
-    HIPTRY(hipStreamWaitEvent(s, ds->ev_join, 0));
-  }
+  HIPTRY(hipEventRecord(ds->ev_join, ds->side));
+  HIPTRY(hipStreamWaitEvent(s, ds->ev_join, 0));
+  if (timing) HIPTRY(hipEventRecord(ds->ev[5], s));
+  STEP("bpe_dropped", launch_bpe_class(w, tb, 3, s));
+  if (timing) HIPTRY(hipEventRecord(ds->ev[3], s));
   // the token count and the counters: written by k_tokoff straight into the pinned host words
   // (two copy launches fewer at the end of every call), or copied
   static const bool copy_res = getenv("CTOK_COPY_RESULTS") != nullptr;
   w.host_res = copy_res ? nullptr : ds->host_dev;
-  {
-    hipStream_t s = s_tail;
-    if (timing) HIPTRY(hipEventRecord(ds->ev[5], s));
-    STEP("bpe_dropped", launch_bpe_class(w, tb, 3, s));
-    if (timing) HIPTRY(hipEventRecord(ds->ev[3], s));
-    STEP("emit", launch_emit(w, d_ids, ids_cap, d_tok_off, s, st != nullptr, seg_cnt[kCtrEmptyDocs] != 0));
-    if (timing) HIPTRY(hipEventRecord(ds->ev[6], s));
-    if (!w.host_res) {
-      HIPTRY(hipMemcpyAsync(ds->host, d_tok_off + n_docs, 8, hipMemcpyDeviceToHost, s));
-      HIPTRY(hipMemcpyAsync(ds->host + 1, ds->counters.p, kNumCounters * 4, hipMemcpyDeviceToHost, s));
-    }
+  STEP("emit", launch_emit(w, d_ids, ids_cap, d_tok_off, s, st != nullptr, seg_cnt[kCtrEmptyDocs] != 0));
+  if (timing) HIPTRY(hipEventRecord(ds->ev[6], s));
+  if (!w.host_res) {
+    HIPTRY(hipMemcpyAsync(ds->host, d_tok_off + n_docs, 8, hipMemcpyDeviceToHost, s));
+    HIPTRY(hipMemcpyAsync(ds->host + 1, ds->counters.p, kNumCounters * 4, hipMemcpyDeviceToHost, s));
   }
-  if (tail_side) {
-    HIPTRY(hipEventRecord(ds->ev_done, ds->side));
-    HIPTRY(hipStreamWaitEvent(s, ds->ev_done, 0));
-  }
-  spin_sync(ds, s_tail);
+  spin_sync(ds, s);
   uint64_t ntok = ((volatile uint64_t*)ds->host)[0];
   if (w.wgrec) {  // per kernel: workgroups, distinct CUs, start / end spread (us from the first start)
     std::vector<uint64_t> r(kWgRecWords);
