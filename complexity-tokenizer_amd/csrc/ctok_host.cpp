@@ -225,6 +225,9 @@ struct DeviceState {
   hipEvent_t ev[12] = {};
   hipEvent_t ev_sync = nullptr;   // spin-waited completion marker (no blocking-wait wakeup latency)
   hipStream_t side = nullptr;     // long-piece pass, overlapped with the short merge passes
+  hipStream_t side2 = nullptr;    // k_c3_list and its count, beside the side stream's counter copy
+  hipEvent_t ev_c3 = nullptr;     // the class-3 list and its count are complete
+  hipEvent_t ev_tot = nullptr;    // the long pieces' totals are in the host words
   hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_cnt = nullptr;
   uint64_t* host = nullptr;       // pinned host words for small device->host readbacks
   uint64_t* host_dev = nullptr;   // the same words as a device pointer (k_tokoff writes the results there)
@@ -310,6 +313,9 @@ struct DeviceState {
       if (ev_join) (void)hipEventDestroy(ev_join);
       if (ev_cnt) (void)hipEventDestroy(ev_cnt);
       if (side) (void)hipStreamDestroy(side);
+      if (side2) (void)hipStreamDestroy(side2);
+      if (ev_c3) (void)hipEventDestroy(ev_c3);
+      if (ev_tot) (void)hipEventDestroy(ev_tot);
       if (host) (void)hipHostFree(host);
       if (stream) (void)hipStreamDestroy(stream);
     }
@@ -348,7 +354,6 @@ struct ctok {
   bool proper = true;
   bool compact = false;
   bool narrow = false;  // every vocab id < 2^16
-  bool hot1 = false;    // the narrow LDS image in the one-bucket layout (CTOK_HOT1)
   bool ids16 = false;   // every id encode can emit (vocab and added tokens) < 2^16: 16-bit ids on PCIe
   // decode (src/huggingface/mod.rs:710-747): decoder kind, per-id decoded bytes
   int decoder = 1;                  // 1 ByteLevel, 0 raw concatenation (unknown decoder type), -1 unsupported
@@ -1080,26 +1085,7 @@ void load_root(ctok* t, const ctj::Value& root) {
       uint64_t* hot16 = t->lds16_image.data();
       std::fill(hot16, hot16 + kHotU64, kEmpty);
       uint32_t* bloom16 = reinterpret_cast<uint32_t*>(hot16 + kHotU64);
-      // one-bucket layout (hot1, CTOK_HOT1=1; ctok_internal.h): a pair's 4 candidate slots in one
-      // 32-byte bucket, its two Bloom bits in one word
-      t->hot1 = getenv("CTOK_HOT1") != nullptr;
       for (const auto& re : by_rank) {
-        if (!t->hot1) break;
-        const uint64_t e = re.second;
-        const uint32_t a = (uint32_t)((e >> kIdBits) & ((1u << kIdBits) - 1)), b = (uint32_t)(e & ((1u << kIdBits) - 1));
-        const uint32_t h = hash16_h(a, b), g = hash16_g(a, b);
-        uint64_t* slot = nullptr;
-        if (use_hot && re.first < valid_new.size())
-          for (int k = 0; k < 4 && !slot; k++)
-            if (hot16[hot1_bucket(h) + k] == kEmpty) slot = &hot16[hot1_bucket(h) + k];
-        if (slot) {
-          *slot = ((e >> 42) << 32) | key16(a, b);
-          continue;
-        }
-        bloom16[hot1_word(g)] |= hot1_bits(g);
-      }
-      for (const auto& re : by_rank) {
-        if (t->hot1) break;
         const uint64_t e = re.second;
         const uint32_t a = (uint32_t)((e >> kIdBits) & ((1u << kIdBits) - 1)), b = (uint32_t)(e & ((1u << kIdBits) - 1));
         const uint32_t h = hash16_h(a, b), g = hash16_g(a, b);
@@ -1415,6 +1401,9 @@ DeviceState* device_state(ctok* t, int device) {
   HIPTRY(hipEventCreateWithFlags(&ds->ev_join, hipEventDisableTiming));
   HIPTRY(hipEventCreateWithFlags(&ds->ev_cnt, hipEventDisableTiming));
   HIPTRY(hipStreamCreateWithFlags(&ds->side, hipStreamNonBlocking));
+  HIPTRY(hipStreamCreateWithFlags(&ds->side2, hipStreamNonBlocking));
+  HIPTRY(hipEventCreateWithFlags(&ds->ev_c3, hipEventDisableTiming));
+  HIPTRY(hipEventCreateWithFlags(&ds->ev_tot, hipEventDisableTiming));
   HIPTRY(hipHostMalloc((void**)&ds->host, 4096, hipHostMallocDefault));
   HIPTRY(hipHostGetDevicePointer((void**)&ds->host_dev, ds->host, 0));
   hipStream_t s = ds->stream;
@@ -1495,7 +1484,6 @@ DeviceState* device_state(ctok* t, int device) {
   tb.proper = (t->proper && !getenv("CTOK_FORCE_IMPROPER")) ? 1 : 0;
   tb.compact = t->compact ? 1 : 0;
   tb.narrow = (t->narrow && !getenv("CTOK_FORCE_WIDE_SLOTS")) ? 1 : 0;
-  tb.hot1 = t->hot1 ? 1 : 0;
   tb.all_bytes = std::all_of(t->byte2id, t->byte2id + 256, [](int32_t v) { return v >= 0; }) ? 1 : 0;
   tb.dbg = getenv("CTOK_DBG_MODE") ? (uint32_t)atoi(getenv("CTOK_DBG_MODE")) : 0;
   DeviceState* r = ds.get();
@@ -1807,9 +1795,17 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   // main stream's merge passes run; the long-piece tiers are then launched with grids sized for
   // the pieces there are, or not at all (no idle workgroups queued behind the merge passes)
   volatile uint32_t* seg_cnt = (volatile uint32_t*)(ds->host + 64);
-  HIPTRY(launch_c3_list(w, ds->side));  // (no LDS: it runs beside k_bpe_short; its count comes back too)
   HIPTRY(hipMemcpyAsync((void*)seg_cnt, ds->counters.p, kNumCounters * 4, hipMemcpyDeviceToHost, ds->side));
   HIPTRY(hipEventRecord(ds->ev_cnt, ds->side));
+  // the class-3 list on a stream of its own (no LDS: it runs beside k_bpe_short), so that the
+  // counter copy above -- which the long-piece tiers wait for -- is not queued behind it
+  volatile uint32_t* c3_cnt = (volatile uint32_t*)(ds->host + 120);
+  if (w.c3_max) {
+    HIPTRY(hipStreamWaitEvent(ds->side2, ds->ev_fork, 0));
+    HIPTRY(launch_c3_list(w, ds->side2));
+    HIPTRY(hipMemcpyAsync((void*)c3_cnt, ds->counters.p + kCtrC3Count, 4, hipMemcpyDeviceToHost, ds->side2));
+    HIPTRY(hipEventRecord(ds->ev_c3, ds->side2));
+  }
   STEP("bpe_short", launch_bpe_class(w, tb, 0, s));
   if (timing) HIPTRY(hipEventRecord(ds->ev[2], s));
   // k_segment's counters (they arrive while the <= 16 B pass runs, long before it ends): the
@@ -1820,7 +1816,34 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
     if (e != hipErrorNotReady) throw_err(CTOK_E_DEVICE, std::string("hipEventQuery: ") + hipGetErrorString(e));
   }
   w.mid_wide = (seg_cnt[0] == 0 && !getenv("CTOK_MID512")) ? 1u : 0u;
-  const uint32_t c3n = seg_cnt[kCtrC3Count];
+  // long pieces: their lengths, order and places first (side stream, before the host waits for
+  // anything else: the long tiers after them are the side stream's critical path on C5 / C3);
+  // lids / lw are sized from the totals read back below, once the merge passes are launched
+  const bool spec_fail1 = w.nfc_watch == 1 && seg_cnt[12];  // (a failed NFC speculation: nothing to launch)
+  const uint32_t n_long = spec_fail1 ? 0u : std::min<uint32_t>((uint32_t)seg_cnt[0], w.long_cap);
+  volatile uint32_t* tot = (volatile uint32_t*)(ds->host + 96);
+  if (n_long) {
+    ds->long_pos.ensure(n_long + 8);
+    ds->lw_pos.ensure(n_long + 8);
+    ds->lwn.ensure(n_long + 8);
+    ds->scan_tmp2.ensure(scan_tmp_elems(n_long + 1) + 64);
+    w.long_pos = ds->long_pos.p;
+    w.lw_pos = ds->lw_pos.p;
+    STEP("long_prep", launch_long_prep(w, tb, ds->side, n_long, ds->lwn.p, (uint32_t*)ds->scan_tmp2.p,
+                                       ds->scan_tmp2.cap * 2));
+    HIPTRY(hipMemcpyAsync((void*)tot, ds->long_pos.p + n_long, 4, hipMemcpyDeviceToHost, ds->side));
+    HIPTRY(hipMemcpyAsync((void*)(tot + 1), ds->lw_pos.p + n_long, 4, hipMemcpyDeviceToHost, ds->side));
+    HIPTRY(hipEventRecord(ds->ev_tot, ds->side));
+  }
+  uint32_t c3n = 0;
+  if (w.c3_max && seg_cnt[kCtrAnyC3]) {  // (the list's count: it arrives while k_bpe_short runs)
+    for (;;) {
+      const hipError_t e = hipEventQuery(ds->ev_c3);
+      if (e == hipSuccess) break;
+      if (e != hipErrorNotReady) throw_err(CTOK_E_DEVICE, std::string("hipEventQuery: ") + hipGetErrorString(e));
+    }
+    c3n = *c3_cnt;
+  }
   const bool c3_sparse = c3n != 0 && c3n <= w.c3_max;
   // Without long pieces the side stream is idle: the 17..32 B pass (overlap >= 1) and the
   // 33..64 B pass (overlap 2) go there, so their workgroups take the CUs that k_bpe_short's
@@ -1837,27 +1860,19 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   if (timing) HIPTRY(hipEventRecord(ds->ev[4], s_c3));
   {
     hipStream_t s = s_c3;
+    if (c3_sparse) HIPTRY(hipStreamWaitEvent(s, ds->ev_c3, 0));  // (the list: complete long before)
     if (c3_sparse) STEP("bpe_c3_sparse", launch_c3_sparse(w, tb, c3n, s));
     else STEP("bpe_c3", launch_bpe_class(w, tb, 4, s));
   }
   if (timing) HIPTRY(hipEventRecord(ds->ev[9], s_c3));
-  if (!(w.nfc_watch == 1 && seg_cnt[12])) {  // (a failed NFC speculation discards this pass: nothing to launch)
-    const uint32_t n_long = std::min<uint32_t>((uint32_t)seg_cnt[0], w.long_cap);
+  if (!spec_fail1) {
     bool any_gmem = false;  // a long piece for the global-memory tier (its state words reserved)
     if (n_long) {
-      // lengths, order and places of the long pieces, then lids / lw sized from their totals
-      ds->long_pos.ensure(n_long + 8);
-      ds->lw_pos.ensure(n_long + 8);
-      ds->lwn.ensure(n_long + 8);
-      ds->scan_tmp2.ensure(scan_tmp_elems(n_long + 1) + 64);
-      w.long_pos = ds->long_pos.p;
-      w.lw_pos = ds->lw_pos.p;
-      STEP("long_prep", launch_long_prep(w, tb, ds->side, n_long, ds->lwn.p, (uint32_t*)ds->scan_tmp2.p,
-                                         ds->scan_tmp2.cap * 2));
-      volatile uint32_t* tot = (volatile uint32_t*)(ds->host + 96);
-      HIPTRY(hipMemcpyAsync((void*)tot, ds->long_pos.p + n_long, 4, hipMemcpyDeviceToHost, ds->side));
-      HIPTRY(hipMemcpyAsync((void*)(tot + 1), ds->lw_pos.p + n_long, 4, hipMemcpyDeviceToHost, ds->side));
-      spin_sync(ds, ds->side);
+      for (;;) {  // the long pieces' totals (launch_long_prep above)
+        const hipError_t e = hipEventQuery(ds->ev_tot);
+        if (e == hipSuccess) break;
+        if (e != hipErrorNotReady) throw_err(CTOK_E_DEVICE, std::string("hipEventQuery: ") + hipGetErrorString(e));
+      }
       any_gmem = tot[1] != 0;
       ds->lids.ensure((uint64_t)tot[0] + 64);
       ds->lw.ensure(4 * (uint64_t)tot[1] + 64);

@@ -143,13 +143,6 @@ __host__ __device__ inline uint32_t hash16_h(uint32_t a, uint32_t b) {
 __host__ __device__ inline uint32_t hash16_g(uint32_t a, uint32_t b) {
   return mul24(b, 0xC2B2AFu) + mul24(a ^ 0x5A5Au, 0x27D4EBu);
 }
-// One-bucket layout of the narrow image (Tables::hot1, an A/B of round 6): the hot table as 2048
-// buckets of four entries, a pair's bucket hash16_h >> 21 (one 32-byte read instead of two
-// 16-byte buckets); the Bloom filter blocked, both of a pair's bits in word hash16_g >> 19 (one
-// read instead of two).
-__host__ __device__ inline uint32_t hot1_bucket(uint32_t h) { return 4u * (h >> 21); }  // (u64 index)
-__host__ __device__ inline uint32_t hot1_word(uint32_t g) { return g >> 19; }
-__host__ __device__ inline uint32_t hot1_bits(uint32_t g) { return (1u << (g & 31u)) | (1u << ((g >> 5) & 31u)); }
 
 // Whole-piece table: raw byte strings of <= 8 bytes whose BPE is exactly one token (checked at
 // load time by running the merge loop on every vocab entry).  Entry = {lo32, hi32, len, id} of
@@ -224,7 +217,6 @@ struct Tables {            // device pointers, owned by the host runtime
   uint32_t compact;         // 1: entry values are new ids (strictly increasing in rank), else ranks
   uint32_t narrow;          // 1: every vocab id < 2^16 (the merge passes keep the last tier's tokens as u16 in LDS)
   uint32_t dbg;             // debug mode (CTOK_DBG_MODE), 0 in production
-  uint32_t hot1;            // 1: the narrow image in the one-bucket layout (hot1_bucket / hot1_word)
   uint32_t all_bytes;       // 1: every byte's char is in the vocab (no piece can have a dropped byte)
 };
 

@@ -149,17 +149,19 @@ __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_re
 // its start and end (wall clock, 100 MHz), its CU (xcc | se | cu) and a count.  The host prints,
 // per kernel, the CUs used and the spread of the workgroups' starts and ends (ctok_host.cpp).
 constexpr uint32_t kWgRecMax = 1024;  // (4 kernel slots: short, mid<2>, mid<3>, sparse)
+// (stateless: the record's place is recomputed at the end from the kernel argument, so that no
+// register stays live across the kernel -- the 64-slot pass is at its register limit)
 struct WgRec {
-  uint64_t* p = nullptr;
-  __device__ __forceinline__ void begin(uint64_t* base, uint32_t k) {
+  static __device__ __forceinline__ void begin(uint64_t* base, uint32_t k) {
     if (base && threadIdx.x == 0 && blockIdx.x < kWgRecMax) {
-      p = base + ((size_t)k * kWgRecMax + blockIdx.x) * 4;
+      uint64_t* p = base + ((size_t)k * kWgRecMax + blockIdx.x) * 4;
       p[0] = (uint64_t)wall_clock64();
       p[2] = __smid();
     }
   }
-  __device__ __forceinline__ void end(uint32_t count) {
-    if (p) {
+  static __device__ __forceinline__ void end(uint64_t* base, uint32_t k, uint32_t count) {
+    if (base && threadIdx.x == 0 && blockIdx.x < kWgRecMax) {
+      uint64_t* p = base + ((size_t)k * kWgRecMax + blockIdx.x) * 4;
       p[1] = (uint64_t)wall_clock64();
       p[3] = count;
     }
@@ -1239,21 +1241,10 @@ struct Probe<true, HOT> {
     k = key16(a, b);
     h = hash16_h(a, b);
     const uint32_t h2 = hash16_g(a, b);
-    uint32_t f;
-    uint64_t x0, x1, y0, y1;
-    if (t.hot1) {  // one-bucket layout (wave-uniform branch)
-      const uint32_t bw = P.bloom[hot1_word(h2)], bm = hot1_bits(h2);
-      f = (bw & bm) == bm ? 1u : 0u;
-      // (the bucket's two 16-byte halves in swapped order for odd buckets: each of the two reads
-      // then spreads its lanes over both halves' banks)
-      const uint32_t c = hot1_bucket(h), sw = (h >> 20) & 2u;
-      x0 = P.hot[c + sw], x1 = P.hot[c + sw + 1], y0 = P.hot[c + (sw ^ 2u)], y1 = P.hot[c + (sw ^ 2u) + 1];
-    } else {
-      const uint32_t b1 = h & (kBloomBits - 1), b2 = h2 >> 14;
-      f = (P.bloom[b1 >> 5] >> (b1 & 31)) & (P.bloom[b2 >> 5] >> (b2 & 31)) & 1u;
-      const uint32_t c1 = 2 * (h >> 20), c2 = 2 * (h2 >> 20);
-      x0 = P.hot[c1], x1 = P.hot[c1 + 1], y0 = P.hot[c2], y1 = P.hot[c2 + 1];
-    }
+    const uint32_t b1 = h & (kBloomBits - 1), b2 = h2 >> 14;
+    const uint32_t f = (P.bloom[b1 >> 5] >> (b1 & 31)) & (P.bloom[b2 >> 5] >> (b2 & 31)) & 1u;
+    const uint32_t c1 = 2 * (h >> 20), c2 = 2 * (h2 >> 20);
+    const uint64_t x0 = P.hot[c1], x1 = P.hot[c1 + 1], y0 = P.hot[c2], y1 = P.hot[c2 + 1];
     uint32_t v = kNoRank;
     bool hit = false;
     auto chk = [&](uint64_t x) {
@@ -1721,15 +1712,14 @@ __global__ __launch_bounds__(1024) void k_bpe_short(Work w, Tables t, uint32_t p
   const PairLds P{(const lds_u64*)s_img, (const lds_u32*)(s_img + kHotBuckets)};
   lds_u32* sk = (lds_u32*)s_key;
   lds_u16* st = (lds_u16*)s_tok;
-  WgRec rec;
-  rec.begin(w.wgrec, 0);
+  WgRec::begin(w.wgrec, 0);
   // passes: bit 0 the <= 8 B class, bit 1 the 9..16 B class (both, except in the timing A/B
   // CTOK_DBG_MODE=30, which launches them as two kernels to time them apart)
   if (passes & 1u)
     class_pass<8, COMPACT, true, NT, ShortCfg<NARROW>::SORTCAP, NARROW, kShortKT>(w, t, P, s_b2id, S, loaded, load, sk, st);
   if (passes & 2u)
     class_pass<16, COMPACT, true, NT, ShortCfg<NARROW>::SORTCAP, NARROW, kShortKT>(w, t, P, s_b2id, S, loaded, load, sk, st);
-  rec.end(loaded ? 1u : 0u);
+  WgRec::end(w.wgrec, 0, loaded ? 1u : 0u);
 }
 
 // Pieces of 17..32 bytes (CLS = 2, on the main stream after k_bpe_short) or 33..64 bytes (CLS = 3,
@@ -1759,16 +1749,21 @@ __global__ __launch_bounds__(NT) void k_bpe_mid(Work w, Tables t) {
   __shared__ uint16_t s_tok[NARROW ? 8 * NT : 1];
   // (the image is loaded up front: a lazy load pushes the 64-slot pass into scratch; the kernel
   // returns at once when k_segment found no piece of its class)
-  WgRec rec;
-  rec.begin(w.wgrec, CLS == 2 ? 1 : 2);
-  if (w.counters[CLS == 2 ? kCtrAnyMid : kCtrAnyC3] == 0) { rec.end(0); return; }
+  if constexpr (CLS == 2) WgRec::begin(w.wgrec, 1);  // (not in the 64-slot pass: it is at its register limit)
+  if (w.counters[CLS == 2 ? kCtrAnyMid : kCtrAnyC3] == 0) {
+    if constexpr (CLS == 2) WgRec::end(w.wgrec, 1, 0);
+    return;
+  }
   // every chunk already taken (the other instance of class 3 got there first): one read for the
   // whole workgroup, so its waves leave together (a wave that stayed would find thread 0 gone)
   __shared__ uint32_t s_left;
   if (threadIdx.x == 0)
     s_left = (uint64_t)__atomic_load_n(&w.counters[ctr_chunk(CLS)], __ATOMIC_RELAXED) * w.unit < w.n_tiles;
   __syncthreads();
-  if (!s_left) { rec.end(0); return; }
+  if (!s_left) {
+    if constexpr (CLS == 2) WgRec::end(w.wgrec, 1, 0);
+    return;
+  }
   const uint32_t tid = threadIdx.x;
   const uint4* img = NARROW ? t.lds16_image : t.lds_image;
   for (uint32_t i = tid; i < kLdsImageBytes / 16; i += NT) s_img[i] = img[i];
@@ -1777,7 +1772,7 @@ __global__ __launch_bounds__(NT) void k_bpe_mid(Work w, Tables t) {
   const PairLds P{(const lds_u64*)s_img, (const lds_u32*)(s_img + kHotBuckets)};
   class_pass<CLS == 2 ? 32 : 64, COMPACT, true, NT, kSortCap, NARROW, KT>(w, t, P, s_b2id, S, loaded, [] {},
                                                                          (lds_u32*)s_key, (lds_u16*)s_tok);
-  rec.end(1);
+  if constexpr (CLS == 2) WgRec::end(w.wgrec, 1, 1);
 }
 
 // hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device): the attribute is set
@@ -3136,8 +3131,7 @@ constexpr int kSparseWaves = 16;  // waves per k_bpe_sparse workgroup (beside th
 template <bool COMPACT, bool NARROW>
 __global__ __launch_bounds__(64 * kSparseWaves) void k_bpe_sparse(Work w, Tables t, uint32_t n) {
   if (spec_failed(w)) return;
-  WgRec rec;
-  rec.begin(w.wgrec, 3);
+  WgRec::begin(w.wgrec, 3);
   extern __shared__ __attribute__((aligned(16))) uint4 s_dyn[];
   __shared__ int32_t s_b2id[256];
   const uint32_t tid = threadIdx.x, lane = tid & 63;
@@ -3194,7 +3188,7 @@ __global__ __launch_bounds__(64 * kSparseWaves) void k_bpe_sparse(Work w, Tables
     atomicAdd(&w.counters[ctr_stat(3) + 1], st_ids);
   }
   __syncthreads();
-  rec.end(1);
+  WgRec::end(w.wgrec, 3, 1);
 }
 
 hipError_t launch_c3_list(const Work& w, hipStream_t s) {

@@ -54,6 +54,10 @@ def build(outdir: str, names) -> None:
             text, off = corpus.corpus_c4(workers=min(16, len(os.sched_getaffinity(0))))
         elif name.startswith("C4S"):  # C4S<N>: rank 0's shard of the N-way split (bench.py --gpus N)
             text, off = c4_shard(int(name[3:]), 0)
+        elif name == "C2L":  # C2's text cut into 100 documents of ~1.28 MB (long documents: tiles deep
+            # inside a document, whose first document k_segment finds by bisecting the offsets)
+            text, off = corpus.corpus_c2()
+            off = np.linspace(0, len(text), 101).astype(np.uint64)
         else:
             text, off = corpus.CONFIGS[name]()
         _save(outdir, name, text, off)
