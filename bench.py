@@ -425,7 +425,9 @@ def main():
                          "traffic_source": traffic_src,
                          "alg_bytes_per_launch": int(alg_dom), "ms_per_launch": round(ms_dom, 4),
                          "kernels": {k: {"ms": round(v[0], 4), "alg_bytes": int(v[1]),
-                                         "GBps": round(v[1] / (v[0] * 1e-3) / 1e9, 2)} for k, v in kernels.items()}},
+                                         # (k_bpe_mid's ms: the time it adds after k_bpe_short's end, 0 when none)
+                                         "GBps": round(v[1] / (v[0] * 1e-3) / 1e9, 2) if v[0] > 0 else None}
+                                     for k, v in kernels.items()}},
             "pipeline": {"ms_device": round(ms_dev, 4), "ms_pretok": round(avg("ms_pretok"), 4),
                          "ms_bpe_short": round(avg("ms_bpe_short"), 4), "ms_bpe_long": round(avg("ms_bpe_long"), 4),
                          "ms_emit": round(avg("ms_emit"), 4), "ms_call": round(avg("ms_total"), 4),

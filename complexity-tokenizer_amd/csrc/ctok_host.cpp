@@ -225,10 +225,9 @@ struct DeviceState {
   hipEvent_t ev[12] = {};
   hipEvent_t ev_sync = nullptr;   // spin-waited completion marker (no blocking-wait wakeup latency)
   hipStream_t side = nullptr;     // long-piece pass, overlapped with the short merge passes
-  hipStream_t side2 = nullptr;    // k_c3_list and its count, beside the side stream's counter copy
-  hipEvent_t ev_c3 = nullptr;     // the class-3 list and its count are complete
   hipEvent_t ev_tot = nullptr;    // the long pieces' totals are in the host words
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_cnt = nullptr;
+  hipEvent_t ev_join = nullptr;   // the side stream's long tiers are done
+  uint32_t seq = 0;               // encode calls (attempts) on this device: Work::seq
   uint64_t* host = nullptr;       // pinned host words for small device->host readbacks
   uint64_t* host_dev = nullptr;   // the same words as a device pointer (k_tokoff writes the results there)
   // tables
@@ -251,7 +250,7 @@ struct DeviceState {
   DevBuf<uint64_t> stamps;  // diagnostic builds (CTOK_SEG_STAMPS) with CTOK_STAMPS=1
   DevBuf<uint64_t> wgrec;   // diagnostic: CTOK_WGREC=1
   DevBuf<uint16_t> wpref;
-  DevBuf<uint32_t> long_cnt, long_ord, long_hist, c3q;
+  DevBuf<uint32_t> long_cnt, long_ord, long_hist;
   DevBuf<uint64_t> long_list, mid_list, scan_tmp, scan_tmp2;
   DevBuf<uint32_t> doc_flag, ncp;
   // NFC splice (nfc_splice): flagged-doc ranks / sub-batch positions, the speculative pass's
@@ -286,7 +285,7 @@ struct DeviceState {
     auto add = [&](const auto& x) { b += (uint64_t)x.cap * sizeof(*x.p); };
     add(tfirst), add(pbits), add(tile_np), add(tile_tok), add(tile_doc), add(tcls), add(list0), add(list1);
     add(list2), add(list3), add(tcnt), add(prec), add(mrec), add(pdoc), add(scratch), add(counters), add(lids), add(lw), add(tregion), add(rend);
-    add(wpref), add(long_cnt), add(long_ord), add(long_hist), add(long_pos), add(lw_pos), add(lwn), add(long_list), add(c3q);
+    add(wpref), add(long_cnt), add(long_ord), add(long_hist), add(long_pos), add(lw_pos), add(lwn), add(long_list);
     add(mid_list), add(scan_tmp), add(scan_tmp2), add(cps);
     add(doc_flag), add(ncp), add(norm_off), add(norm_text);
     add(nfc_bits), add(spl_rank), add(spl_ids), add(sub_ids), add(spl_pos), add(spl_toff), add(sub_off), add(sub_toff), add(sub_text);
@@ -309,12 +308,8 @@ struct DeviceState {
       for (auto& e : ev) if (e) (void)hipEventDestroy(e);
       for (auto& e : dev_ev) if (e) (void)hipEventDestroy(e);
       if (ev_sync) (void)hipEventDestroy(ev_sync);
-      if (ev_fork) (void)hipEventDestroy(ev_fork);
       if (ev_join) (void)hipEventDestroy(ev_join);
-      if (ev_cnt) (void)hipEventDestroy(ev_cnt);
       if (side) (void)hipStreamDestroy(side);
-      if (side2) (void)hipStreamDestroy(side2);
-      if (ev_c3) (void)hipEventDestroy(ev_c3);
       if (ev_tot) (void)hipEventDestroy(ev_tot);
       if (host) (void)hipHostFree(host);
       if (stream) (void)hipStreamDestroy(stream);
@@ -1397,14 +1392,11 @@ DeviceState* device_state(ctok* t, int device) {
   for (auto& e : ds->ev) HIPTRY(hipEventCreate(&e));
   for (auto& e : ds->dev_ev) HIPTRY(hipEventCreate(&e));
   HIPTRY(hipEventCreateWithFlags(&ds->ev_sync, hipEventDisableTiming));
-  HIPTRY(hipEventCreateWithFlags(&ds->ev_fork, hipEventDisableTiming));
   HIPTRY(hipEventCreateWithFlags(&ds->ev_join, hipEventDisableTiming));
-  HIPTRY(hipEventCreateWithFlags(&ds->ev_cnt, hipEventDisableTiming));
   HIPTRY(hipStreamCreateWithFlags(&ds->side, hipStreamNonBlocking));
-  HIPTRY(hipStreamCreateWithFlags(&ds->side2, hipStreamNonBlocking));
-  HIPTRY(hipEventCreateWithFlags(&ds->ev_c3, hipEventDisableTiming));
   HIPTRY(hipEventCreateWithFlags(&ds->ev_tot, hipEventDisableTiming));
-  HIPTRY(hipHostMalloc((void**)&ds->host, 4096, hipHostMallocDefault));
+  // (coherent: the host polls words k_report writes while the call runs -- Work::report)
+  HIPTRY(hipHostMalloc((void**)&ds->host, 4096, hipHostMallocCoherent));
   HIPTRY(hipHostGetDevicePointer((void**)&ds->host_dev, ds->host, 0));
   hipStream_t s = ds->stream;
   upload(ds->merge_tab, t->merge_tab.data(), t->merge_tab.size(), s);
@@ -1509,12 +1501,76 @@ bool debug_sync() {
 
 // Wait for all work on s by spinning on an event: a blocking stream synchronise can add
 // hundreds of microseconds of wake-up latency per call on this path's few sync points.
-void spin_sync(DeviceState* ds, hipStream_t s) {
+// (idle: called between polls -- the timed calls read their event pairs there, see Laps)
+template <class Idle>
+void spin_sync(DeviceState* ds, hipStream_t s, Idle idle) {
   HIPTRY(hipEventRecord(ds->ev_sync, s));
   for (;;) {
     hipError_t e = hipEventQuery(ds->ev_sync);
     if (e == hipSuccess) return;
     if (e != hipErrorNotReady) throw_err(CTOK_E_DEVICE, std::string("hipEventQuery: ") + hipGetErrorString(e));
+    idle();
+  }
+}
+void spin_sync(DeviceState* ds, hipStream_t s) {
+  spin_sync(ds, s, [] {});
+}
+
+// The elapsed times of a timed call's event pairs, each read as soon as its later event has
+// completed, while the host waits for the rest of the call: a read costs a few microseconds, and
+// the ten of an encode call, read after its final wait, added ~40 us to every timed call
+// (C4S8 1.20 -> 1.16 ms untimed, profiles/r06).
+struct Laps {
+  struct Lap {
+    hipEvent_t a, b;
+    double v;
+    bool done;
+  };
+  Lap l[12];
+  int n = 0;
+  int add(hipEvent_t a, hipEvent_t b) {
+    l[n] = {a, b, 0.0, false};
+    return n++;
+  }
+  void read(Lap& p) {
+    float v = 0;
+    HIPTRY(hipEventElapsedTime(&v, p.a, p.b));
+    p.v = v;
+    p.done = true;
+  }
+  void poll() {  // reads the first pair whose events have both completed, if any
+    for (int k = 0; k < n; k++) {
+      if (l[k].done) continue;
+      // (both: the events can be on two streams, the "later" one done first)
+      if (!done(l[k].b) || !done(l[k].a)) continue;
+      read(l[k]);
+      return;
+    }
+  }
+  static bool done(hipEvent_t ev) {
+    const hipError_t e = hipEventQuery(ev);
+    if (e == hipErrorNotReady) return false;
+    if (e != hipSuccess) throw_err(CTOK_E_DEVICE, std::string("hipEventQuery: ") + hipGetErrorString(e));
+    return true;
+  }
+  void finish() {
+    for (int k = 0; k < n; k++)
+      if (!l[k].done) read(l[k]);
+  }
+  double operator[](int k) const { return k < 0 ? 0.0 : l[k].v; }  // (-1: a pair not timed)
+};
+
+// Waits for k_report's report of this call (Work::report: the counters, then the sequence number);
+// a device error, or the stream running dry without it, ends the wait
+void wait_report(hipStream_t s, volatile uint32_t* rep, uint32_t seq) {
+  for (uint32_t i = 1;; i++) {
+    if (rep[kNumCounters] == seq) return;
+    if ((i & 4095) == 0) {
+      const hipError_t e = hipStreamQuery(s);
+      if (e == hipSuccess && rep[kNumCounters] != seq) throw_err(CTOK_E_DEVICE, "k_report: the call's report never came");
+      if (e != hipSuccess && e != hipErrorNotReady)
+        throw_err(CTOK_E_DEVICE, std::string("hipStreamQuery: ") + hipGetErrorString(e));
+    }
   }
 }
 
@@ -1603,10 +1659,18 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   // lean list capacities first; a call whose lists outgrow them runs again with the safe ones
   static const bool always_safe = getenv("CTOK_SAFE_CAPACITIES") != nullptr;
   bool safe = always_safe;
+  // diagnostic (CTOK_HOSTPROF=1): host time at points of the call, printed at its end
+  static const bool hostprof = getenv("CTOK_HOSTPROF") != nullptr;
+  double hp[10] = {};
+#define HP(i) \
+  if (hostprof) hp[i] = now_ms()
+  HP(0);
   for (;;) {
-  if (timing) HIPTRY(hipEventRecord(ds->ev[0], s));
+  // (timing: ev[0] is k_clear's start event, or a marker here when normalising work comes first)
+  const bool ev0_marker = timing && (t->add_prefix_space || (t->nfc && n_bytes && (all_nfc || !speculate)));
+  if (ev0_marker) HIPTRY(hipEventRecord(ds->ev[0], s));
 
-  ds->counters.ensure(kNumCounters);
+  ds->counters.ensure(kCounterWords);
   bool ctr_zeroed = false;  // (else launch_docstart zeroes them, in the bitmap's clearing launch)
   const uint8_t* text = d_text;
   const uint64_t* off = d_off;
@@ -1621,7 +1685,7 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   } else if (t->nfc && n_bytes && !speculate) {
     ds->doc_flag.ensure(n_docs + 1);
     HIPTRY(hipMemsetAsync(ds->doc_flag.p, 0, (n_docs + 1) * 4, s));
-    HIPTRY(hipMemsetAsync(ds->counters.p, 0, kNumCounters * 4, s));
+    HIPTRY(hipMemsetAsync(ds->counters.p, 0, kCounterWords * 4, s));
     ctr_zeroed = true;
     STEP("nfc_check", launch_nfc_check(d_text, n_bytes, d_off, (uint32_t)n_docs, tb, ds->doc_flag.p, ds->counters.p + 3, s));
     HIPTRY(hipMemcpyAsync(ds->host, ds->counters.p + 3, 4, hipMemcpyDeviceToHost, s));
@@ -1745,16 +1809,12 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   w.counters = ds->counters.p;
   w.scan_tmp = (uint32_t*)ds->scan_tmp.p;
   w.scan_tmp_cap = ds->scan_tmp.cap * 2;
-  // sparse class 3 (k_c3_list / k_bpe_sparse): at most c3_max pieces of 33..64 B are merged a
-  // wavefront each instead of by the register pass (CTOK_C3_SPARSE=n sets the bound, 0 disables)
-  // (read per call: the GPU tests switch it within one process)
+  // sparse class 3: at most c3_max pieces of 33..64 B are merged a wavefront each, by the 17..32 B
+  // pass's workgroups, instead of by the register pass (CTOK_C3_SPARSE=n sets the bound, 0
+  // disables) (read per call: the GPU tests switch it within one process)
   const char* c3_var = getenv("CTOK_C3_SPARSE");
   const uint64_t c3_env = c3_var ? strtoull(c3_var, nullptr, 10) : kC3SparseDefault;
-  w.c3_max = tb.n_at == 0 ? (uint32_t)std::min<uint64_t>(c3_env, B / 33 + 64) : 0u;
-  if (w.c3_max) {
-    ds->c3q.ensure(w.c3_max + 8);
-    w.c3q = ds->c3q.p;
-  }
+  w.c3_max = tb.n_at == 0 ? (uint32_t)std::min<uint64_t>(c3_env, 0xFFFFFFFFull) : 0u;
 #ifdef CTOK_CHECK
   // (range-checking build: every merged record starts out of range, so one no pass wrote traps)
   HIPTRY(hipMemsetAsync(ds->mrec.p, 0xFF, (size_t)nt * kTileSlots * 4, s));
@@ -1772,14 +1832,38 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
     w.stamps = ds->stamps.p;
   }
 
-  // events (main stream s): 0 start | 7 segment start | 1 segment end | 2 <= 16 B merge pass end |
-  //   8, 10 around the 17..32 B pass | 9 after the 33..64 B pass (main instance) | 5 side stream joined | 3 dropped-byte pass end | 6 emit end.
-  //   The side stream runs the long-piece pass, forked after k_segment (it reads only its output)
-  //   and joined before the dropped-byte pass (fed by all merge passes) and k_emit.
-  STEP("docstart", launch_docstart(w, s, !ctr_zeroed));
-  if (timing) HIPTRY(hipEventRecord(ds->ev[7], s));
-  STEP("segment", launch_segment(w, tb, s));
-  if (timing) HIPTRY(hipEventRecord(ds->ev[1], s));
+  // Streams and ordering.  The main stream s runs k_clear, k_tilefirst, k_segment, k_bpe_short,
+  // whose first wave writes the report the host polls (k_segment's counters, the class-3 count
+  // among them, into pinned host words, then the call's sequence number; k_report does it when
+  // k_bpe_short does not run).  Having seen it, the host knows k_segment has completed, so it
+  // launches what reads k_segment's output on the side stream with no fork event: the 17..32 B
+  // pass when the call has no long pieces (its workgroups take the CUs k_bpe_short's free at its
+  // end, beside the 33..64 B pass -- register or sparse -- on the main stream), else the
+  // long-piece preparation and tiers; one join before the tail (dropped-byte pass, tile scan,
+  // k_emit, k_tokoff).  The round-5 flow forked the side stream with an event after k_segment
+  // (the counter copy and, in round 6's first build, the class-3 list there), and the sparse pass
+  // waited for the list's event: ~3 us per event marker on the main stream and ~10 us per
+  // cross-stream wait (tools/queue_gaps.hip, profiles/r06).  Any-order packets
+  // (hipExtAnyOrderLaunch) do not help here: one starts when the previous kernel's first
+  // workgroup retires, and k_bpe_short's persistent workgroups retire together at its end
+  // (tools/anyorder_check.hip).
+  // Timing (stats): events recorded by the kernels' own dispatches (Lx), no marker packets, and
+  // none on the launches the device waits for at the call's start (an event costs the host ~3 us
+  // per launch there; later launches run ahead of the device): 0 k_clear start (a marker when
+  //   normalising work precedes it) | 7 k_tilefirst end | 1 k_segment end | 2 k_bpe_short end |
+  //   8, 10 the 17..32 B pass | 9 the 33..64 B pass's end | 5 the dropped-byte pass start | 3 the
+  //   tile scan start | 6 k_tokoff end
+  const bool tm = timing && st && nt;  // (no tiles: no merge pass to time)
+  auto lx = [&](int a, int b, bool any_order) {
+    Lx x;
+    x.any_order = any_order;
+    if (tm && a >= 0) x.start = ds->ev[a];
+    if (tm && b >= 0) x.stop = ds->ev[b];
+    return x;
+  };
+  HP(1);
+  STEP("docstart", launch_docstart(w, s, !ctr_zeroed, lx(ev0_marker ? -1 : 0, -1, false), lx(-1, 7, false)));
+  STEP("segment", launch_segment(w, tb, s, lx(-1, 1, false)));
   if (segment_only) {  // pre-tokenization only (the trainer's word counting): pbits of the text
     HIPTRY(hipMemcpyAsync(ds->host + 1, ds->counters.p, kNumCounters * 4, hipMemcpyDeviceToHost, s));
     spin_sync(ds, s);
@@ -1789,32 +1873,18 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
     }
     return 0;
   }
-  HIPTRY(hipEventRecord(ds->ev_fork, s));
-  HIPTRY(hipStreamWaitEvent(ds->side, ds->ev_fork, 0));
-  // k_segment's counters (long pieces, class 3 present) come back on the side stream while the
-  // main stream's merge passes run; the long-piece tiers are then launched with grids sized for
-  // the pieces there are, or not at all (no idle workgroups queued behind the merge passes)
+  if (++ds->seq == 0) ds->seq = 1;
+  w.seq = ds->seq;
+  w.report = (uint32_t*)(ds->host_dev + 64);
   volatile uint32_t* seg_cnt = (volatile uint32_t*)(ds->host + 64);
-  HIPTRY(hipMemcpyAsync((void*)seg_cnt, ds->counters.p, kNumCounters * 4, hipMemcpyDeviceToHost, ds->side));
-  HIPTRY(hipEventRecord(ds->ev_cnt, ds->side));
-  // the class-3 list on a stream of its own (no LDS: it runs beside k_bpe_short), so that the
-  // counter copy above -- which the long-piece tiers wait for -- is not queued behind it
-  volatile uint32_t* c3_cnt = (volatile uint32_t*)(ds->host + 120);
-  if (w.c3_max) {
-    HIPTRY(hipStreamWaitEvent(ds->side2, ds->ev_fork, 0));
-    HIPTRY(launch_c3_list(w, ds->side2));
-    HIPTRY(hipMemcpyAsync((void*)c3_cnt, ds->counters.p + kCtrC3Count, 4, hipMemcpyDeviceToHost, ds->side2));
-    HIPTRY(hipEventRecord(ds->ev_c3, ds->side2));
-  }
-  STEP("bpe_short", launch_bpe_class(w, tb, 0, s));
-  if (timing) HIPTRY(hipEventRecord(ds->ev[2], s));
-  // k_segment's counters (they arrive while the <= 16 B pass runs, long before it ends): the
-  // 17..32 B pass takes 768 threads per workgroup when there are no long pieces
-  for (;;) {
-    const hipError_t e = hipEventQuery(ds->ev_cnt);
-    if (e == hipSuccess) break;
-    if (e != hipErrorNotReady) throw_err(CTOK_E_DEVICE, std::string("hipEventQuery: ") + hipGetErrorString(e));
-  }
+  // (k_bpe_short's first wave writes the report; without it -- added tokens, no tiles -- k_report)
+  HP(2);
+  if (tb.n_at != 0 || !nt) STEP("report", launch_report(w, s));
+  STEP("bpe_short", launch_bpe_class(w, tb, 0, s, lx(-1, 2, false)));
+  HP(3);
+  wait_report(s, seg_cnt, w.seq);
+  HP(4);
+  // the 17..32 B pass takes 768 threads per workgroup when there are no long pieces
   w.mid_wide = (seg_cnt[0] == 0 && !getenv("CTOK_MID512")) ? 1u : 0u;
   // long pieces: their lengths, order and places first (side stream, before the host waits for
   // anything else: the long tiers after them are the side stream's critical path on C5 / C3);
@@ -1835,68 +1905,72 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
     HIPTRY(hipMemcpyAsync((void*)(tot + 1), ds->lw_pos.p + n_long, 4, hipMemcpyDeviceToHost, ds->side));
     HIPTRY(hipEventRecord(ds->ev_tot, ds->side));
   }
-  uint32_t c3n = 0;
-  if (w.c3_max && seg_cnt[kCtrAnyC3]) {  // (the list's count: it arrives while k_bpe_short runs)
-    for (;;) {
-      const hipError_t e = hipEventQuery(ds->ev_c3);
-      if (e == hipSuccess) break;
-      if (e != hipErrorNotReady) throw_err(CTOK_E_DEVICE, std::string("hipEventQuery: ") + hipGetErrorString(e));
-    }
-    c3n = *c3_cnt;
-  }
+  const uint32_t c3n = seg_cnt[kCtrC3Count];
   const bool c3_sparse = c3n != 0 && c3n <= w.c3_max;
-  // Without long pieces the side stream is idle: the 17..32 B pass (overlap >= 1) and the
-  // 33..64 B pass (overlap 2) go there, so their workgroups take the CUs that k_bpe_short's
-  // workgroups free at its end instead of waiting for its last one (the classes' pieces,
-  // regions and records are disjoint; the main stream joins the side stream before k_emit)
+  // Without long pieces the side stream is idle: the 17..32 B pass goes there (CTOK_OVERLAP=0: on
+  // the main stream after k_bpe_short), so its workgroups take the CUs k_bpe_short's free at its
+  // end, beside the 33..64 B pass on the main stream (the classes' pieces, regions and records are
+  // disjoint); no fork event -- the report orders it after k_segment --, one join before the tail
   const char* ov_var = getenv("CTOK_OVERLAP");
   const int overlap = ov_var ? atoi(ov_var) : kOverlapDefault;
   const bool mid_side = overlap >= 1 && seg_cnt[0] == 0;
   ds->last_mid_side = mid_side;
-  hipStream_t s_mid = mid_side ? ds->side : s, s_c3 = (mid_side && overlap >= 2) ? ds->side : s;
-  if (timing) HIPTRY(hipEventRecord(ds->ev[8], s_mid));
-  { hipStream_t s = s_mid; STEP("bpe_mid", launch_bpe_class(w, tb, 2, s)); }
-  if (timing) HIPTRY(hipEventRecord(ds->ev[10], s_mid));
-  if (timing) HIPTRY(hipEventRecord(ds->ev[4], s_c3));
-  {
-    hipStream_t s = s_c3;
-    if (c3_sparse) HIPTRY(hipStreamWaitEvent(s, ds->ev_c3, 0));  // (the list: complete long before)
-    if (c3_sparse) STEP("bpe_c3_sparse", launch_c3_sparse(w, tb, c3n, s));
-    else STEP("bpe_c3", launch_bpe_class(w, tb, 4, s));
-  }
-  if (timing) HIPTRY(hipEventRecord(ds->ev[9], s_c3));
-  if (!spec_fail1) {
-    bool any_gmem = false;  // a long piece for the global-memory tier (its state words reserved)
-    if (n_long) {
-      for (;;) {  // the long pieces' totals (launch_long_prep above)
-        const hipError_t e = hipEventQuery(ds->ev_tot);
-        if (e == hipSuccess) break;
-        if (e != hipErrorNotReady) throw_err(CTOK_E_DEVICE, std::string("hipEventQuery: ") + hipGetErrorString(e));
-      }
-      any_gmem = tot[1] != 0;
-      ds->lids.ensure((uint64_t)tot[0] + 64);
-      ds->lw.ensure(4 * (uint64_t)tot[1] + 64);
-      w.lids = ds->lids.p;
-      w.lw = ds->lw.p;
+  STEP("bpe_mid", launch_bpe_class(w, tb, 2, mid_side ? ds->side : s, lx(8, 10, false)));
+  if (c3_sparse) STEP("bpe_c3_sparse", launch_c3_sparse(w, tb, c3n, s, lx(-1, 9, false)));
+  else STEP("bpe_c3", launch_bpe_class(w, tb, 4, s, lx(-1, 9, false)));
+  if (!spec_fail1 && n_long) {
+    for (;;) {  // the long pieces' totals (launch_long_prep above)
+      const hipError_t e = hipEventQuery(ds->ev_tot);
+      if (e == hipSuccess) break;
+      if (e != hipErrorNotReady) throw_err(CTOK_E_DEVICE, std::string("hipEventQuery: ") + hipGetErrorString(e));
     }
+    const bool any_gmem = tot[1] != 0;  // a long piece for the global-memory tier (its state words reserved)
+    ds->lids.ensure((uint64_t)tot[0] + 64);
+    ds->lw.ensure(4 * (uint64_t)tot[1] + 64);
+    w.lids = ds->lids.p;
+    w.lw = ds->lw.p;
     STEP("bpe_long", launch_bpe_long(w, tb, ds->side, n_long, seg_cnt[kCtrAnyC3] != 0 && !c3_sparse, any_gmem));
   }
-  HIPTRY(hipEventRecord(ds->ev_join, ds->side));
-  HIPTRY(hipStreamWaitEvent(s, ds->ev_join, 0));
-  if (timing) HIPTRY(hipEventRecord(ds->ev[5], s));
-  STEP("bpe_dropped", launch_bpe_class(w, tb, 3, s));
-  if (timing) HIPTRY(hipEventRecord(ds->ev[3], s));
+  if (n_long || mid_side) {
+    HIPTRY(hipEventRecord(ds->ev_join, ds->side));
+    HIPTRY(hipStreamWaitEvent(s, ds->ev_join, 0));
+  }
+  const bool dropped_pass = tb.n_at == 0 && !tb.all_bytes;
+  STEP("bpe_dropped", launch_bpe_class(w, tb, 3, s, lx(5, -1, false)));
   // the token count and the counters: written by k_tokoff straight into the pinned host words
   // (two copy launches fewer at the end of every call), or copied
   static const bool copy_res = getenv("CTOK_COPY_RESULTS") != nullptr;
   w.host_res = copy_res ? nullptr : ds->host_dev;
-  STEP("emit", launch_emit(w, d_ids, ids_cap, d_tok_off, s, st != nullptr, seg_cnt[kCtrEmptyDocs] != 0));
-  if (timing) HIPTRY(hipEventRecord(ds->ev[6], s));
+  STEP("emit", launch_emit(w, d_ids, ids_cap, d_tok_off, s, st != nullptr, seg_cnt[kCtrEmptyDocs] != 0,
+                           lx(3, -1, false), lx(-1, 6, false)));
   if (!w.host_res) {
     HIPTRY(hipMemcpyAsync(ds->host, d_tok_off + n_docs, 8, hipMemcpyDeviceToHost, s));
     HIPTRY(hipMemcpyAsync(ds->host + 1, ds->counters.p, kNumCounters * 4, hipMemcpyDeviceToHost, s));
   }
-  spin_sync(ds, s);
+  Laps laps;
+  int lap[11];
+  if (tm) {
+    hipEvent_t* e = ds->ev;
+    const bool passes = tb.n_at == 0;  // (with added tokens one kernel merges every <= 32 B piece)
+    lap[0] = laps.add(e[0], e[1]);  // pretok
+    lap[1] = laps.add(e[7], e[1]);  // segment (from k_tilefirst's end)
+    lap[2] = laps.add(e[1], e[2]);  // <= 16 B pass (from k_segment's end)
+    // class 2; on the side stream its events span the wait for k_bpe_short's CUs, so the time it
+    // adds after k_bpe_short's end is reported
+    lap[3] = !passes ? -1 : mid_side ? laps.add(e[2], e[10]) : laps.add(e[8], e[10]);
+    lap[4] = passes ? laps.add(e[2], e[9]) : -1;  // class 3 (register or sparse pass; after k_bpe_short)
+    lap[5] = laps.add(e[1], e[2]);  // k_segment's end to the merge passes' ends
+    lap[6] = passes ? laps.add(e[1], e[10]) : -1;
+    lap[7] = passes ? laps.add(e[1], e[9]) : -1;
+    lap[8] = laps.add(e[1], e[dropped_pass ? 5 : 3]);  // ... to the tail's start
+    lap[9] = laps.add(e[3], e[6]);  // tile scan + emit
+    lap[10] = laps.add(e[0], e[6]);  // device
+  }
+  HP(5);
+  spin_sync(ds, s, [&] { laps.poll(); });
+  HP(6);
+  laps.finish();
+  HP(7);
   uint64_t ntok = ((volatile uint64_t*)ds->host)[0];
   if (w.wgrec) {  // per kernel: workgroups, distinct CUs, start / end spread (us from the first start)
     std::vector<uint64_t> r(kWgRecWords);
@@ -1985,25 +2059,32 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
       st->class_bytes[c] = cnt[ctr_stat(c)];
       st->class_ids[c] = cnt[ctr_stat(c) + 1];
     }
-    if (timing) {
-      auto el = [&](int i, int j) {
+    if (tm) {
+      st->ms_pretok = laps[lap[0]];
+      st->ms_segment = laps[lap[1]];
+      st->ms_bpe_lo = laps[lap[2]];
+      st->ms_bpe_hi = std::max(0.0, laps[lap[3]]);
+      st->ms_bpe_med = laps[lap[4]];
+      // the merge passes (k_segment's end to the last one's end) and the side stream's long tiers
+      // past them (the tail's start waits for the join)
+      st->ms_bpe_short = std::max(laps[lap[5]], std::max(laps[lap[6]], laps[lap[7]]));
+      st->ms_bpe_long = std::max(0.0, laps[lap[8]] - st->ms_bpe_short);
+      st->ms_emit = laps[lap[9]];
+      st->ms_device = laps[lap[10]];
+      if (w.nfc_watch == 2 && cnt[12]) {  // (the NFC splice ran after the main call: ev[11] ends it)
         float v = 0;
-        HIPTRY(hipEventElapsedTime(&v, ds->ev[i], ds->ev[j]));
-        return (double)v;
-      };
-      st->ms_pretok = el(0, 1);
-      st->ms_segment = el(7, 1);
-      st->ms_bpe_lo = el(1, 2);
-      // class 2; on the side stream (overlap) its events span the wait for k_bpe_short's CUs, so
-      // the time it adds after k_bpe_short's end is reported instead
-      st->ms_bpe_hi = ds->last_mid_side ? std::max(0.0, el(2, 10)) : el(8, 10);
-      st->ms_bpe_med = el(4, 9);   // class 3, main-stream instance (the side instance overlaps) or sparse path
-      st->ms_bpe_short = el(1, 9);
-      st->ms_bpe_long = el(9, 5);
-      st->ms_emit = el(3, 6);
-      st->ms_device = w.nfc_watch == 2 && cnt[12] ? el(0, 11) : el(0, 6);
+        HIPTRY(hipEventElapsedTime(&v, ds->ev[0], ds->ev[11]));
+        st->ms_device = v;
+      }
     }
   }
+  HP(8);
+  if (hostprof)
+    fprintf(stderr, "[ctok hostprof] us from entry: prep %.1f  clear..segment launched %.1f  short launched %.1f  report %.1f  "
+            "all launched %.1f  synced %.1f  laps %.1f  end %.1f\n", (hp[1] - hp[0]) * 1e3, (hp[2] - hp[0]) * 1e3,
+            (hp[3] - hp[0]) * 1e3, (hp[4] - hp[0]) * 1e3, (hp[5] - hp[0]) * 1e3, (hp[6] - hp[0]) * 1e3,
+            (hp[7] - hp[0]) * 1e3, (hp[8] - hp[0]) * 1e3);
+#undef HP
   return ntok;
   }
 }

@@ -37,14 +37,18 @@ constexpr uint32_t kCap0 = kTile, kCap1 = (kTile + 8) / 9, kCap2 = (kTile + 16) 
 constexpr uint32_t kCap0Lean = 1040;  // (65 lines per tile: a power-of-two stride put every tile's list on one memory channel)
 constexpr int kNumClasses = 4;
 constexpr int kNumCounters = 32;
+// the counters buffer: kNumCounters words, then kC3Shards class-3 counts (k_segment adds tile t's
+// class-3 pieces to shard t % kC3Shards; the report sums them into counters[kCtrC3Count])
+constexpr int kC3Shards = 64;
+constexpr int kCounterWords = kNumCounters + kC3Shards;
 // counters[] slots of class pass c: bytes merged / ids produced (statistics), next chunk
 __host__ __device__ constexpr int ctr_stat(int c) { return c < 3 ? 6 + 2 * c : 16; }
 __host__ __device__ constexpr int ctr_chunk(int c) { return c < 3 ? 13 + c : 18; }
 constexpr int kCtrAnyMid = 19;  // counters[19] != 0: some tile has a class-2 piece
 constexpr int kCtrAnyC3 = 20;   // counters[20] != 0: some tile has a class-3 piece
 constexpr int kCtrEmptyDocs = 21;  // counters[21]: empty documents (k_tilefirst); 0: k_emit writes tok_off
-constexpr int kCtrC3Count = 22;    // counters[22]: class-3 pieces (k_c3_list; the sparse path's list length)
-constexpr int kCtrC3Take = 23;     // counters[23]: next entry of that list (k_bpe_sparse's waves)
+constexpr int kCtrC3Count = 22;    // counters[22] of the report: class-3 pieces (the shards' sum)
+constexpr int kCtrC3Take = 23;     // counters[23]: next 64-tile chunk of the sparse class-3 pass
 constexpr uint32_t kC3SparseDefault = 65536;  // Work::c3_max unless CTOK_C3_SPARSE says otherwise
 constexpr uint32_t kWgRecWords = 4 * 1024 * 4;  // Work::wgrec: 4 kernels x 1024 workgroups x 4 words
 constexpr int kOverlapDefault = 1;             // merge passes on the side stream without long pieces (CTOK_OVERLAP)
@@ -278,11 +282,22 @@ struct Work {              // device pointers, sized by the host for one call
   uint32_t* scan_tmp;      // scan partials
   uint64_t scan_tmp_cap;
   uint64_t* stamps;        // diagnostic builds only (CTOK_SEG_STAMPS): 8 u64 per tile, else null
-  uint32_t* c3q;           // [c3_max] class-3 pieces as tile << 7 | list index (k_c3_list), for the sparse path
   uint32_t c3_max;         // the sparse path takes class 3 when it holds at most this many pieces (0: never)
   uint64_t* host_res;      // pinned host words (device pointer): k_tokoff writes the token count to [0] and
                            // the counters to [1 ..] (null: the host copies them)
   uint64_t* wgrec;         // diagnostic (CTOK_WGREC=1): per-workgroup start / end / CU of the merge passes, else null
+  uint32_t* report;        // pinned host words (device pointer): k_report writes the counters to
+                           // [0, kNumCounters) and then seq to [kNumCounters] (the host polls it)
+  uint32_t seq;            // this call's sequence number (nonzero)
+};
+
+// Launch options of one kernel (hipExtLaunchKernel): any_order -- its packet does not wait for the
+// stream's earlier kernels to end (measured: it starts when the previous kernel's first workgroup
+// retires; a start event on it cancels that); start / stop -- events the kernel's own dispatch
+// records (a timed call puts no marker packets between its kernels).
+struct Lx {
+  bool any_order = false;
+  hipEvent_t start = nullptr, stop = nullptr;
 };
 
 // ---- decode (decode.hip): ids -> UTF-8 text -------------------------------------------
@@ -359,23 +374,26 @@ hipError_t launch_pad_rows(const PadWork& w, hipStream_t s);
 
 // ---- launchers (kernels.hip) -----------------------------------------------------------
 void upload_done();
-hipError_t launch_docstart(const Work& w, hipStream_t s, bool zero_counters);  // also zeroes the counters and nfc_bits
+// also zeroes the counters and nfc_bits; x: k_clear's launch options, x2: k_tilefirst's
+hipError_t launch_docstart(const Work& w, hipStream_t s, bool zero_counters, Lx x = {}, Lx x2 = {});
 uint64_t nfc_bits_words(uint64_t n_bytes);  // nfc_bits size (u32 words)
-hipError_t scan_tiles(const Work& w, hipStream_t s, bool count);  // tile_tok, tile_doc: exclusive scans + totals
-                                                                  // at n_tiles; count: pieces into counters[5]
+// tile_tok, tile_doc: exclusive scans + totals at n_tiles; count: pieces into counters[5]; x: the first launch's
+hipError_t scan_tiles(const Work& w, hipStream_t s, bool count, Lx x = {});
 hipError_t launch_nfc_check(const uint8_t* text, uint64_t n_bytes, const uint64_t* doc_off, uint32_t n_docs,
                             const Tables& t, uint32_t* doc_flag, uint32_t* counter, hipStream_t s);
 hipError_t launch_norm(const uint8_t* text, const uint64_t* doc_off, uint32_t n_docs, const uint32_t* doc_flag,
                        int add_prefix, int nfc, const Tables& t, uint32_t* cp_scratch, uint32_t* ncp,
                        uint64_t* new_len_then_off, uint8_t* out_text, int phase, hipStream_t s);
-hipError_t launch_segment(const Work& w, const Tables& t, hipStream_t s);
-// cls 0: classes 0 and 1; 2: classes 2 and 3; 3: dropped-byte pieces (mid_list)
-hipError_t launch_bpe_class(const Work& w, const Tables& t, int cls, hipStream_t s);
-// sparse class 3: k_c3_list gathers the class-3 pieces (count into counters[kCtrC3Count]);
-// launch_c3_sparse merges them a wavefront per piece (the host launches it instead of the
-// 33..64 B register pass when the count is at most Work::c3_max)
-hipError_t launch_c3_list(const Work& w, hipStream_t s);
-hipError_t launch_c3_sparse(const Work& w, const Tables& t, uint32_t n_pieces, hipStream_t s);
+hipError_t launch_segment(const Work& w, const Tables& t, hipStream_t s, Lx x = {});
+// cls 0: classes 0 and 1; 2: class 2; 4: class 3 (main instance); 3: dropped-byte pieces (mid_list).
+// (With added tokens only cls 0 launches a kernel; cls 3 none when Tables::all_bytes; none without tiles.)
+hipError_t launch_bpe_class(const Work& w, const Tables& t, int cls, hipStream_t s, Lx x = {});
+// k_report: the counters into Work::report, then Work::seq (one wave, after k_segment; k_bpe_short's
+// first wave does the same, so the host launches it only when k_bpe_short does not run)
+hipError_t launch_report(const Work& w, hipStream_t s);
+// sparse class 3 (k_bpe_sparse): the host launches it instead of the 33..64 B register pass when
+// the report's class-3 count is at most Work::c3_max
+hipError_t launch_c3_sparse(const Work& w, const Tables& t, uint32_t n_pieces, hipStream_t s, Lx x = {});
 // long-piece preparation (side stream): lengths, order, id places (long_pos) and global-memory
 // state places (lw_pos); long_pos[n_long] / lw_pos[n_long] = the totals the host sizes lids / lw by
 hipError_t launch_long_prep(const Work& w, const Tables& t, hipStream_t s, uint32_t n_long, uint32_t* lwn,
@@ -385,8 +403,9 @@ hipError_t launch_long_prep(const Work& w, const Tables& t, hipStream_t s, uint3
 hipError_t launch_bpe_long(const Work& w, const Tables& t, hipStream_t s, uint32_t n_long, bool any_c3, bool any_gmem);
 // count_pieces: counters[5] = pieces (statistics); empty_docs: some document is empty (k_tokoff
 // then writes every tok_off entry; else k_emit wrote them and k_tokoff only the total)
+// (first: the tile scan's first launch; last: k_tokoff)
 hipError_t launch_emit(const Work& w, uint32_t* ids, uint64_t ids_cap, uint64_t* tok_off, hipStream_t s,
-                       bool count_pieces, bool empty_docs = true);
+                       bool count_pieces, bool empty_docs = true, Lx first = {}, Lx last = {});
 // exclusive scan of n u32 (n read from *n_dev when non-null, else n_max); out[n] = total
 hipError_t scan_u32(const uint32_t* in, uint32_t* out, uint64_t n_max, const uint32_t* n_dev,
                     uint32_t* tmp, uint64_t tmp_cap, hipStream_t s);

@@ -22,6 +22,7 @@
 //
 // The regex of GPT2_PATTERN is evaluated as a "piece starts here" predicate over code-point
 // classes {White_Space, L, N, other} (derivation in DESIGN.md), bit-parallel on 64-bit masks.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -35,12 +36,38 @@ namespace ctok_dev {
 
 #define HIPCHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) return e_; } while (0)
 
+// A kernel launch with Lx's options (any-order packet, start / stop events of its own dispatch)
+// through hipExtLaunchKernel, or a plain launch when it has none.
+template <typename F, typename... A>
+static void launch_lx(const Lx& x, F k, dim3 grid, dim3 block, uint32_t lds, hipStream_t s, A... a) {
+  if (x.any_order || x.start || x.stop)
+    hipExtLaunchKernelGGL(k, grid, block, lds, s, x.start, x.stop, x.any_order ? (uint32_t)hipExtAnyOrderLaunch : 0u,
+                          a...);
+  else
+    hipLaunchKernelGGL(k, grid, block, lds, s, a...);
+}
+
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 constexpr uint32_t kDead = 0xFFFFFFFFu;
 constexpr uint32_t kSel = kNoRank - 1;  // marks a merge site during a parallel round
 
 // ------------------------------------------------------------------------------------------
 // small device helpers
+
+// The call's report (Work::report; one wave, after k_segment has completed): the counters, with
+// the class-3 shards summed into counters[kCtrC3Count], into the pinned host words, a
+// system-scope release, then the call's sequence number (see k_report).
+__device__ __forceinline__ void write_report(const Work& w) {
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t c3 = w.counters[kNumCounters + lane];  // (kC3Shards == 64: one shard per lane)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c3 += (uint32_t)__shfl_xor((int)c3, o, 64);
+  if (lane < (uint32_t)kNumCounters) w.report[lane] = lane == (uint32_t)kCtrC3Count ? c3 : w.counters[lane];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (lane == 0) __hip_atomic_store(&w.report[kNumCounters], w.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // (and the sequence number itself on its way)
+}
 
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
 #pragma unroll
@@ -311,18 +338,18 @@ __global__ __launch_bounds__(256) void k_clear(uint32_t* __restrict__ bits, uint
                                                uint32_t* __restrict__ tfirst, uint32_t n_tiles) {
   if (bits) clear_words(bits, n);
   for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n_tiles; i += gridDim.x * 256) tfirst[i] = ~0u;
-  if (blockIdx.x == 0 && counters && threadIdx.x < (uint32_t)kNumCounters) counters[threadIdx.x] = 0u;
+  if (blockIdx.x == 0 && counters && threadIdx.x < (uint32_t)kCounterWords) counters[threadIdx.x] = 0u;
 }
 
 uint64_t nfc_bits_words(uint64_t n_bytes) { return (n_bytes + 2047) / 2048 + 8; }
 
-hipError_t launch_docstart(const Work& w, hipStream_t s, bool zero_counters) {
+hipError_t launch_docstart(const Work& w, hipStream_t s, bool zero_counters, Lx x, Lx x2) {
   const bool nfc = w.nfc_watch == 2;
   const uint64_t n = nfc ? nfc_bits_words(w.n_bytes) : 0;
   const uint64_t work = std::max<uint64_t>(n / 4, w.n_tiles);
-  k_clear<<<(unsigned)std::min<uint64_t>((work + 255) / 256 + 1, 8ull * w.n_cus), 256, 0, s>>>(
-      nfc ? w.nfc_bits : nullptr, n, zero_counters ? w.counters : nullptr, w.tfirst, w.n_tiles);
-  if (w.n_tiles) k_tilefirst<<<(w.n_docs + 1 + 255) / 256, 256, 0, s>>>(w.doc_off, w.n_docs, w.n_tiles, w.tfirst, w.counters);
+  launch_lx(x, k_clear, (unsigned)std::min<uint64_t>((work + 255) / 256 + 1, 8ull * w.n_cus), 256, 0, s,
+            nfc ? w.nfc_bits : nullptr, n, zero_counters ? w.counters : nullptr, w.tfirst, w.n_tiles);
+  if (w.n_tiles) launch_lx(x2, k_tilefirst, (w.n_docs + 1 + 255) / 256, 256, 0, s, w.doc_off, w.n_docs, w.n_tiles, w.tfirst, w.counters);
   else if (w.n_docs)  // (no text: only the empty-document count)
     k_tilefirst<<<(w.n_docs + 255) / 256, 256, 0, s>>>(w.doc_off, w.n_docs, 0, w.tfirst, w.counters);
   return hipGetLastError();
@@ -918,16 +945,19 @@ __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(
     w.tcls[(size_t)lane * w.n_tiles + tile] = lane == 0 ? n0 : lane == 1 ? n1 : lane == 2 ? n2 : n3;
   if (lane == 0 && n2) w.counters[kCtrAnyMid] = 1;  // plain stores: every writer stores 1
   if (lane == 0 && n3) w.counters[kCtrAnyC3] = 1;
+  // the class-3 count (the host's choice of the sparse path): one of kC3Shards counters per tile
+  // (one counter for every tile: C5 k_segment 1.7 -> 5.9 ms, its atomics serialised on one address)
+  if (lane == 0 && n3) atomicAdd(&w.counters[kNumCounters + (tile & (kC3Shards - 1))], n3);
   SEG_STAMP(5);
 #ifdef CTOK_SEG_STAMPS
   if (w.stamps && lane == 0) w.stamps[(size_t)tile * 8 + 6] = np;
 #endif
 }
 
-hipError_t launch_segment(const Work& w, const Tables& t, hipStream_t s) {
+hipError_t launch_segment(const Work& w, const Tables& t, hipStream_t s, Lx x) {
   const uint32_t grid = (w.n_tiles + kSegWaves - 1) / kSegWaves;
-  if (w.n_tiles && w.rec16) k_segment<true><<<grid, 64 * kSegWaves, 0, s>>>(w, t);
-  else if (w.n_tiles) k_segment<false><<<grid, 64 * kSegWaves, 0, s>>>(w, t);
+  if (w.n_tiles && w.rec16) launch_lx(x, k_segment<true>, grid, 64 * kSegWaves, 0, s, w, t);
+  else if (w.n_tiles) launch_lx(x, k_segment<false>, grid, 64 * kSegWaves, 0, s, w, t);
   return hipGetLastError();
 }
 
@@ -1695,6 +1725,7 @@ constexpr int kShortKT = 64;
 
 template <bool COMPACT, bool NARROW>
 __global__ __launch_bounds__(1024) void k_bpe_short(Work w, Tables t, uint32_t passes) {
+  if (w.report && blockIdx.x == 0 && threadIdx.x < 64) write_report(w);  // (k_report's work: see there)
   if (spec_failed(w)) return;
   constexpr uint32_t NT = ShortCfg<NARROW>::NT;
   extern __shared__ __attribute__((aligned(16))) uint4 s_img[];
@@ -1721,6 +1752,142 @@ __global__ __launch_bounds__(1024) void k_bpe_short(Work w, Tables t, uint32_t p
     class_pass<16, COMPACT, true, NT, ShortCfg<NARROW>::SORTCAP, NARROW, kShortKT>(w, t, P, s_b2id, S, loaded, load, sk, st);
   WgRec::end(w.wgrec, 0, loaded ? 1u : 0u);
 }
+
+// ------------------------------------------------------------------------------------------
+// Sparse 33..64 B class (round 6).  On English-like text class 3 is a few pieces per thousand
+// tiles (C4: ~600 pieces in 322k tiles; C2 or a 1/8 C4 shard: ~70), and the register pass
+// (k_bpe_mid<3>: a thread per piece over 64 slots, ~1,300 VALU per merge) then costs one thread's
+// whole merge chain: 90 us on C2, 190 us on C4 for a few kilobytes.  When k_segment counted at
+// most Work::c3_max of them, the host launches k_bpe_sparse instead: its waves take 64-tile
+// chunks of tcls[3] from a counter and merge each listed piece on the whole wavefront
+// (merge_wave64), its ids into the tile's class-3 region (reserved from rend, as the dropped-byte
+// pass does) and its merged record in mrec -- what the register pass would write.  (Round 6's
+// first build gathered the pieces into a list in a kernel of its own, on a stream forked after
+// k_segment; k_segment appending them instead -- one atomic per tile on one counter -- took C5's
+// k_segment from 1.7 to 5.9 ms; folding the pass into the 17..32 B pass's workgroups put its
+// merge chains at that pass's end, +20..40 us on a 1/8 C4 shard.)
+
+// The merge loop of one <= 64-token piece on a whole wavefront: lane k holds token k (positions
+// stay put) and the value of the pair its token starts (kNoRank when it starts none); the live
+// mask lv (wave-uniform, in SGPRs) marks the lanes that still hold a token.  A merge is a 64-lane
+// minimum of value << 6 | lane (the lowest value, leftmost on ties: src/bpe.rs:118-149, as
+// merge_slots), its neighbours found with scalar bit scans of lv, the two new pairs looked up at
+// once by lanes 0 and 1, and three selects -- a chain of ~40 instructions and one LDS probe per
+// merge where the register pass spends ~1,300 on one lane.  Returns the token count.
+template <bool COMPACT, bool NARROW>
+__device__ __forceinline__ uint32_t merge_wave64(const Tables& t, const PairLds& P, uint32_t& tok, uint32_t rk,
+                                                 uint64_t& lv, uint32_t* err) {
+  const uint32_t lane = threadIdx.x & 63;
+  for (;;) {
+    const uint32_t best = wave_min_full_u32((rk << 6) | lane);
+    const uint32_t r = best >> 6, bi = best & 63u;
+    if (r == kNoRank) break;
+    const uint32_t nid = COMPACT ? r : uni(t.rank_newid[r]);
+    const uint64_t right = lv & ~((2ull << bi) - 1ull);  // live lanes past bi (bi < 63: it starts a pair)
+    const uint32_t p = (uint32_t)__builtin_ctzll(right);  // the right token
+    const uint64_t after = right & (right - 1ull);
+    const bool has_r = after != 0;
+    const uint32_t q = has_r ? (uint32_t)__builtin_ctzll(after) : 0u;  // the token after it
+    const uint64_t left = lv & ((1ull << bi) - 1ull);
+    const bool has_l = left != 0;
+    const uint32_t pv = has_l ? 63u - (uint32_t)__builtin_clzll(left) : 0u;  // the token before
+    const uint32_t L = __builtin_amdgcn_readlane(tok, pv), R = __builtin_amdgcn_readlane(tok, q);
+    uint32_t v = kNoRank;
+    if (lane < 2) {  // lane 0: (L, nid), lane 1: (nid, R)
+      Probe<NARROW, true> pr;
+      pr.start(t, P, lane == 0 ? L : nid, lane == 0 ? nid : R, lane == 0 ? has_l : has_r);
+      v = pr.finish(t, err);
+    }
+    const uint32_t rl = __builtin_amdgcn_readlane(v, 0), rr = __builtin_amdgcn_readlane(v, 1);
+    tok = lane == bi ? nid : tok;
+    rk = (has_l && lane == pv) ? rl : rk;
+    rk = lane == bi ? (has_r ? rr : kNoRank) : rk;
+    rk = lane == p ? kNoRank : rk;
+    lv &= ~(1ull << p);
+  }
+  return (uint32_t)__popcll(lv);
+}
+
+// One wave's share of the sparse class-3 pass (see above); P / s_b2id: the workgroup's LDS image.
+template <bool COMPACT, bool NARROW>
+__device__ __forceinline__ void sparse_c3(const Work& w, const Tables& t, const PairLds& P, const int32_t* s_b2id) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t* cnt3 = w.tcls + 3ull * w.n_tiles;
+  uint32_t* err = &w.counters[2];
+  uint32_t st_bytes = 0, st_ids = 0;
+  for (;;) {
+    // (every lane takes part, lane 0 adding 1: no divergent branch around the atomic)
+    const uint32_t t0 = 64u * uni(atomicAdd(&w.counters[kCtrC3Take], lane == 0 ? 1u : 0u));
+    if (t0 >= w.n_tiles) break;
+    const uint32_t c = t0 + lane < w.n_tiles ? cnt3[t0 + lane] : 0u;
+    uint64_t tiles = __ballot(c != 0);
+    while (tiles) {
+      const uint32_t src = (uint32_t)__builtin_ctzll(tiles);
+      tiles &= tiles - 1ull;
+      const uint32_t tile = t0 + src, n3 = __builtin_amdgcn_readlane(c, src);
+      for (uint32_t q = 0; q < n3; q++) {
+        const uint32_t e = uni(w.list3[(size_t)tile * kCap3 + q]);
+        const uint32_t s = tile * kTile + (e & 0xFFFu), o = ent_ord(e), len = ent_len(e);
+        // lane k: byte k, its token, the value of the byte pair it starts (the 256 x 256 table)
+        const uint32_t b0 = lane < len ? w.text[s + lane] : 0u;
+        const uint32_t b1 = lane + 1 < len ? w.text[s + lane + 1] : 0u;
+        const int32_t id = s_b2id[b0];
+        if (__ballot(lane < len && id < 0)) {  // a byte char absent from the vocab: the generic pass drops it
+          if (lane == 0) {
+            const uint32_t mi = atomicAdd(&w.counters[4], 1u);
+            if (mi < w.mid_cap) w.mid_list[mi] = (uint64_t)s | ((uint64_t)o << 32) | ((uint64_t)len << 48);
+            else atomicOr(&w.counters[kCtrOverflow], 1u);
+          }
+          continue;
+        }
+        uint32_t rk = lane + 1 < len ? t.pair0[(b0 << 8) | b1] : kNoRank;
+        if (rk != kNoRank && value_panics(t, rk)) {
+          atomicOr(err, kErrPanic);
+          rk = kNoRank;
+        }
+        uint32_t tok = (uint32_t)id;
+        uint64_t lv = len >= 64 ? ~0ull : (1ull << len) - 1ull;
+        const uint32_t m = merge_wave64<COMPACT, NARROW>(t, P, tok, rk, lv, err);
+        uint32_t pos = 0;
+        if (lane == 0) pos = atomicAdd(&w.rend[3ull * w.n_tiles + tile], m);
+        pos = uni(pos);
+        if ((lv >> lane) & 1u) w.scratch[(size_t)tile * kTileSlots + pos + __popcll(lv & lanemask_lt())] = tok;
+        CTOK_CHECK_REC(m >= 1 && m <= len && pos + m <= (uint32_t)kTileSlots,
+                       "[ctok check] sparse class 3 tile %u: record m=%u n=%u pos=%u\n", tile, m, len, pos);
+        if (lane == 0) {
+          w.mrec[(size_t)tile * kTileSlots + o] = rec_short(m, pos);
+          atomicAdd(&w.tile_tok[tile], m);
+        }
+        st_bytes += len;
+        st_ids += m;
+      }
+    }
+  }
+  if (lane == 0 && st_bytes) {  // statistics: bytes merged / ids produced by class 3
+    atomicAdd(&w.counters[ctr_stat(3)], st_bytes);
+    atomicAdd(&w.counters[ctr_stat(3) + 1], st_ids);
+  }
+}
+
+constexpr int kSparseWaves = 16;  // waves per k_bpe_sparse workgroup (beside the 96 KiB image: one per CU)
+
+template <bool COMPACT, bool NARROW>
+__global__ __launch_bounds__(64 * kSparseWaves) void k_bpe_sparse(Work w, Tables t) {
+  if (spec_failed(w)) return;
+  WgRec::begin(w.wgrec, 3);
+  extern __shared__ __attribute__((aligned(16))) uint4 s_dyn[];
+  __shared__ int32_t s_b2id[256];
+  const uint32_t tid = threadIdx.x;
+  const uint4* img = NARROW ? t.lds16_image : t.lds_image;
+  for (uint32_t i = tid; i < kLdsImageBytes / 16; i += 64 * kSparseWaves) s_dyn[i] = img[i];
+  for (uint32_t i = tid; i < 256; i += 64 * kSparseWaves) s_b2id[i] = t.byte2id[i];
+  __syncthreads();
+  const PairLds P{(const lds_u64*)s_dyn, (const lds_u32*)(s_dyn + kHotBuckets)};
+  sparse_c3<COMPACT, NARROW>(w, t, P, s_b2id);
+  __syncthreads();
+  WgRec::end(w.wgrec, 3, 1);
+}
+
 
 // Pieces of 17..32 bytes (CLS = 2, on the main stream after k_bpe_short) or 33..64 bytes (CLS = 3,
 // e.g. runs of CJK letters, 3 bytes each): 512-thread workgroups (two waves per SIMD at <= 256
@@ -1794,7 +1961,7 @@ static hipError_t lds_attr_once(LdsAttr& a, const void* fn, size_t bytes) {
 }
 
 template <bool C, int CLS, bool NW>
-static hipError_t launch_mid_t(const Work& w, const Tables& t, hipStream_t s) {
+static hipError_t launch_mid_t(const Work& w, const Tables& t, hipStream_t s, const Lx& x) {
   static LdsAttr attr;
   HIPCHK(lds_attr_once(attr, (const void*)k_bpe_mid<C, CLS, NW>, kLdsImageBytes));
   if (!w.n_tiles) return hipSuccess;
@@ -1803,20 +1970,20 @@ static hipError_t launch_mid_t(const Work& w, const Tables& t, hipStream_t s) {
     if (w.mid_wide) {
       static LdsAttr attr768;
       HIPCHK(lds_attr_once(attr768, (const void*)k_bpe_mid<C, CLS, NW, 768>, kLdsImageBytes));
-      k_bpe_mid<C, CLS, NW, 768><<<grid, 768, kLdsImageBytes, s>>>(w, t);
+      launch_lx(x, k_bpe_mid<C, CLS, NW, 768>, grid, 768, kLdsImageBytes, s, w, t);
       return hipGetLastError();
     }
   }
-  k_bpe_mid<C, CLS, NW><<<grid, 512, kLdsImageBytes, s>>>(w, t);
+  launch_lx(x, k_bpe_mid<C, CLS, NW>, grid, 512, kLdsImageBytes, s, w, t);
   return hipGetLastError();
 }
 template <bool C, int CLS>
-static hipError_t launch_mid(const Work& w, const Tables& t, hipStream_t s) {
-  return t.narrow ? launch_mid_t<C, CLS, true>(w, t, s) : launch_mid_t<C, CLS, false>(w, t, s);
+static hipError_t launch_mid(const Work& w, const Tables& t, hipStream_t s, const Lx& x = {}) {
+  return t.narrow ? launch_mid_t<C, CLS, true>(w, t, s, x) : launch_mid_t<C, CLS, false>(w, t, s, x);
 }
 
 template <bool C, bool NW>
-static hipError_t launch_short_t(const Work& w, const Tables& t, hipStream_t s) {
+static hipError_t launch_short_t(const Work& w, const Tables& t, hipStream_t s, const Lx& x) {
   static LdsAttr attr;
   HIPCHK(lds_attr_once(attr, (const void*)k_bpe_short<C, NW>, kLdsImageBytes));
   if (!w.n_tiles) return hipSuccess;
@@ -1826,27 +1993,47 @@ static hipError_t launch_short_t(const Work& w, const Tables& t, hipStream_t s) 
     k_bpe_short<C, NW><<<grid, ShortCfg<NW>::NT, kLdsImageBytes, s>>>(w, t, 1u);
     k_bpe_short<C, NW><<<grid, ShortCfg<NW>::NT, kLdsImageBytes, s>>>(w, t, 2u);
   } else {
-    k_bpe_short<C, NW><<<grid, ShortCfg<NW>::NT, kLdsImageBytes, s>>>(w, t, 3u);
+    launch_lx(x, k_bpe_short<C, NW>, grid, ShortCfg<NW>::NT, kLdsImageBytes, s, w, t, 3u);
   }
   return hipGetLastError();
 }
 template <bool C>
-static hipError_t launch_short(const Work& w, const Tables& t, hipStream_t s) {
-  return t.narrow ? launch_short_t<C, true>(w, t, s) : launch_short_t<C, false>(w, t, s);
+static hipError_t launch_short(const Work& w, const Tables& t, hipStream_t s, const Lx& x) {
+  return t.narrow ? launch_short_t<C, true>(w, t, s, x) : launch_short_t<C, false>(w, t, s, x);
 }
 
-hipError_t launch_bpe_class(const Work& w, const Tables& t, int cls, hipStream_t s) {
+template <bool C, bool NW>
+static hipError_t launch_sparse_t(const Work& w, const Tables& t, uint32_t n_pieces, hipStream_t s, const Lx& x) {
+  static LdsAttr attr;
+  HIPCHK(lds_attr_once(attr, (const void*)k_bpe_sparse<C, NW>, kLdsImageBytes));
+  // a wave per piece at most, and waves enough to scan the tiles' class-3 counts in 64-tile
+  // chunks about four each
+  const uint32_t chunks = (w.n_tiles + 63) / 64;
+  const uint32_t want = std::max((n_pieces + kSparseWaves - 1) / kSparseWaves, (chunks + 4 * kSparseWaves - 1) / (4 * kSparseWaves));
+  launch_lx(x, k_bpe_sparse<C, NW>, std::max(1u, std::min(want, w.n_cus)), 64 * kSparseWaves, kLdsImageBytes, s, w, t);
+  return hipGetLastError();
+}
+
+hipError_t launch_c3_sparse(const Work& w, const Tables& t, uint32_t n_pieces, hipStream_t s, Lx x) {
+  if (!n_pieces || n_pieces > w.c3_max || !w.n_tiles) return hipSuccess;
+  if (t.compact)
+    return t.narrow ? launch_sparse_t<true, true>(w, t, n_pieces, s, x) : launch_sparse_t<true, false>(w, t, n_pieces, s, x);
+  return t.narrow ? launch_sparse_t<false, true>(w, t, n_pieces, s, x) : launch_sparse_t<false, false>(w, t, n_pieces, s, x);
+}
+
+hipError_t launch_bpe_class(const Work& w, const Tables& t, int cls, hipStream_t s, Lx x) {
   if (t.n_at != 0) {  // every <= 32 B piece is in list0
-    if (cls == 0 && w.n_tiles) k_bpe_generic<false><<<(w.n_tiles + kTilesGeneric - 1) / kTilesGeneric, 256, 0, s>>>(w, t);
+    if (cls == 0 && w.n_tiles)
+      launch_lx(x, k_bpe_generic<false>, (w.n_tiles + kTilesGeneric - 1) / kTilesGeneric, 256, 0, s, w, t);
     return hipGetLastError();
   }
   switch (cls) {
-    case 0: return t.compact ? launch_short<true>(w, t, s) : launch_short<false>(w, t, s);  // classes 0 and 1
-    case 2: return t.compact ? launch_mid<true, 2>(w, t, s) : launch_mid<false, 2>(w, t, s);
-    case 4: return t.compact ? launch_mid<true, 3>(w, t, s) : launch_mid<false, 3>(w, t, s);  // main-stream instance
+    case 0: return t.compact ? launch_short<true>(w, t, s, x) : launch_short<false>(w, t, s, x);  // classes 0 and 1
+    case 2: return t.compact ? launch_mid<true, 2>(w, t, s, x) : launch_mid<false, 2>(w, t, s, x);
+    case 4: return t.compact ? launch_mid<true, 3>(w, t, s, x) : launch_mid<false, 3>(w, t, s, x);  // main-stream instance
     case 3:  // pieces with dropped bytes, found by the merge passes (none when every byte's char is in the vocab)
       if (t.all_bytes) return hipSuccess;
-      k_bpe_generic<true><<<64, 128, 0, s>>>(w, t);
+      launch_lx(x, k_bpe_generic<true>, 64, 128, 0, s, w, t);
       return hipGetLastError();
     default:
       return hipSuccess;
@@ -3058,159 +3245,20 @@ hipError_t launch_bpe_long(const Work& w, const Tables& t, hipStream_t s, uint32
   return t.compact ? launch_mid<true, 3>(w, t, s) : launch_mid<false, 3>(w, t, s);
 }
 
-// ------------------------------------------------------------------------------------------
-// Sparse 33..64 B class (round 6).  On English-like text class 3 is a few pieces per thousand
-// tiles (C4: ~600 pieces in 322k tiles; C2 or a 1/8 C4 shard: ~70), and the register pass
-// (k_bpe_mid<3>: a thread per piece over 64 slots, ~1,300 VALU per merge) then costs one thread's
-// whole merge chain: 90 us on C2, 190 us on C4 for a few kilobytes.  k_c3_list gathers the
-// class-3 list entries into one list (a wave per 64 tiles of tcls, one atomic per wave that meets
-// any); when the host sees at most Work::c3_max of them it launches k_bpe_sparse instead of the
-// register pass: a wavefront per piece (merge_wave64), its ids into the tile's class-3 region
-// (reserved from rend, as the dropped-byte pass does) and its merged record in mrec -- what the
-// register pass would write.
-__global__ __launch_bounds__(256) void k_c3_list(Work w) {
-  if (spec_failed(w)) return;
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t* cnt3 = w.tcls + 3ull * w.n_tiles;
-  for (uint32_t t0 = blockIdx.x * 256 + (threadIdx.x & ~63u); t0 < w.n_tiles; t0 += gridDim.x * 256) {
-    const uint32_t tile = t0 + lane;
-    const uint32_t c = tile < w.n_tiles ? cnt3[tile] : 0u;
-    if (__ballot(c != 0) == 0) continue;  // (wave-uniform)
-    const uint32_t inc = wave_incl_scan(c);
-    uint32_t b = 0;
-    if (lane == 63) b = atomicAdd(&w.counters[kCtrC3Count], inc);
-    b = __builtin_amdgcn_readlane(b, 63) + inc - c;
-    for (uint32_t j = 0; j < c; j++)
-      if (b + j < w.c3_max) w.c3q[b + j] = (tile << 7) | j;
-  }
+
+// The call's report (Work::report): k_segment's counters, the class-3 count among them, into
+// pinned host words, then the call's sequence number (write_report).  k_bpe_short's first wave
+// writes it as that kernel starts (its packet waited for k_segment); this one-wave kernel does it
+// when k_bpe_short does not run (added tokens, no tiles).  The host polls the word instead of
+// copying the counters on a second stream forked by an event after k_segment; having seen it, it
+// knows k_segment has completed, so what it launches next -- on any stream -- needs no fork event.
+__global__ __launch_bounds__(64) void k_report(Work w) {
+  write_report(w);
 }
 
-// The merge loop of one <= 64-token piece on a whole wavefront: lane k holds token k (positions
-// stay put) and the value of the pair its token starts (kNoRank when it starts none); the live
-// mask lv (wave-uniform, in SGPRs) marks the lanes that still hold a token.  A merge is a 64-lane
-// minimum of value << 6 | lane (the lowest value, leftmost on ties: src/bpe.rs:118-149, as
-// merge_slots), its neighbours found with scalar bit scans of lv, the two new pairs looked up at
-// once by lanes 0 and 1, and three selects -- a chain of ~40 instructions and one LDS probe per
-// merge where the register pass spends ~1,300 on one lane.  Returns the token count.
-template <bool COMPACT, bool NARROW>
-__device__ __forceinline__ uint32_t merge_wave64(const Tables& t, const PairLds& P, uint32_t& tok, uint32_t rk,
-                                                 uint64_t& lv, uint32_t* err) {
-  const uint32_t lane = threadIdx.x & 63;
-  for (;;) {
-    const uint32_t best = wave_min_full_u32((rk << 6) | lane);
-    const uint32_t r = best >> 6, bi = best & 63u;
-    if (r == kNoRank) break;
-    const uint32_t nid = COMPACT ? r : uni(t.rank_newid[r]);
-    const uint64_t right = lv & ~((2ull << bi) - 1ull);  // live lanes past bi (bi < 63: it starts a pair)
-    const uint32_t p = (uint32_t)__builtin_ctzll(right);  // the right token
-    const uint64_t after = right & (right - 1ull);
-    const bool has_r = after != 0;
-    const uint32_t q = has_r ? (uint32_t)__builtin_ctzll(after) : 0u;  // the token after it
-    const uint64_t left = lv & ((1ull << bi) - 1ull);
-    const bool has_l = left != 0;
-    const uint32_t pv = has_l ? 63u - (uint32_t)__builtin_clzll(left) : 0u;  // the token before
-    const uint32_t L = __builtin_amdgcn_readlane(tok, pv), R = __builtin_amdgcn_readlane(tok, q);
-    uint32_t v = kNoRank;
-    if (lane < 2) {  // lane 0: (L, nid), lane 1: (nid, R)
-      Probe<NARROW, true> pr;
-      pr.start(t, P, lane == 0 ? L : nid, lane == 0 ? nid : R, lane == 0 ? has_l : has_r);
-      v = pr.finish(t, err);
-    }
-    const uint32_t rl = __builtin_amdgcn_readlane(v, 0), rr = __builtin_amdgcn_readlane(v, 1);
-    tok = lane == bi ? nid : tok;
-    rk = (has_l && lane == pv) ? rl : rk;
-    rk = lane == bi ? (has_r ? rr : kNoRank) : rk;
-    rk = lane == p ? kNoRank : rk;
-    lv &= ~(1ull << p);
-  }
-  return (uint32_t)__popcll(lv);
-}
-
-constexpr int kSparseWaves = 16;  // waves per k_bpe_sparse workgroup (beside the 96 KiB image: one per CU)
-
-template <bool COMPACT, bool NARROW>
-__global__ __launch_bounds__(64 * kSparseWaves) void k_bpe_sparse(Work w, Tables t, uint32_t n) {
-  if (spec_failed(w)) return;
-  WgRec::begin(w.wgrec, 3);
-  extern __shared__ __attribute__((aligned(16))) uint4 s_dyn[];
-  __shared__ int32_t s_b2id[256];
-  const uint32_t tid = threadIdx.x, lane = tid & 63;
-  const uint4* img = NARROW ? t.lds16_image : t.lds_image;
-  for (uint32_t i = tid; i < kLdsImageBytes / 16; i += 64 * kSparseWaves) s_dyn[i] = img[i];
-  for (uint32_t i = tid; i < 256; i += 64 * kSparseWaves) s_b2id[i] = t.byte2id[i];
-  __syncthreads();
-  const PairLds P{(const lds_u64*)s_dyn, (const lds_u32*)(s_dyn + kHotBuckets)};
-  uint32_t* err = &w.counters[2];
-  uint32_t st_bytes = 0, st_ids = 0;
-  for (;;) {
-    // (every lane takes part, lane 0 adding 1: no divergent branch around the atomic)
-    const uint32_t k = uni(atomicAdd(&w.counters[kCtrC3Take], lane == 0 ? 1u : 0u));
-    if (k >= n) break;
-    const uint32_t qe = uni(w.c3q[k]);
-    const uint32_t tile = qe >> 7;
-    const uint32_t e = uni(w.list3[(size_t)tile * kCap3 + (qe & 127u)]);
-    const uint32_t s = tile * kTile + (e & 0xFFFu), o = ent_ord(e), len = ent_len(e);
-    // lane k: byte k, its token, the value of the byte pair it starts (the 256 x 256 table)
-    const uint32_t b0 = lane < len ? w.text[s + lane] : 0u;
-    const uint32_t b1 = lane + 1 < len ? w.text[s + lane + 1] : 0u;
-    const int32_t id = s_b2id[b0];
-    if (__ballot(lane < len && id < 0)) {  // a byte char absent from the vocab: the generic pass drops it
-      if (lane == 0) {
-        const uint32_t mi = atomicAdd(&w.counters[4], 1u);
-        if (mi < w.mid_cap) w.mid_list[mi] = (uint64_t)s | ((uint64_t)o << 32) | ((uint64_t)len << 48);
-        else atomicOr(&w.counters[kCtrOverflow], 1u);
-      }
-      continue;
-    }
-    uint32_t rk = lane + 1 < len ? t.pair0[(b0 << 8) | b1] : kNoRank;
-    if (rk != kNoRank && value_panics(t, rk)) {
-      atomicOr(err, kErrPanic);
-      rk = kNoRank;
-    }
-    uint32_t tok = (uint32_t)id;
-    uint64_t lv = len >= 64 ? ~0ull : (1ull << len) - 1ull;
-    const uint32_t m = merge_wave64<COMPACT, NARROW>(t, P, tok, rk, lv, err);
-    uint32_t pos = 0;
-    if (lane == 0) pos = atomicAdd(&w.rend[3ull * w.n_tiles + tile], m);
-    pos = uni(pos);
-    if ((lv >> lane) & 1u) w.scratch[(size_t)tile * kTileSlots + pos + __popcll(lv & lanemask_lt())] = tok;
-    CTOK_CHECK_REC(m >= 1 && m <= len && pos + m <= (uint32_t)kTileSlots,
-                   "[ctok check] k_bpe_sparse tile %u: record m=%u n=%u pos=%u\n", tile, m, len, pos);
-    if (lane == 0) {
-      w.mrec[(size_t)tile * kTileSlots + o] = rec_short(m, pos);
-      atomicAdd(&w.tile_tok[tile], m);
-    }
-    st_bytes += len;
-    st_ids += m;
-  }
-  if (lane == 0 && st_bytes) {  // statistics: bytes merged / ids produced by class 3
-    atomicAdd(&w.counters[ctr_stat(3)], st_bytes);
-    atomicAdd(&w.counters[ctr_stat(3) + 1], st_ids);
-  }
-  __syncthreads();
-  WgRec::end(w.wgrec, 3, 1);
-}
-
-hipError_t launch_c3_list(const Work& w, hipStream_t s) {
-  if (!w.n_tiles || !w.c3_max) return hipSuccess;
-  const uint32_t grid = std::max(1u, std::min((w.n_tiles + 255) / 256, 4 * w.n_cus));
-  k_c3_list<<<grid, 256, 0, s>>>(w);
+hipError_t launch_report(const Work& w, hipStream_t s) {
+  k_report<<<1, 64, 0, s>>>(w);
   return hipGetLastError();
-}
-
-template <bool C, bool NW>
-static hipError_t launch_sparse_t(const Work& w, const Tables& t, uint32_t n_pieces, hipStream_t s) {
-  static LdsAttr attr;
-  HIPCHK(lds_attr_once(attr, (const void*)k_bpe_sparse<C, NW>, kLdsImageBytes));
-  const uint32_t grid = std::max(1u, std::min((n_pieces + kSparseWaves - 1) / kSparseWaves, w.n_cus));
-  k_bpe_sparse<C, NW><<<grid, 64 * kSparseWaves, kLdsImageBytes, s>>>(w, t, n_pieces);
-  return hipGetLastError();
-}
-
-hipError_t launch_c3_sparse(const Work& w, const Tables& t, uint32_t n_pieces, hipStream_t s) {
-  if (!n_pieces || n_pieces > w.c3_max) return hipSuccess;
-  if (t.compact) return t.narrow ? launch_sparse_t<true, true>(w, t, n_pieces, s) : launch_sparse_t<true, false>(w, t, n_pieces, s);
-  return t.narrow ? launch_sparse_t<false, true>(w, t, n_pieces, s) : launch_sparse_t<false, false>(w, t, n_pieces, s);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -3544,15 +3592,16 @@ __global__ void k_tokoff(Work w, uint64_t* __restrict__ tok_off) {
 }
 
 hipError_t launch_emit(const Work& w, uint32_t* ids, uint64_t ids_cap, uint64_t* tok_off, hipStream_t s,
-                       bool count_pieces, bool empty_docs) {
-  HIPCHK(scan_tiles(w, s, count_pieces));
+                       bool count_pieces, bool empty_docs, Lx first, Lx last) {
+  HIPCHK(scan_tiles(w, s, count_pieces, first));
   if (w.n_tiles) {
     const uint32_t nb = (w.n_tiles + kEmitWaves - 1) / kEmitWaves;
     if (w.rec16) k_emit<uint16_t><<<nb, 64 * kEmitWaves, 0, s>>>(w, ids, ids_cap, tok_off);
     else k_emit<uint32_t><<<nb, 64 * kEmitWaves, 0, s>>>(w, ids, ids_cap, tok_off);
   }
   // (grid-stride: with no empty document only tok_off[n_docs] is left to write)
-  k_tokoff<<<empty_docs ? std::min<uint32_t>((w.n_docs + 1 + 255) / 256, 4096) : 1u, 256, 0, s>>>(w, tok_off);
+  launch_lx(last, k_tokoff, empty_docs ? std::min<uint32_t>((w.n_docs + 1 + 255) / 256, 4096) : 1u, 256, 0, s, w,
+            tok_off);
   return hipGetLastError();
 }
 
@@ -3714,16 +3763,16 @@ uint64_t tile_scan_tmp_elems(uint64_t n_tiles) {
   return nb + 1 + scan_tmp_elems(nb + 1);
 }
 
-hipError_t scan_tiles(const Work& w, hipStream_t s, bool count) {
+hipError_t scan_tiles(const Work& w, hipStream_t s, bool count, Lx x) {
   const uint64_t nb = ((uint64_t)w.n_tiles + kTileScanBlock - 1) / kTileScanBlock;
   if (nb <= 1) {
-    k_tiles_apply<<<1, 256, 0, s>>>(w, nullptr, count ? 1u : 0u);
+    launch_lx(x, k_tiles_apply, 1, 256, 0, s, w, (const uint64_t*)nullptr, count ? 1u : 0u);
     return hipGetLastError();
   }
   uint64_t* part = reinterpret_cast<uint64_t*>(w.scan_tmp);
   const uint64_t cap = w.scan_tmp_cap / 2;
   if (nb + 1 > cap) return hipErrorInvalidValue;
-  k_tiles_reduce<<<(unsigned)nb, 256, 0, s>>>(w, part);
+  launch_lx(x, k_tiles_reduce, (unsigned)nb, 256, 0, s, w, part);
   HIPCHK(hipGetLastError());
   HIPCHK(scan_u64(part, nb, part + nb + 1, cap - nb - 1, s));
   k_tiles_apply<<<(unsigned)nb, 256, 0, s>>>(w, part, count ? 1u : 0u);
