@@ -25,6 +25,12 @@ for step in "$@"; do
       if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "tests: exit $rc"; exit 1; fi
       grep -E "^(FAILED|ERROR)" "$OUT/gpu_tests.log" || true
       if [ -n "$STRICT" ] && [ $rc -ne 0 ]; then echo "tests: failures (STRICT): session ends"; exit 1; fi ;;
+    checksuite)  # the whole GPU suite on the range-checking build (abl/check.so: tools/build_variant.sh worktree abl/check.so -DCTOK_CHECK)
+      rc=0
+      CTOK_LIB=$ROOT/abl/check.so timeout -k 10 1000 python -u -m pytest tests -m gpu -q --maxfail=3 --timeout 900 --timeout-method thread \
+        > "$OUT/check_suite.log" 2>&1 || rc=$?
+      tail -2 "$OUT/check_suite.log"
+      if [ $rc -ne 0 ]; then echo "checksuite: exit $rc"; exit 1; fi ;;
     ptest:*)  # a subset of the GPU tests: ptest:FILE[,FILE...] (paths under tests/)
       rc=0; files=$(echo "${step#ptest:}" | tr , ' ' | sed 's|\([^ ]*\)|tests/\1|g')
       timeout -k 10 900 python -u -m pytest $files -m gpu -v --maxfail=5 --timeout 600 --timeout-method thread \
