@@ -250,7 +250,7 @@ struct DeviceState {
   DevBuf<uint64_t> stamps;  // diagnostic builds (CTOK_SEG_STAMPS) with CTOK_STAMPS=1
   DevBuf<uint64_t> wgrec;   // diagnostic: CTOK_WGREC=1
   DevBuf<uint16_t> wpref;
-  DevBuf<uint32_t> long_cnt, long_ord, long_hist;
+  DevBuf<uint32_t> long_cnt, long_ord, long_hist, c3q, c3pre;
   DevBuf<uint64_t> long_list, mid_list, scan_tmp, scan_tmp2;
   DevBuf<uint32_t> doc_flag, ncp;
   // NFC splice (nfc_splice): flagged-doc ranks / sub-batch positions, the speculative pass's
@@ -285,7 +285,7 @@ struct DeviceState {
     auto add = [&](const auto& x) { b += (uint64_t)x.cap * sizeof(*x.p); };
     add(tfirst), add(pbits), add(tile_np), add(tile_tok), add(tile_doc), add(tcls), add(list0), add(list1);
     add(list2), add(list3), add(tcnt), add(prec), add(mrec), add(pdoc), add(scratch), add(counters), add(lids), add(lw), add(tregion), add(rend);
-    add(wpref), add(long_cnt), add(long_ord), add(long_hist), add(long_pos), add(lw_pos), add(lwn), add(long_list);
+    add(wpref), add(long_cnt), add(long_ord), add(long_hist), add(long_pos), add(lw_pos), add(lwn), add(long_list), add(c3q), add(c3pre);
     add(mid_list), add(scan_tmp), add(scan_tmp2), add(cps);
     add(doc_flag), add(ncp), add(norm_off), add(norm_text);
     add(nfc_bits), add(spl_rank), add(spl_ids), add(sub_ids), add(spl_pos), add(spl_toff), add(sub_off), add(sub_toff), add(sub_text);
@@ -1809,12 +1809,25 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   w.counters = ds->counters.p;
   w.scan_tmp = (uint32_t*)ds->scan_tmp.p;
   w.scan_tmp_cap = ds->scan_tmp.cap * 2;
-  // sparse class 3: at most c3_max pieces of 33..64 B are merged a wavefront each, by the 17..32 B
-  // pass's workgroups, instead of by the register pass (CTOK_C3_SPARSE=n sets the bound, 0
-  // disables) (read per call: the GPU tests switch it within one process)
+  // sparse class 3 (k_bpe_sparse): at most c3_limit pieces of 33..64 B are merged a wavefront
+  // each instead of by the register pass -- by default the class is sparse at <= 1 piece per 16
+  // tiles (English text: C4 ~600 in 322k tiles; C5-NFC's sub-batch of CJK-heavy documents, ~17
+  // per tile, is faster in the register pass), up to kC3SparseDefault; CTOK_C3_SPARSE=n sets the
+  // bound (0 disables), read per call (the GPU tests switch it within one process).  k_segment
+  // queues the pieces in c3q: capacity the bound (at most one piece per 33 bytes) rounded up to
+  // whole shards.
   const char* c3_var = getenv("CTOK_C3_SPARSE");
-  const uint64_t c3_env = c3_var ? strtoull(c3_var, nullptr, 10) : kC3SparseDefault;
-  w.c3_max = tb.n_at == 0 ? (uint32_t)std::min<uint64_t>(c3_env, 0xFFFFFFFFull) : 0u;
+  const uint64_t c3_limit = tb.n_at != 0 ? 0ull
+                            : c3_var     ? strtoull(c3_var, nullptr, 10)
+                                         : std::min<uint64_t>(kC3SparseDefault, std::max<uint64_t>(64, nt / 16));
+  const uint64_t c3_cap = std::min<uint64_t>(c3_limit, B / 33 + 64);
+  w.c3_max = c3_limit ? (uint32_t)((c3_cap + kC3Shards - 1) / kC3Shards * kC3Shards) : 0u;
+  if (w.c3_max) {
+    ds->c3q.ensure(w.c3_max + 8);
+    ds->c3pre.ensure(kC3Shards + 8);
+    w.c3q = ds->c3q.p;
+    w.c3pre = ds->c3pre.p;
+  }
 #ifdef CTOK_CHECK
   // (range-checking build: every merged record starts out of range, so one no pass wrote traps)
   HIPTRY(hipMemsetAsync(ds->mrec.p, 0xFF, (size_t)nt * kTileSlots * 4, s));
@@ -1906,7 +1919,7 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
     HIPTRY(hipEventRecord(ds->ev_tot, ds->side));
   }
   const uint32_t c3n = seg_cnt[kCtrC3Count];
-  const bool c3_sparse = c3n != 0 && c3n <= w.c3_max;
+  const bool c3_sparse = c3n != 0 && c3n <= c3_limit && c3n <= w.c3_max;  // (all ones: a shard overflowed)
   // Without long pieces the side stream is idle: the 17..32 B pass goes there (CTOK_OVERLAP=0: on
   // the main stream after k_bpe_short), so its workgroups take the CUs k_bpe_short's free at its
   // end, beside the 33..64 B pass on the main stream (the classes' pieces, regions and records are

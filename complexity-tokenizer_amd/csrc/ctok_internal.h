@@ -37,8 +37,8 @@ constexpr uint32_t kCap0 = kTile, kCap1 = (kTile + 8) / 9, kCap2 = (kTile + 16) 
 constexpr uint32_t kCap0Lean = 1040;  // (65 lines per tile: a power-of-two stride put every tile's list on one memory channel)
 constexpr int kNumClasses = 4;
 constexpr int kNumCounters = 32;
-// the counters buffer: kNumCounters words, then kC3Shards class-3 counts (k_segment adds tile t's
-// class-3 pieces to shard t % kC3Shards; the report sums them into counters[kCtrC3Count])
+// the counters buffer: kNumCounters words, then kC3Shards class-3 counts (k_segment queues tile t's
+// class-3 pieces in shard t % kC3Shards; the report sums them into counters[kCtrC3Count])
 constexpr int kC3Shards = 64;
 constexpr int kCounterWords = kNumCounters + kC3Shards;
 // counters[] slots of class pass c: bytes merged / ids produced (statistics), next chunk
@@ -48,8 +48,8 @@ constexpr int kCtrAnyMid = 19;  // counters[19] != 0: some tile has a class-2 pi
 constexpr int kCtrAnyC3 = 20;   // counters[20] != 0: some tile has a class-3 piece
 constexpr int kCtrEmptyDocs = 21;  // counters[21]: empty documents (k_tilefirst); 0: k_emit writes tok_off
 constexpr int kCtrC3Count = 22;    // counters[22] of the report: class-3 pieces (the shards' sum)
-constexpr int kCtrC3Take = 23;     // counters[23]: next 64-tile chunk of the sparse class-3 pass
-constexpr uint32_t kC3SparseDefault = 65536;  // Work::c3_max unless CTOK_C3_SPARSE says otherwise
+constexpr int kCtrC3Take = 23;     // counters[23]: next piece of the sparse class-3 pass
+constexpr uint32_t kC3SparseDefault = 65536;  // the most pieces the sparse class-3 path takes by default (ctok_host.cpp)
 constexpr uint32_t kWgRecWords = 4 * 1024 * 4;  // Work::wgrec: 4 kernels x 1024 workgroups x 4 words
 constexpr int kOverlapDefault = 1;             // merge passes on the side stream without long pieces (CTOK_OVERLAP)
 constexpr int kCtrSink = 31;       // counters[31]: panic bits of lookups whose pairs need not exist (discarded)
@@ -282,7 +282,10 @@ struct Work {              // device pointers, sized by the host for one call
   uint32_t* scan_tmp;      // scan partials
   uint64_t scan_tmp_cap;
   uint64_t* stamps;        // diagnostic builds only (CTOK_SEG_STAMPS): 8 u64 per tile, else null
-  uint32_t c3_max;         // the sparse path takes class 3 when it holds at most this many pieces (0: never)
+  uint32_t c3_max;         // the sparse path takes class 3 when it holds at most this many pieces (0: never;
+                           // a multiple of kC3Shards: each shard of c3q holds c3_max / kC3Shards)
+  uint32_t* c3q;           // [c3_max] class-3 pieces as tile << 7 | list index, in kC3Shards shards (k_segment)
+  uint32_t* c3pre;         // [kC3Shards + 1] the shards' exclusive prefix (the report writer), for k_bpe_sparse
   uint64_t* host_res;      // pinned host words (device pointer): k_tokoff writes the token count to [0] and
                            // the counters to [1 ..] (null: the host copies them)
   uint64_t* wgrec;         // diagnostic (CTOK_WGREC=1): per-workgroup start / end / CU of the merge passes, else null

@@ -59,9 +59,22 @@ constexpr uint32_t kSel = kNoRank - 1;  // marks a merge site during a parallel 
 // system-scope release, then the call's sequence number (see k_report).
 __device__ __forceinline__ void write_report(const Work& w) {
   const uint32_t lane = threadIdx.x & 63;
-  uint32_t c3 = w.counters[kNumCounters + lane];  // (kC3Shards == 64: one shard per lane)
+  // the class-3 shards (kC3Shards == 64: one per lane): their exclusive prefix into c3pre for
+  // k_bpe_sparse, their sum into the report (all ones when a shard overflowed its capacity)
+  uint32_t c3 = 0;
+  if (w.c3_max) {
+    const uint32_t c = w.counters[kNumCounters + lane];
+    uint32_t inc = c;
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) c3 += (uint32_t)__shfl_xor((int)c3, o, 64);
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t v = (uint32_t)__shfl_up((int)inc, o, 64);
+      if (lane >= (uint32_t)o) inc += v;
+    }
+    w.c3pre[lane] = inc - c;
+    if (lane == 63) w.c3pre[64] = inc;
+    c3 = __shfl((int)inc, 63, 64);
+    if (__ballot(c > w.c3_max / kC3Shards)) c3 = ~0u;
+  }
   if (lane < (uint32_t)kNumCounters) w.report[lane] = lane == (uint32_t)kCtrC3Count ? c3 : w.counters[lane];
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -945,9 +958,18 @@ __global__ __launch_bounds__(64 * kSegWaves) __attribute__((amdgpu_waves_per_eu(
     w.tcls[(size_t)lane * w.n_tiles + tile] = lane == 0 ? n0 : lane == 1 ? n1 : lane == 2 ? n2 : n3;
   if (lane == 0 && n2) w.counters[kCtrAnyMid] = 1;  // plain stores: every writer stores 1
   if (lane == 0 && n3) w.counters[kCtrAnyC3] = 1;
-  // the class-3 count (the host's choice of the sparse path): one of kC3Shards counters per tile
-  // (one counter for every tile: C5 k_segment 1.7 -> 5.9 ms, its atomics serialised on one address)
-  if (lane == 0 && n3) atomicAdd(&w.counters[kNumCounters + (tile & (kC3Shards - 1))], n3);
+  // the sparse class-3 queue (k_bpe_sparse): the tile's class-3 entries into one of kC3Shards
+  // shards, its count into the shard's counter (one counter for every tile: C5 k_segment
+  // 1.7 -> 5.9 ms, its atomics serialised on one address); a shard that overflows its capacity
+  // keeps counting, and the report then steers the call to the register pass
+  if (n3 && w.c3_max) {
+    const uint32_t sh = tile & (kC3Shards - 1), cap = w.c3_max / kC3Shards;
+    uint32_t b = 0;
+    if (lane == 0) b = atomicAdd(&w.counters[kNumCounters + sh], n3);
+    b = __builtin_amdgcn_readfirstlane(b);
+    for (uint32_t j = lane; j < n3; j += 64)
+      if (b + j < cap) w.c3q[(size_t)sh * cap + b + j] = (tile << 7) | j;
+  }
   SEG_STAMP(5);
 #ifdef CTOK_SEG_STAMPS
   if (w.stamps && lane == 0) w.stamps[(size_t)tile * 8 + 6] = np;
@@ -1757,15 +1779,18 @@ __global__ __launch_bounds__(1024) void k_bpe_short(Work w, Tables t, uint32_t p
 // Sparse 33..64 B class (round 6).  On English-like text class 3 is a few pieces per thousand
 // tiles (C4: ~600 pieces in 322k tiles; C2 or a 1/8 C4 shard: ~70), and the register pass
 // (k_bpe_mid<3>: a thread per piece over 64 slots, ~1,300 VALU per merge) then costs one thread's
-// whole merge chain: 90 us on C2, 190 us on C4 for a few kilobytes.  When k_segment counted at
-// most Work::c3_max of them, the host launches k_bpe_sparse instead: its waves take 64-tile
-// chunks of tcls[3] from a counter and merge each listed piece on the whole wavefront
-// (merge_wave64), its ids into the tile's class-3 region (reserved from rend, as the dropped-byte
-// pass does) and its merged record in mrec -- what the register pass would write.  (Round 6's
-// first build gathered the pieces into a list in a kernel of its own, on a stream forked after
-// k_segment; k_segment appending them instead -- one atomic per tile on one counter -- took C5's
-// k_segment from 1.7 to 5.9 ms; folding the pass into the 17..32 B pass's workgroups put its
-// merge chains at that pass's end, +20..40 us on a 1/8 C4 shard.)
+// whole merge chain: 90 us on C2, 190 us on C4 for a few kilobytes.  k_segment queues each tile's
+// class-3 pieces in one of 64 shards (Work::c3q; a shard per tile % 64, so its atomics spread
+// over 64 counters); when the report counts at most Work::c3_max of them, the host launches
+// k_bpe_sparse instead of the register pass: its waves take the queue's pieces one at a time from
+// a counter and merge each on the whole wavefront (merge_wave64), its ids into the tile's class-3
+// region (reserved from rend, as the dropped-byte pass does) and its merged record in mrec --
+// what the register pass would write.  (Round 6's first build gathered the list in a kernel of
+// its own, on a stream forked after k_segment; k_segment appending to one list -- one atomic per
+// tile on one counter -- took C5's k_segment from 1.7 to 5.9 ms; folding the pass into the 17..32
+// B pass's workgroups put its merge chains at that pass's end, +20..40 us on a 1/8 C4 shard; waves
+// scanning 64-tile chunks of the class counts themselves left a dense chunk's pieces to one wave:
+// C5-NFC's sub-batch 2.4 -> 17 ms.)
 
 // The merge loop of one <= 64-token piece on a whole wavefront: lane k holds token k (positions
 // stay put) and the value of the pair its token starts (kNoRank when it starts none); the live
@@ -1808,60 +1833,59 @@ __device__ __forceinline__ uint32_t merge_wave64(const Tables& t, const PairLds&
   return (uint32_t)__popcll(lv);
 }
 
-// One wave's share of the sparse class-3 pass (see above); P / s_b2id: the workgroup's LDS image.
+// One wave's share of the sparse class-3 pass (see above): n pieces in the sharded queue c3q
+// (shard i: pieces c3pre[i] .. c3pre[i + 1] - 1 of the pass, at c3q + i * cap); P / s_b2id: the
+// workgroup's LDS image.
 template <bool COMPACT, bool NARROW>
-__device__ __forceinline__ void sparse_c3(const Work& w, const Tables& t, const PairLds& P, const int32_t* s_b2id) {
+__device__ __forceinline__ void sparse_c3(const Work& w, const Tables& t, const PairLds& P, const int32_t* s_b2id,
+                                          uint32_t n) {
   const uint32_t lane = threadIdx.x & 63;
-  const uint32_t* cnt3 = w.tcls + 3ull * w.n_tiles;
+  const uint32_t cap = w.c3_max / kC3Shards;
+  const uint32_t pre = w.c3pre[lane];  // (kC3Shards == 64: shard `lane`'s first piece)
   uint32_t* err = &w.counters[2];
   uint32_t st_bytes = 0, st_ids = 0;
   for (;;) {
     // (every lane takes part, lane 0 adding 1: no divergent branch around the atomic)
-    const uint32_t t0 = 64u * uni(atomicAdd(&w.counters[kCtrC3Take], lane == 0 ? 1u : 0u));
-    if (t0 >= w.n_tiles) break;
-    const uint32_t c = t0 + lane < w.n_tiles ? cnt3[t0 + lane] : 0u;
-    uint64_t tiles = __ballot(c != 0);
-    while (tiles) {
-      const uint32_t src = (uint32_t)__builtin_ctzll(tiles);
-      tiles &= tiles - 1ull;
-      const uint32_t tile = t0 + src, n3 = __builtin_amdgcn_readlane(c, src);
-      for (uint32_t q = 0; q < n3; q++) {
-        const uint32_t e = uni(w.list3[(size_t)tile * kCap3 + q]);
-        const uint32_t s = tile * kTile + (e & 0xFFFu), o = ent_ord(e), len = ent_len(e);
-        // lane k: byte k, its token, the value of the byte pair it starts (the 256 x 256 table)
-        const uint32_t b0 = lane < len ? w.text[s + lane] : 0u;
-        const uint32_t b1 = lane + 1 < len ? w.text[s + lane + 1] : 0u;
-        const int32_t id = s_b2id[b0];
-        if (__ballot(lane < len && id < 0)) {  // a byte char absent from the vocab: the generic pass drops it
-          if (lane == 0) {
-            const uint32_t mi = atomicAdd(&w.counters[4], 1u);
-            if (mi < w.mid_cap) w.mid_list[mi] = (uint64_t)s | ((uint64_t)o << 32) | ((uint64_t)len << 48);
-            else atomicOr(&w.counters[kCtrOverflow], 1u);
-          }
-          continue;
-        }
-        uint32_t rk = lane + 1 < len ? t.pair0[(b0 << 8) | b1] : kNoRank;
-        if (rk != kNoRank && value_panics(t, rk)) {
-          atomicOr(err, kErrPanic);
-          rk = kNoRank;
-        }
-        uint32_t tok = (uint32_t)id;
-        uint64_t lv = len >= 64 ? ~0ull : (1ull << len) - 1ull;
-        const uint32_t m = merge_wave64<COMPACT, NARROW>(t, P, tok, rk, lv, err);
-        uint32_t pos = 0;
-        if (lane == 0) pos = atomicAdd(&w.rend[3ull * w.n_tiles + tile], m);
-        pos = uni(pos);
-        if ((lv >> lane) & 1u) w.scratch[(size_t)tile * kTileSlots + pos + __popcll(lv & lanemask_lt())] = tok;
-        CTOK_CHECK_REC(m >= 1 && m <= len && pos + m <= (uint32_t)kTileSlots,
-                       "[ctok check] sparse class 3 tile %u: record m=%u n=%u pos=%u\n", tile, m, len, pos);
-        if (lane == 0) {
-          w.mrec[(size_t)tile * kTileSlots + o] = rec_short(m, pos);
-          atomicAdd(&w.tile_tok[tile], m);
-        }
-        st_bytes += len;
-        st_ids += m;
+    const uint32_t k = uni(atomicAdd(&w.counters[kCtrC3Take], lane == 0 ? 1u : 0u));
+    if (k >= n) break;
+    // its shard: the last one starting at or before k (empty shards share their successor's start)
+    const uint32_t sh = 63u - (uint32_t)__builtin_clzll(__ballot(pre <= k));
+    const uint32_t qe = uni(w.c3q[(size_t)sh * cap + (k - __builtin_amdgcn_readlane(pre, sh))]);
+    const uint32_t tile = qe >> 7;
+    const uint32_t e = uni(w.list3[(size_t)tile * kCap3 + (qe & 127u)]);
+    const uint32_t s = tile * kTile + (e & 0xFFFu), o = ent_ord(e), len = ent_len(e);
+    // lane k: byte k, its token, the value of the byte pair it starts (the 256 x 256 table)
+    const uint32_t b0 = lane < len ? w.text[s + lane] : 0u;
+    const uint32_t b1 = lane + 1 < len ? w.text[s + lane + 1] : 0u;
+    const int32_t id = s_b2id[b0];
+    if (__ballot(lane < len && id < 0)) {  // a byte char absent from the vocab: the generic pass drops it
+      if (lane == 0) {
+        const uint32_t mi = atomicAdd(&w.counters[4], 1u);
+        if (mi < w.mid_cap) w.mid_list[mi] = (uint64_t)s | ((uint64_t)o << 32) | ((uint64_t)len << 48);
+        else atomicOr(&w.counters[kCtrOverflow], 1u);
       }
+      continue;
     }
+    uint32_t rk = lane + 1 < len ? t.pair0[(b0 << 8) | b1] : kNoRank;
+    if (rk != kNoRank && value_panics(t, rk)) {
+      atomicOr(err, kErrPanic);
+      rk = kNoRank;
+    }
+    uint32_t tok = (uint32_t)id;
+    uint64_t lv = len >= 64 ? ~0ull : (1ull << len) - 1ull;
+    const uint32_t m = merge_wave64<COMPACT, NARROW>(t, P, tok, rk, lv, err);
+    uint32_t pos = 0;
+    if (lane == 0) pos = atomicAdd(&w.rend[3ull * w.n_tiles + tile], m);
+    pos = uni(pos);
+    if ((lv >> lane) & 1u) w.scratch[(size_t)tile * kTileSlots + pos + __popcll(lv & lanemask_lt())] = tok;
+    CTOK_CHECK_REC(m >= 1 && m <= len && pos + m <= (uint32_t)kTileSlots,
+                   "[ctok check] sparse class 3 tile %u: record m=%u n=%u pos=%u\n", tile, m, len, pos);
+    if (lane == 0) {
+      w.mrec[(size_t)tile * kTileSlots + o] = rec_short(m, pos);
+      atomicAdd(&w.tile_tok[tile], m);
+    }
+    st_bytes += len;
+    st_ids += m;
   }
   if (lane == 0 && st_bytes) {  // statistics: bytes merged / ids produced by class 3
     atomicAdd(&w.counters[ctr_stat(3)], st_bytes);
@@ -1872,7 +1896,7 @@ __device__ __forceinline__ void sparse_c3(const Work& w, const Tables& t, const 
 constexpr int kSparseWaves = 16;  // waves per k_bpe_sparse workgroup (beside the 96 KiB image: one per CU)
 
 template <bool COMPACT, bool NARROW>
-__global__ __launch_bounds__(64 * kSparseWaves) void k_bpe_sparse(Work w, Tables t) {
+__global__ __launch_bounds__(64 * kSparseWaves) void k_bpe_sparse(Work w, Tables t, uint32_t n) {
   if (spec_failed(w)) return;
   WgRec::begin(w.wgrec, 3);
   extern __shared__ __attribute__((aligned(16))) uint4 s_dyn[];
@@ -1883,7 +1907,7 @@ __global__ __launch_bounds__(64 * kSparseWaves) void k_bpe_sparse(Work w, Tables
   for (uint32_t i = tid; i < 256; i += 64 * kSparseWaves) s_b2id[i] = t.byte2id[i];
   __syncthreads();
   const PairLds P{(const lds_u64*)s_dyn, (const lds_u32*)(s_dyn + kHotBuckets)};
-  sparse_c3<COMPACT, NARROW>(w, t, P, s_b2id);
+  sparse_c3<COMPACT, NARROW>(w, t, P, s_b2id, n);
   __syncthreads();
   WgRec::end(w.wgrec, 3, 1);
 }
@@ -2006,11 +2030,8 @@ template <bool C, bool NW>
 static hipError_t launch_sparse_t(const Work& w, const Tables& t, uint32_t n_pieces, hipStream_t s, const Lx& x) {
   static LdsAttr attr;
   HIPCHK(lds_attr_once(attr, (const void*)k_bpe_sparse<C, NW>, kLdsImageBytes));
-  // a wave per piece at most, and waves enough to scan the tiles' class-3 counts in 64-tile
-  // chunks about four each
-  const uint32_t chunks = (w.n_tiles + 63) / 64;
-  const uint32_t want = std::max((n_pieces + kSparseWaves - 1) / kSparseWaves, (chunks + 4 * kSparseWaves - 1) / (4 * kSparseWaves));
-  launch_lx(x, k_bpe_sparse<C, NW>, std::max(1u, std::min(want, w.n_cus)), 64 * kSparseWaves, kLdsImageBytes, s, w, t);
+  const uint32_t grid = std::max(1u, std::min((n_pieces + kSparseWaves - 1) / kSparseWaves, w.n_cus));  // (a wave per piece at most)
+  launch_lx(x, k_bpe_sparse<C, NW>, grid, 64 * kSparseWaves, kLdsImageBytes, s, w, t, n_pieces);
   return hipGetLastError();
 }
 
