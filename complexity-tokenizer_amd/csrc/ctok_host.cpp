@@ -1814,14 +1814,16 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   // tiles (English text: C4 ~600 in 322k tiles; C5-NFC's sub-batch of CJK-heavy documents, ~17
   // per tile, is faster in the register pass), up to kC3SparseDefault; CTOK_C3_SPARSE=n sets the
   // bound (0 disables), read per call (the GPU tests switch it within one process).  k_segment
-  // queues the pieces in c3q: capacity the bound (at most one piece per 33 bytes) rounded up to
-  // whole shards.
+  // queues the pieces in c3q's 64 shards (shard = tile % 64): capacity the bound rounded up to
+  // whole shards, at most what a shard's tiles can hold (kCap3 each) -- a bound that large never
+  // overflows; a smaller one overflows when the pieces crowd into a few tiles, and the call then
+  // takes the register pass (locally dense: the faster one there).
   const char* c3_var = getenv("CTOK_C3_SPARSE");
   const uint64_t c3_limit = tb.n_at != 0 ? 0ull
                             : c3_var     ? strtoull(c3_var, nullptr, 10)
                                          : std::min<uint64_t>(kC3SparseDefault, std::max<uint64_t>(64, nt / 16));
-  const uint64_t c3_cap = std::min<uint64_t>(c3_limit, B / 33 + 64);
-  w.c3_max = c3_limit ? (uint32_t)((c3_cap + kC3Shards - 1) / kC3Shards * kC3Shards) : 0u;
+  const uint64_t c3_most = (uint64_t)kCap3 * ((nt + kC3Shards - 1) / kC3Shards) * kC3Shards;
+  w.c3_max = c3_limit ? (uint32_t)std::min<uint64_t>((c3_limit + kC3Shards - 1) / kC3Shards * kC3Shards, c3_most) : 0u;
   if (w.c3_max) {
     ds->c3q.ensure(w.c3_max + 8);
     ds->c3pre.ensure(kC3Shards + 8);

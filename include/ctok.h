@@ -123,20 +123,20 @@ typedef struct ctok_stats {
   double ms_total;        /* wall time of the call (host clock)                        */
   double ms_device;       /* first kernel start -> last kernel end (HIP events)        */
   double ms_pretok;       /* normalise check + doc bitmap + pre-tokenizer/routing      */
-  double ms_bpe_short;    /* merge passes of pieces <= 64 bytes                          */
-  double ms_bpe_long;     /* wait for the long-piece pass (side stream) after them       */
+  double ms_bpe_short;    /* merge passes of pieces <= 64 bytes (k_segment's end -> the last one's end) */
+  double ms_bpe_long;     /* wait for the side stream (long-piece tiers) after them         */
   double ms_emit;         /* tile token scan + id emission + tok_off                   */
   double ms_h2d, ms_d2h;  /* host-buffer copies (ctok_encode_batch only)               */
   uint64_t bytes_in;      /* raw UTF-8 bytes of the batch                              */
   uint64_t bytes_norm;    /* bytes after normalisation / prefix space                  */
   uint64_t docs, pieces, long_pieces, tokens, nfc_docs;  /* nfc_docs: documents NFC-normalised (a superset
                                                           of those NFC changes: flagged per 64-byte word) */
-  double ms_segment;      /* k_segment alone: piece starts + whole-piece probes/routing */
-  double ms_bpe_lo;       /* k_bpe_short: pieces of <= 16 bytes (classes 0 and 1)        */
+  double ms_segment;      /* k_segment (from k_tilefirst's end): piece starts + probes/routing */
+  double ms_bpe_lo;       /* k_bpe_short (from k_segment's end): pieces of <= 16 bytes     */
   double ms_bpe_hi;       /* k_bpe_mid<2>: pieces of 17..32 bytes (on the side stream: the time it adds after k_bpe_short) */
   uint64_t class_bytes[4];  /* text bytes merged per length class (<= 8, 9..16, 17..32, 33..64 B) */
   uint64_t class_ids[4];    /* ids produced per length class                             */
-  double ms_bpe_med;      /* k_bpe_mid<3>, main-stream instance: pieces of 33..64 bytes    */
+  double ms_bpe_med;      /* 33..64-byte pieces (k_bpe_mid<3> main instance or k_bpe_sparse), after k_bpe_short */
   uint64_t workspace_bytes; /* device workspace held by the device for this tokenizer's calls */
   uint64_t long_rounds;     /* merge rounds of the long-piece wave tiers (<= 4096 B pieces), summed over pieces */
 } ctok_stats;

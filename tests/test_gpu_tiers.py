@@ -125,7 +125,7 @@ class _env:
 def test_c3_register_and_sparse_paths(gpt2, multi_path, bound):
     """The 33..64 B class by either implementation, against the C oracle: the register pass
     (k_bpe_mid<3>; CTOK_C3_SPARSE=0 or a bound below the class's size) and the sparse path
-    (k_c3_list + k_bpe_sparse: a wavefront per piece, taken when the class holds at most the
+    (k_bpe_sparse over k_segment's class-3 queue: a wavefront per piece, taken when the class holds at most the
     bound's pieces; 100000000 forces it on the multilingual sample's dense class 3)."""
     _, tok, rc = gpt2
     with open(multi_path) as f:
@@ -142,6 +142,30 @@ def test_c3_register_and_sparse_paths(gpt2, multi_path, bound):
         ref5 = check(mtok, mrc, c5 + tier_docs(6))
     # both implementations merge the same pieces into the same number of ids
     assert st5["class_bytes"][3] == ref5["class_bytes"][3] and st5["class_ids"][3] == ref5["class_ids"][3]
+
+
+@pytest.mark.parametrize("bound", ["default", "100000000"])
+def test_c3_sparse_queue_shards(gpt2, bound):
+    """k_segment's 64-shard class-3 queue (shard = tile % 64), against the C oracle.  Packed: 40
+    pieces of 33..64 B in one tile of a ~200 KB batch; under the default bound (one piece per 16
+    tiles, at least 64: capacity one piece per shard) that shard overflows and the report steers
+    the call to the register pass; at 10^8 the sparse pass takes them.  Spread: one such piece in
+    each of 12 tiles, taken by the sparse pass under either bound."""
+    _, tok, rc = gpt2
+    rng = random.Random(5)
+
+    def word(n):
+        return "".join(rng.choice("etaoinshrdlu") for _ in range(n))
+
+    # (~4.6 KB documents with no class-3 piece: one piece at each one's end lands in a tile of its
+    # own, 12 tiles, so in a shard of its own)
+    filler = [" ".join(word(rng.randint(2, 9)) for _ in range(700)) for _ in range(12)]
+    packed = [" ".join(word(rng.randint(33, 48)) for _ in range(40))] + filler
+    spread = [f + " " + word(rng.randint(33, 60)) for f in filler]
+    env = _env("CTOK_C3_SPARSE", bound) if bound != "default" else _env("CTOK_C3_SPARSE_UNUSED", "1")
+    with env:
+        assert check(tok, rc, packed)["class_ids"][3] > 0
+        assert check(tok, rc, spread)["class_ids"][3] > 0
 
 
 def test_c3_sparse_improper_and_wide_tables(gpt2, llama3_path):
