@@ -1869,16 +1869,15 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   //   8, 10 the 17..32 B pass | 9 the 33..64 B pass's end | 5 the dropped-byte pass start | 3 the
   //   tile scan start | 6 k_tokoff end
   const bool tm = timing && st && nt;  // (no tiles: no merge pass to time)
-  auto lx = [&](int a, int b, bool any_order) {
+  auto lx = [&](int a, int b) {
     Lx x;
-    x.any_order = any_order;
     if (tm && a >= 0) x.start = ds->ev[a];
     if (tm && b >= 0) x.stop = ds->ev[b];
     return x;
   };
   HP(1);
-  STEP("docstart", launch_docstart(w, s, !ctr_zeroed, lx(ev0_marker ? -1 : 0, -1, false), lx(-1, 7, false)));
-  STEP("segment", launch_segment(w, tb, s, lx(-1, 1, false)));
+  STEP("docstart", launch_docstart(w, s, !ctr_zeroed, lx(ev0_marker ? -1 : 0, -1), lx(-1, 7)));
+  STEP("segment", launch_segment(w, tb, s, lx(-1, 1)));
   if (segment_only) {  // pre-tokenization only (the trainer's word counting): pbits of the text
     HIPTRY(hipMemcpyAsync(ds->host + 1, ds->counters.p, kNumCounters * 4, hipMemcpyDeviceToHost, s));
     spin_sync(ds, s);
@@ -1895,7 +1894,7 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   // (k_bpe_short's first wave writes the report; without it -- added tokens, no tiles -- k_report)
   HP(2);
   if (tb.n_at != 0 || !nt) STEP("report", launch_report(w, s));
-  STEP("bpe_short", launch_bpe_class(w, tb, 0, s, lx(-1, 2, false)));
+  STEP("bpe_short", launch_bpe_class(w, tb, 0, s, lx(-1, 2)));
   HP(3);
   wait_report(s, seg_cnt, w.seq);
   HP(4);
@@ -1930,9 +1929,9 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
   const int overlap = ov_var ? atoi(ov_var) : kOverlapDefault;
   const bool mid_side = overlap >= 1 && seg_cnt[0] == 0;
   ds->last_mid_side = mid_side;
-  STEP("bpe_mid", launch_bpe_class(w, tb, 2, mid_side ? ds->side : s, lx(8, 10, false)));
-  if (c3_sparse) STEP("bpe_c3_sparse", launch_c3_sparse(w, tb, c3n, s, lx(-1, 9, false)));
-  else STEP("bpe_c3", launch_bpe_class(w, tb, 4, s, lx(-1, 9, false)));
+  STEP("bpe_mid", launch_bpe_class(w, tb, 2, mid_side ? ds->side : s, lx(8, 10)));
+  if (c3_sparse) STEP("bpe_c3_sparse", launch_c3_sparse(w, tb, c3n, s, lx(-1, 9)));
+  else STEP("bpe_c3", launch_bpe_class(w, tb, 4, s, lx(-1, 9)));
   if (!spec_fail1 && n_long) {
     for (;;) {  // the long pieces' totals (launch_long_prep above)
       const hipError_t e = hipEventQuery(ds->ev_tot);
@@ -1951,13 +1950,13 @@ uint64_t encode_device(ctok* t, DeviceState* ds, const uint8_t* d_text, const ui
     HIPTRY(hipStreamWaitEvent(s, ds->ev_join, 0));
   }
   const bool dropped_pass = tb.n_at == 0 && !tb.all_bytes;
-  STEP("bpe_dropped", launch_bpe_class(w, tb, 3, s, lx(5, -1, false)));
+  STEP("bpe_dropped", launch_bpe_class(w, tb, 3, s, lx(5, -1)));
   // the token count and the counters: written by k_tokoff straight into the pinned host words
   // (two copy launches fewer at the end of every call), or copied
   static const bool copy_res = getenv("CTOK_COPY_RESULTS") != nullptr;
   w.host_res = copy_res ? nullptr : ds->host_dev;
   STEP("emit", launch_emit(w, d_ids, ids_cap, d_tok_off, s, st != nullptr, seg_cnt[kCtrEmptyDocs] != 0,
-                           lx(3, -1, false), lx(-1, 6, false)));
+                           lx(3, -1), lx(-1, 6)));
   if (!w.host_res) {
     HIPTRY(hipMemcpyAsync(ds->host, d_tok_off + n_docs, 8, hipMemcpyDeviceToHost, s));
     HIPTRY(hipMemcpyAsync(ds->host + 1, ds->counters.p, kNumCounters * 4, hipMemcpyDeviceToHost, s));

@@ -294,12 +294,11 @@ struct Work {              // device pointers, sized by the host for one call
   uint32_t seq;            // this call's sequence number (nonzero)
 };
 
-// Launch options of one kernel (hipExtLaunchKernel): any_order -- its packet does not wait for the
-// stream's earlier kernels to end (measured: it starts when the previous kernel's first workgroup
-// retires; a start event on it cancels that); start / stop -- events the kernel's own dispatch
-// records (a timed call puts no marker packets between its kernels).
+// Launch options of one kernel: start / stop events its own dispatch records (hipExtLaunchKernel),
+// so a timed call puts no marker packets between its kernels.  (hipExtAnyOrderLaunch was measured
+// and left out: such a packet starts only when the previous kernel's first workgroup retires,
+// tools/anyorder_check.hip.)
 struct Lx {
-  bool any_order = false;
   hipEvent_t start = nullptr, stop = nullptr;
 };
 

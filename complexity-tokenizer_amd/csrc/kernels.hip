@@ -36,13 +36,12 @@ namespace ctok_dev {
 
 #define HIPCHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) return e_; } while (0)
 
-// A kernel launch with Lx's options (any-order packet, start / stop events of its own dispatch)
-// through hipExtLaunchKernel, or a plain launch when it has none.
+// A kernel launch with Lx's start / stop events (recorded by its own dispatch) through
+// hipExtLaunchKernel, or a plain launch when it has none.
 template <typename F, typename... A>
 static void launch_lx(const Lx& x, F k, dim3 grid, dim3 block, uint32_t lds, hipStream_t s, A... a) {
-  if (x.any_order || x.start || x.stop)
-    hipExtLaunchKernelGGL(k, grid, block, lds, s, x.start, x.stop, x.any_order ? (uint32_t)hipExtAnyOrderLaunch : 0u,
-                          a...);
+  if (x.start || x.stop)
+    hipExtLaunchKernelGGL(k, grid, block, lds, s, x.start, x.stop, 0u, a...);
   else
     hipLaunchKernelGGL(k, grid, block, lds, s, a...);
 }
